@@ -1,0 +1,713 @@
+/*
+ * amodem_oracle.c — CPU restatement of the playok/audio-modem receive path
+ * (and, for synthetic inputs only, its transmit path).
+ *
+ * TEST INFRASTRUCTURE / CPU BASELINE ONLY — see amodem_oracle.h. The product
+ * (audio-modem_amd/) never links this file.
+ *
+ * Arithmetic is IEEE double in the same order as modem.js; build with
+ * -ffp-contract=off so no fused multiply-add changes a rounding.
+ */
+#define _GNU_SOURCE
+#include "amodem_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------ config --- */
+/* OFDM_CONFIGS presets, modem.js:69-85 */
+void orc_config(const char *name, orc_cfg *o) {
+  static const int std_p[] = {15, 29, 43, 57, 71, 85, 99, 113, 127, 141, 155, 169, 183, 197, 211, 225};
+  static const int ac_p[] = {25, 35, 45, 55, 65, 75, 85};
+  static const int nb_p[] = {37, 45, 53};
+  memset(o, 0, sizeof *o);
+  o->fft_size = 512;
+  o->sample_rate = 44100;
+  const int *p;
+  int np;
+  if (name && strcmp(name, "acoustic") == 0) {
+    o->cp_len = 128; o->sub_start = 23; o->sub_end = 93; p = ac_p; np = 7;
+  } else if (name && strcmp(name, "narrowband") == 0) {
+    o->cp_len = 256; o->sub_start = 35; o->sub_end = 58; p = nb_p; np = 3;
+  } else { /* setOFDMConfig falls back to standard for unknown names (modem.js:96) */
+    o->cp_len = 64; o->sub_start = 12; o->sub_end = 232; p = std_p; np = 16;
+  }
+  o->symbol_len = o->fft_size + o->cp_len;
+  o->npilots = np;
+  for (int i = 0; i < np; i++) o->pilots[i] = p[i];
+}
+
+static int is_pilot(const orc_cfg *c, int k) { /* OFDM.isPilot, modem.js:88 */
+  for (int i = 0; i < c->npilots; i++)
+    if (c->pilots[i] == k) return 1;
+  return 0;
+}
+
+int orc_num_data_subs(const orc_cfg *c) { /* modem.js:89-93 */
+  int n = 0;
+  for (int k = c->sub_start; k <= c->sub_end; k++) n += !is_pilot(c, k);
+  return n;
+}
+
+int orc_bps(int mod) { return mod == ORC_BPSK ? 1 : mod == ORC_QPSK ? 2 : 4; }
+
+/* --------------------------------------------------------------- FFT --- */
+/* Radix-2 DIT with per-stage twiddle recurrence, modem.js:26-47 / 49-66. */
+void orc_fft(double *re, double *im, int n, int inverse) {
+  int bits = 0;
+  for (int t = n; t > 1; t >>= 1) bits++;
+  for (int i = 0; i < n; i++) {
+    int j = 0, x = i;
+    for (int b = 0; b < bits; b++) { j = (j << 1) | (x & 1); x >>= 1; }
+    if (i < j) {
+      double t = re[i]; re[i] = re[j]; re[j] = t;
+      t = im[i]; im[i] = im[j]; im[j] = t;
+    }
+  }
+  for (int size = 2; size <= n; size <<= 1) {
+    const int half = size >> 1;
+    const double sign = inverse ? 1.0 : -1.0;
+    const double angle = sign * 2.0 * M_PI / (double)size;
+    const double wn_re = cos(angle), wn_im = sin(angle);
+    for (int start = 0; start < n; start += size) {
+      double w_re = 1.0, w_im = 0.0;
+      for (int j = 0; j < half; j++) {
+        const int a = start + j, b = a + half;
+        const double t_re = w_re * re[b] - w_im * im[b];
+        const double t_im = w_re * im[b] + w_im * re[b];
+        re[b] = re[a] - t_re; im[b] = im[a] - t_im;
+        re[a] += t_re; im[a] += t_im;
+        const double nw = w_re * wn_re - w_im * wn_im;
+        w_im = w_re * wn_im + w_im * wn_re;
+        w_re = nw;
+      }
+    }
+  }
+  if (inverse) { /* ifft, modem.js:21-22 */
+    const double scale = 1.0 / (double)n;
+    for (int i = 0; i < n; i++) { re[i] *= scale; im[i] *= scale; }
+  }
+}
+
+/* ------------------------------------------------------ templates --- */
+/* seededRandom: product and sum in double, then ToInt32 & 0x7fffffff (modem.js:153-156) */
+double orc_seeded_next(double *state) {
+  const double prod = *state * 1103515245.0;
+  const double sum = prod + 12345.0;
+  const uint64_t as_int = (uint64_t)fmod(sum, 18446744073709551616.0);
+  const uint32_t low = (uint32_t)as_int & 0x7fffffffu;
+  *state = (double)low;
+  return (double)low / 2147483647.0;
+}
+
+static void to_f32_with_cp(const orc_cfg *c, const double *td, float *out) { /* addCP 202-208 */
+  const int n = c->fft_size, cp = c->cp_len;
+  for (int i = 0; i < cp; i++) out[i] = (float)td[n - cp + i];
+  for (int i = 0; i < n; i++) out[cp + i] = (float)td[i];
+}
+
+static void hermitian_ifft_cp(const orc_cfg *c, double *re, double *im, float *out) {
+  const int n = c->fft_size;
+  for (int k = 1; k < n / 2; k++) { re[n - k] = re[k]; im[n - k] = -im[k]; }
+  re[0] = 0; re[n / 2] = 0; im[n / 2] = 0;
+  orc_fft(re, im, n, 1);
+  to_f32_with_cp(c, re, out);
+}
+
+static void random_symbol(const orc_cfg *c, double seed, int step, float *out, double *known) {
+  const int n = c->fft_size;
+  double *re = calloc((size_t)n, sizeof(double)), *im = calloc((size_t)n, sizeof(double));
+  double st = seed;
+  for (int k = c->sub_start; k <= c->sub_end; k += step) {
+    re[k] = orc_seeded_next(&st) > 0.5 ? 1.0 : -1.0;
+    if (known) known[k] = re[k];
+  }
+  hermitian_ifft_cp(c, re, im, out);
+  free(re); free(im);
+}
+
+void orc_preamble1(const orc_cfg *c, float *out) { random_symbol(c, 42.0, 2, out, NULL); }
+void orc_preamble2(const orc_cfg *c, float *out) { random_symbol(c, 43.0, 1, out, NULL); }
+void orc_ce_symbol(const orc_cfg *c, float *out, double *known_re) {
+  if (known_re) memset(known_re, 0, sizeof(double) * (size_t)c->fft_size);
+  random_symbol(c, 44.0, 1, out, known_re);
+}
+
+/* ----------------------------------------------------- constellation --- */
+void orc_const_point(int mod, int idx, double *re, double *im) { /* modem.js:107-131 */
+  if (mod == ORC_BPSK) { *re = idx == 0 ? 1.0 : -1.0; *im = 0.0; return; }
+  if (mod == ORC_QPSK) {
+    const double s = 1.0 / M_SQRT2;
+    static const int sr[4] = {1, -1, -1, 1}, si[4] = {1, 1, -1, -1};
+    *re = sr[idx] * s; *im = si[idx] * s;
+    return;
+  }
+  const int row = idx >> 2, col = idx & 3;
+  const int gr = row ^ (row >> 1), gc = col ^ (col >> 1);
+  const double s = 1.0 / sqrt(10.0); /* mean |p|^2 of the raw 16 points is exactly 10 */
+  *re = (double)(2 * gc - 3) * s; *im = (double)(2 * gr - 3) * s;
+}
+
+int orc_demap(int mod, double re, double im) { /* first strict minimum, modem.js:140-150 */
+  const int np = mod == ORC_BPSK ? 2 : mod == ORC_QPSK ? 4 : 16;
+  double best = INFINITY;
+  int bi = 0;
+  for (int i = 0; i < np; i++) {
+    double pr, pi;
+    orc_const_point(mod, i, &pr, &pi);
+    const double dr = re - pr, di = im - pi;
+    const double d = dr * dr + di * di;
+    if (d < best) { best = d; bi = i; }
+  }
+  return bi;
+}
+
+/* ------------------------------------------------------------ CRC ---- */
+uint32_t orc_crc32(const uint8_t *d, size_t n) { /* modem.js:443-457 */
+  static uint32_t table[256];
+  static int init = 0;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int j = 0; j < 8; j++) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+      table[i] = c;
+    }
+    __atomic_store_n(&init, 1, __ATOMIC_RELEASE);
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = table[(c ^ d[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+int orc_majority(const uint8_t *bits, int nbits, int n, uint8_t *out) { /* 487-495 */
+  int m = 0;
+  for (int i = 0; i + n - 1 < nbits; i += n) {
+    int sum = 0;
+    for (int j = 0; j < n; j++) sum += bits[i + j];
+    out[m++] = (double)sum >= (double)n / 2.0 ? 1 : 0;
+  }
+  return m;
+}
+
+int orc_bits_to_bytes(const uint8_t *bits, int nbits, uint8_t *out) { /* 468-476 */
+  int m = 0;
+  for (int i = 0; i + 7 < nbits; i += 8) {
+    int b = 0;
+    for (int j = 0; j < 8; j++) b = (b << 1) | (bits[i + j] & 1);
+    out[m++] = (uint8_t)b;
+  }
+  return m;
+}
+
+int orc_estimate_frame_samples(const orc_cfg *c, int payload, int mod, int rep) { /* 863-874 */
+  if (rep < 1) rep = 1;
+  const int bps_sym = orc_num_data_subs(c) * orc_bps(mod);
+  const double total = (double)payload * 8.0 * (double)rep;
+  const int nsym = (int)ceil(total / (double)bps_sym);
+  return (3 + nsym) * c->symbol_len;
+}
+
+/* ------------------------------------------------------------- RX ---- */
+static double js_max(double a, double b) { /* Math.max: NaN-propagating */
+  if (isnan(a) || isnan(b)) return NAN;
+  return b > a ? b : a;
+}
+
+void orc_preprocess(const float *x, int n, float *out, double *mean_o, double *mx_o) { /* 213-232 */
+  double mean = 0.0;
+  for (int i = 0; i < n; i++) mean += (double)x[i];
+  mean /= (double)n;
+  double mx = 0.0;
+  for (int i = 0; i < n; i++) {
+    out[i] = (float)((double)x[i] - mean);
+    mx = js_max(mx, fabs((double)out[i]));
+  }
+  if (mx > 1e-6)
+    for (int i = 0; i < n; i++) out[i] = (float)((double)out[i] / mx);
+  if (mean_o) *mean_o = mean;
+  if (mx_o) *mx_o = mx;
+}
+
+int orc_detect_preamble(const float *s, int n, const orc_cfg *c) { /* 286-319 */
+  const int half = c->fft_size / 2;
+  if (n < 2 * half) return -1;
+  double p = 0, ra = 0, rb = 0;
+  for (int m = 0; m < half; m++) {
+    const double a = s[m], b = s[m + half];
+    p += a * b; ra += a * a; rb += b * b;
+  }
+  double best = 0;
+  int best_idx = -1;
+  const int end = n - 2 * half;
+  for (int d = 0; d <= end; d++) {
+    if (ra > 0.01 && rb > 0.01) {
+      const double metric = (p * p) / (ra * rb);
+      if (metric > best) { best = metric; best_idx = d; }
+    }
+    if (d < end) {
+      const double a_out = s[d], mid = s[d + half], b_in = s[d + 2 * half];
+      p += mid * b_in - a_out * mid;
+      ra += mid * mid - a_out * a_out;
+      rb += b_in * b_in - mid * mid;
+    }
+  }
+  return best > 0.5 ? best_idx : -1;
+}
+
+int orc_fine_timing(const float *s, int n, const orc_cfg *c, int coarse, double *best_o) { /* 567-588 */
+  const int plen = c->symbol_len;
+  float *pre1 = malloc(sizeof(float) * (size_t)plen);
+  orc_preamble1(c, pre1);
+  double te = 0;
+  for (int i = 0; i < plen; i++) te += (double)pre1[i] * (double)pre1[i];
+  const int radius = c->cp_len * 3;
+  const int lo = coarse - radius > 0 ? coarse - radius : 0;
+  const int hi = n - plen < coarse + radius ? n - plen : coarse + radius;
+  double best = -INFINITY;
+  int start = coarse;
+  for (int d = lo; d <= hi; d++) {
+    double corr = 0, se = 0;
+    for (int i = 0; i < plen; i++) {
+      corr += (double)s[d + i] * (double)pre1[i];
+      se += (double)s[d + i] * (double)s[d + i];
+    }
+    const double den = sqrt(se * te);
+    if (den > 0.001) {
+      const double m = corr / den;
+      if (m > best) { best = m; start = d; }
+    }
+  }
+  free(pre1);
+  *best_o = best;
+  return start;
+}
+
+static double or_zero(float v) { return (v != v || v == 0.0f) ? 0.0 : (double)v; } /* `x || 0` */
+
+void orc_estimate_channel(const float *ce, const orc_cfg *c, double *h_re, double *h_im) { /* 421-440 */
+  const int n = c->fft_size;
+  double *re = calloc((size_t)n, sizeof(double)), *im = calloc((size_t)n, sizeof(double));
+  double *known = calloc((size_t)n, sizeof(double));
+  float *tmp = malloc(sizeof(float) * (size_t)c->symbol_len);
+  orc_ce_symbol(c, tmp, known);
+  for (int i = 0; i < n; i++) re[i] = or_zero(ce[c->cp_len + i]);
+  orc_fft(re, im, n, 0);
+  for (int k = 0; k < n; k++) { h_re[k] = 0; h_im[k] = 0; }
+  for (int k = c->sub_start; k <= c->sub_end; k++) {
+    const double xr = known[k], xi = 0.0;
+    const double d = xr * xr + xi * xi;
+    if (d > 1e-10) {
+      h_re[k] = (re[k] * xr + im[k] * xi) / d;
+      h_im[k] = (im[k] * xr - re[k] * xi) / d;
+    }
+  }
+  free(re); free(im); free(known); free(tmp);
+}
+
+void orc_symbol_detail(const float *data, int len, int s, const orc_cfg *c, const double *h_re,
+                       const double *h_im, double *x_re, double *x_im, double *eq_re, double *eq_im,
+                       double *phase) { /* one iteration of the loop at modem.js:371-406 */
+  const int n = c->fft_size, off = s * c->symbol_len;
+  (void)len;
+  for (int i = 0; i < n; i++) { x_re[i] = or_zero(data[off + c->cp_len + i]); x_im[i] = 0; }
+  orc_fft(x_re, x_im, n, 0);
+  for (int k = 0; k < n; k++) { eq_re[k] = 0; eq_im[k] = 0; }
+  for (int k = c->sub_start; k <= c->sub_end; k++) {
+    const double hr = h_re[k], hi = h_im[k];
+    const double mag = hr * hr + hi * hi;
+    if (mag > 1e-10) {
+      eq_re[k] = (x_re[k] * hr + x_im[k] * hi) / mag;
+      eq_im[k] = (x_im[k] * hr - x_re[k] * hi) / mag;
+    } else {
+      eq_re[k] = x_re[k]; eq_im[k] = x_im[k];
+    }
+  }
+  double sum = 0;
+  int cnt = 0;
+  for (int i = 0; i < c->npilots; i++) {
+    const int p = c->pilots[i];
+    if (p >= c->sub_start && p <= c->sub_end && fabs(eq_re[p]) > 1e-6) { sum += eq_im[p] / eq_re[p]; cnt++; }
+  }
+  *phase = cnt > 0 ? sum / (double)cnt : 0.0;
+}
+
+int orc_demodulate(const float *data, int len, const orc_cfg *c, int mod, const double *h_re,
+                   const double *h_im, uint8_t *bits) { /* 365-418 */
+  const int n = c->fft_size, bps = orc_bps(mod);
+  const int nsym = len / c->symbol_len;
+  double *xr = malloc(sizeof(double) * 4 * (size_t)n);
+  double *xi = xr + n, *er = xi + n, *ei = er + n;
+  int nb = 0;
+  for (int s = 0; s < nsym; s++) {
+    double ph;
+    orc_symbol_detail(data, len, s, c, h_re, h_im, xr, xi, er, ei, &ph);
+    for (int k = c->sub_start; k <= c->sub_end; k++) {
+      if (is_pilot(c, k)) continue;
+      const double cr = er[k] + ei[k] * ph;
+      const double ci = ei[k] - er[k] * ph;
+      const int idx = orc_demap(mod, cr, ci);
+      for (int b = bps - 1; b >= 0; b--) bits[nb++] = (uint8_t)((idx >> b) & 1);
+    }
+  }
+  free(xr);
+  return nb;
+}
+
+static int32_t be32(const uint8_t *b) { /* (b0<<24)|(b1<<16)|(b2<<8)|b3 as int32 */
+  return (int32_t)(((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]);
+}
+
+void orc_parse_bytes(const uint8_t *b, int nb, int legacy_allowed, orc_result *r) {
+  r->nbytes = nb;
+  const int t = nb > 0 ? b[0] : -1;
+  if (t == 0xFE) { /* parseMetadataResult, modem.js:805-828 */
+    r->frame_type = 0xFE;
+    if (nb < 16) { r->status = ORC_E_META_SHORT; return; }
+    int off = 1;
+    r->total_chunks = be32(b + off); off += 4;
+    r->total_size = be32(b + off); off += 4;
+    r->chunk_size = (b[off] << 8) | b[off + 1]; off += 2;
+    const int name_len = b[off++];
+    if (off + name_len + 4 > nb) { r->status = ORC_E_META_TRUNC; return; }
+    r->name_off = off; r->name_len = name_len;
+    off += name_len;
+    r->expected_crc = (uint32_t)be32(b + off);
+    r->actual_crc = orc_crc32(b, (size_t)off);
+    r->crc_valid = r->expected_crc == r->actual_crc;
+    r->status = ORC_OK;
+    return;
+  }
+  if (t == 0xFF) { /* parseDataChunkResult, modem.js:830-849 */
+    r->frame_type = 0xFF;
+    if (nb < 11) { r->status = ORC_E_CHUNK_SHORT; return; }
+    int off = 1;
+    r->seq_num = be32(b + off); off += 4;
+    const int dlen = (b[off] << 8) | b[off + 1]; off += 2;
+    if (off + dlen + 4 > nb) { r->status = ORC_E_CHUNK_TRUNC; return; }
+    r->data_off = off; r->data_len = dlen;
+    off += dlen;
+    r->expected_crc = (uint32_t)be32(b + off);
+    r->actual_crc = orc_crc32(b, (size_t)off);
+    r->crc_valid = r->expected_crc == r->actual_crc;
+    r->status = ORC_OK;
+    return;
+  }
+  if (!legacy_allowed) { /* decodeChunkFrame, modem.js:800-802 */
+    r->frame_type = t;
+    r->aux = t;
+    r->status = ORC_E_UNKNOWN_TYPE;
+    return;
+  }
+  /* legacy packet, modem.js:622-653 */
+  r->frame_type = 0;
+  int off = 0;
+  const int name_len = b[off++];
+  if (off + name_len + 4 + 4 > nb) { r->status = ORC_E_SHORT_HEADER; return; }
+  r->name_off = off; r->name_len = name_len;
+  off += name_len;
+  const int32_t dlen = be32(b + off);
+  off += 4;
+  if (dlen <= 0 || (int64_t)off + dlen + 4 > nb) { r->status = ORC_E_INVALID_LEN; r->aux = dlen; return; }
+  r->data_off = off; r->data_len = dlen;
+  off += dlen;
+  r->expected_crc = (uint32_t)be32(b + off);
+  r->actual_crc = orc_crc32(b, (size_t)off);
+  r->crc_valid = r->expected_crc == r->actual_crc;
+  r->status = ORC_OK;
+}
+
+static void result_init(orc_result *r) {
+  memset(r, 0, sizeof *r);
+  r->preamble_idx = -1;
+  r->coarse_idx = -1;
+  r->frame_type = -1;
+  r->fine_metric = NAN;
+}
+
+/* demod + vote + pack the data region; returns byte count and fills out */
+static int demod_to_bytes(const float *data, int len, const orc_cfg *c, int mod, int rep,
+                          const double *h_re, const double *h_im, uint8_t **bytes_o, int *nbits_o) {
+  const int nsym = len / c->symbol_len;
+  const size_t max_bits = (size_t)nsym * (size_t)orc_num_data_subs(c) * (size_t)orc_bps(mod) + 1;
+  uint8_t *bits = malloc(max_bits);
+  int nb = orc_demodulate(data, len, c, mod, h_re, h_im, bits);
+  *nbits_o = nb;
+  if (rep > 1) nb = orc_majority(bits, nb, rep, bits); /* in place: output index <= input index */
+  uint8_t *bytes = malloc((size_t)nb / 8 + 1);
+  const int nbytes = orc_bits_to_bytes(bits, nb, bytes);
+  free(bits);
+  *bytes_o = bytes;
+  return nbytes;
+}
+
+static void copy_out(const uint8_t *bytes, int nb, uint8_t *out, int cap) {
+  if (out && cap > 0) memcpy(out, bytes, (size_t)(nb < cap ? nb : cap));
+}
+
+int orc_decode_received(const orc_cfg *c, const float *x, int n, int mod, int rep, orc_result *r,
+                        uint8_t *bytes_out, int bytes_cap) { /* decodeReceivedSignal, 557-654 */
+  result_init(r);
+  if (rep < 1) rep = 1;
+  float *sig = malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+  orc_preprocess(x, n, sig, NULL, NULL);
+  const int coarse = orc_detect_preamble(sig, n, c);
+  r->coarse_idx = coarse;
+  if (coarse < 0) { r->status = ORC_E_PREAMBLE; free(sig); return r->status; }
+  double best;
+  const int start = orc_fine_timing(sig, n, c, coarse, &best);
+  r->fine_metric = best;
+  if (best < 0.1) { r->status = ORC_E_LOW_CORR; free(sig); return r->status; }
+  const int ce_start = start + 2 * c->symbol_len;
+  if (ce_start + c->symbol_len > n) { r->status = ORC_E_SHORT_CE; free(sig); return r->status; }
+  double *h = malloc(sizeof(double) * 2 * (size_t)c->fft_size);
+  orc_estimate_channel(sig + ce_start, c, h, h + c->fft_size);
+  const int data_start = ce_start + c->symbol_len;
+  if (data_start >= n) { r->status = ORC_E_NO_DATA; free(h); free(sig); return r->status; }
+  uint8_t *bytes;
+  const int nb = demod_to_bytes(sig + data_start, n - data_start, c, mod, rep, h, h + c->fft_size, &bytes, &r->nbits);
+  free(h); free(sig);
+  r->nbytes = nb;
+  copy_out(bytes, nb, bytes_out, bytes_cap);
+  if (nb < 10) { r->status = ORC_E_DECODED_SHORT; free(bytes); return r->status; }
+  orc_parse_bytes(bytes, nb, 1, r);
+  r->preamble_idx = start; /* set on 0xFE/0xFF results even when they are errors (612-619) */
+  if (r->frame_type == 0 && r->status != ORC_OK) r->preamble_idx = -1; /* legacy errors carry no idx */
+  free(bytes);
+  return r->status;
+}
+
+int orc_decode_chunk(const orc_cfg *c, const float *x, int n, int mod, int rep, orc_result *r,
+                     uint8_t *bytes_out, int bytes_cap) { /* decodeChunkFrame, 770-803 */
+  result_init(r);
+  if (rep < 1) rep = 1;
+  const int ce_start = 2 * c->symbol_len;
+  if (ce_start + c->symbol_len > n) { r->status = ORC_E_FRAME_SHORT_CE; return r->status; }
+  double *h = malloc(sizeof(double) * 2 * (size_t)c->fft_size);
+  orc_estimate_channel(x + ce_start, c, h, h + c->fft_size);
+  const int data_start = ce_start + c->symbol_len;
+  if (data_start >= n) { r->status = ORC_E_NO_DATA; free(h); return r->status; }
+  uint8_t *bytes;
+  const int nb = demod_to_bytes(x + data_start, n - data_start, c, mod, rep, h, h + c->fft_size, &bytes, &r->nbits);
+  free(h);
+  r->nbytes = nb;
+  copy_out(bytes, nb, bytes_out, bytes_cap);
+  if (nb < 6) { r->status = ORC_E_DECODED_SHORT; free(bytes); return r->status; }
+  orc_parse_bytes(bytes, nb, 0, r);
+  free(bytes);
+  return r->status;
+}
+
+/* ------------------------------------------------------------- TX ---- */
+/* modulateOFDM, modem.js:322-362: appends nsym symbols of SYMBOL_LEN floats to out */
+static int modulate(const orc_cfg *c, const uint8_t *bits_in, int nbits, int mod, float *out) {
+  const int bps = orc_bps(mod), n = c->fft_size;
+  const int per_sym = orc_num_data_subs(c) * bps;
+  const int nsym = (nbits + per_sym - 1) / per_sym;
+  if (!out) return nsym;
+  const int np = mod == ORC_BPSK ? 2 : mod == ORC_QPSK ? 4 : 16;
+  double *re = malloc(sizeof(double) * 2 * (size_t)n), *im = re + n;
+  for (int s = 0; s < nsym; s++) {
+    memset(re, 0, sizeof(double) * 2 * (size_t)n);
+    int di = 0;
+    for (int k = c->sub_start; k <= c->sub_end; k++) {
+      if (is_pilot(c, k)) { re[k] = 1; im[k] = 0; continue; }
+      int idx = 0;
+      for (int b = 0; b < bps; b++) {
+        const int bit_pos = s * per_sym + di * bps + b;
+        idx = (idx << 1) | (bit_pos < nbits ? (bits_in[bit_pos] & 1) : 0); /* zero padding (329) */
+      }
+      orc_const_point(mod, idx % np, &re[k], &im[k]);
+      di++;
+    }
+    for (int k = 1; k < n / 2; k++) { re[n - k] = re[k]; im[n - k] = -im[k]; }
+    re[0] = 0; im[0] = 0; im[n / 2] = 0;
+    orc_fft(re, im, n, 1);
+    to_f32_with_cp(c, re, out + (size_t)s * c->symbol_len);
+  }
+  free(re);
+  return nsym;
+}
+
+/* bytesToBits + repeatBits (modem.js:460-485) */
+static uint8_t *payload_bits(const uint8_t *p, int len, int rep, int *nbits) {
+  if (rep < 1) rep = 1;
+  uint8_t *bits = malloc((size_t)len * 8 * (size_t)rep + 1);
+  int m = 0;
+  for (int i = 0; i < len; i++)
+    for (int b = 7; b >= 0; b--)
+      for (int r = 0; r < rep; r++) bits[m++] = (p[i] >> b) & 1;
+  *nbits = m;
+  return bits;
+}
+
+/* assemble silence + pre1 + pre2 + CE + data + silence and normalise to 0.8 peak */
+static int assemble(const orc_cfg *c, const uint8_t *payload, int plen, int mod, int rep, int pre,
+                    int post, float *out) {
+  int nbits;
+  uint8_t *bits = payload_bits(payload, plen, rep, &nbits);
+  const int nsym = modulate(c, bits, nbits, mod, NULL);
+  const int sl = c->symbol_len;
+  const int total = pre + 3 * sl + nsym * sl + post;
+  if (!out) { free(bits); return total; }
+  memset(out, 0, sizeof(float) * (size_t)total);
+  orc_preamble1(c, out + pre);
+  orc_preamble2(c, out + pre + sl);
+  orc_ce_symbol(c, out + pre + 2 * sl, NULL);
+  modulate(c, bits, nbits, mod, out + pre + 3 * sl);
+  free(bits);
+  double mx = 0;
+  for (int i = 0; i < total; i++) mx = js_max(mx, fabs((double)out[i]));
+  if (mx > 0) {
+    const double s = 0.8 / mx;
+    for (int i = 0; i < total; i++) out[i] = (float)((double)out[i] * s);
+  }
+  return total;
+}
+
+static void put_be32(uint8_t *b, int32_t v) {
+  b[0] = (uint8_t)((v >> 24) & 0xFF); b[1] = (uint8_t)((v >> 16) & 0xFF);
+  b[2] = (uint8_t)((v >> 8) & 0xFF); b[3] = (uint8_t)(v & 0xFF);
+}
+
+int orc_build_legacy(const orc_cfg *c, const uint8_t *data, int len, const uint8_t *name, int name_len,
+                     int mod, int rep, float *out) { /* buildTransmitSignal, 498-555 */
+  if (name_len > 255) name_len = 255;
+  const int psize = 1 + name_len + 4 + len + 4;
+  uint8_t *p = malloc((size_t)psize);
+  int off = 0;
+  p[off++] = (uint8_t)name_len;
+  memcpy(p + off, name, (size_t)name_len); off += name_len;
+  put_be32(p + off, len); off += 4;
+  memcpy(p + off, data, (size_t)len); off += len;
+  put_be32(p + off, (int32_t)orc_crc32(p, (size_t)off));
+  const int ac = c->cp_len >= 128;
+  const int pre = (int)((double)c->sample_rate * (ac ? 0.5 : 0.3));
+  const int post = (int)((double)c->sample_rate * (ac ? 0.5 : 0.2));
+  const int n = assemble(c, p, psize, mod, rep, pre, post, out);
+  free(p);
+  return n;
+}
+
+static int chunk_frame(const orc_cfg *c, const uint8_t *p, int plen, int mod, int rep, int first, float *out) {
+  const int ac = c->cp_len >= 128;
+  const int pre = first ? (int)floor((double)c->sample_rate * (ac ? 0.5 : 0.3) + 0.5)
+                        : (int)floor((double)c->sample_rate * 0.05 + 0.5);
+  const int post = (int)floor((double)c->sample_rate * 0.02 + 0.5);
+  return assemble(c, p, plen, mod, rep, pre, post, out); /* buildChunkOFDMFrame, 718-756 */
+}
+
+int orc_build_meta(const orc_cfg *c, int total_chunks, int total_size, int chunk_size,
+                   const uint8_t *name, int name_len, int mod, int rep, float *out) {
+  if (name_len > 255) name_len = 255;
+  const int size = 1 + 4 + 4 + 2 + 1 + name_len + 4;
+  uint8_t *p = malloc((size_t)size);
+  int off = 0;
+  p[off++] = 0xFE;
+  put_be32(p + off, total_chunks); off += 4;
+  put_be32(p + off, total_size); off += 4;
+  p[off++] = (uint8_t)((chunk_size >> 8) & 0xFF);
+  p[off++] = (uint8_t)(chunk_size & 0xFF);
+  p[off++] = (uint8_t)name_len;
+  memcpy(p + off, name, (size_t)name_len); off += name_len;
+  put_be32(p + off, (int32_t)orc_crc32(p, (size_t)off));
+  const int n = chunk_frame(c, p, size, mod, rep, 1, out);
+  free(p);
+  return n;
+}
+
+int orc_build_chunk(const orc_cfg *c, const uint8_t *data, int len, int seq, int mod, int rep, float *out) {
+  const int size = 1 + 4 + 2 + len + 4;
+  uint8_t *p = malloc((size_t)size);
+  int off = 0;
+  p[off++] = 0xFF;
+  put_be32(p + off, seq); off += 4;
+  p[off++] = (uint8_t)((len >> 8) & 0xFF);
+  p[off++] = (uint8_t)(len & 0xFF);
+  memcpy(p + off, data, (size_t)len); off += len;
+  put_be32(p + off, (int32_t)orc_crc32(p, (size_t)off));
+  const int n = chunk_frame(c, p, size, mod, rep, 0, out);
+  free(p);
+  return n;
+}
+
+int orc_build_test_signal(const orc_cfg *c, int mod, int rep, float *out) { /* 914-973 */
+  uint8_t data[16];
+  for (int i = 0; i < 16; i++) data[i] = (uint8_t)i;
+  return orc_build_legacy(c, data, 16, (const uint8_t *)"test", 4, mod, rep, out);
+}
+
+/* ---------------------------------------------------------- recipes --- */
+uint32_t orc_xs32(uint32_t s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return s;
+}
+
+void orc_payload(uint32_t seed, int len, uint8_t *out) {
+  uint32_t s = seed;
+  for (int i = 0; i < len; i++) {
+    if ((i & 3) == 0) s = orc_xs32(s);
+    out[i] = (uint8_t)((s >> (8 * (i & 3))) & 0xFF);
+  }
+}
+
+void orc_add_noise(const float *in, int n, int snr_db, uint32_t seed, float *out) {
+  double p = 0;
+  int cnt = 0;
+  for (int i = 0; i < n; i++)
+    if (in[i] != 0.0f) { p += (double)in[i] * (double)in[i]; cnt++; }
+  p = cnt > 0 ? p / (double)cnt : 0.0;
+  double div = 1;
+  for (int k = 0; k < snr_db / 10; k++) div *= 10;
+  const double sigma = sqrt(p / div);
+  uint32_t s = seed;
+  for (int i = 0; i < n; i++) {
+    double g = 0;
+    for (int j = 0; j < 12; j++) { s = orc_xs32(s); g += (double)s / 4294967296.0; }
+    g -= 6;
+    out[i] = (float)((double)in[i] + sigma * g);
+  }
+}
+
+/* ------------------------------------------------------ CPU baseline --- */
+typedef struct {
+  const orc_cfg *c;
+  const float *x;
+  const int64_t *off;
+  const int32_t *len;
+  int nframes, mod, rep, tid, nthreads;
+  int32_t *status;
+  uint32_t *crc;
+} bench_job;
+
+static void *bench_worker(void *arg) {
+  bench_job *j = arg;
+  for (int f = j->tid; f < j->nframes; f += j->nthreads) {
+    orc_result r;
+    orc_decode_received(j->c, j->x + j->off[f], j->len[f], j->mod, j->rep, &r, NULL, 0);
+    if (j->status) j->status[f] = r.status;
+    if (j->crc) j->crc[f] = r.actual_crc;
+  }
+  return NULL;
+}
+
+double orc_bench_decode(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
+                        int nframes, int mod, int rep, int threads, int32_t *status_out, uint32_t *crc_out) {
+  if (threads < 1) threads = 1;
+  pthread_t *th = malloc(sizeof(pthread_t) * (size_t)threads);
+  bench_job *jobs = malloc(sizeof(bench_job) * (size_t)threads);
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (bench_job){c, x, off, len, nframes, mod, rep, t, threads, status_out, crc_out};
+    pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  free(th); free(jobs);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
