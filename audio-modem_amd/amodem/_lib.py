@@ -1,0 +1,120 @@
+"""ctypes binding of libamodem.so (include/amodem.h).
+
+This is the host plumbing the tests and bench.py use to drive the HIP product;
+the JavaScript surface (audio-modem_amd/js/modem.js) binds the same C ABI through
+N-API. There is no CPU fallback: if the library is missing this import fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(HERE), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libamodem.so")
+
+MAX_PILOTS = 32
+BPSK, QPSK, QAM16 = 0, 1, 2
+MODS = {"BPSK": BPSK, "QPSK": QPSK, "QAM16": QAM16}
+MODE_RECEIVED, MODE_CHUNK = 0, 1
+OPT_FORCE_EXACT = 1
+
+OK = 0
+E_CAPACITY = 100
+FLAG_EXACT = 1 << 15
+
+
+class Cfg(C.Structure):
+    _fields_ = [("fft_size", C.c_int32), ("cp_len", C.c_int32), ("symbol_len", C.c_int32),
+                ("sample_rate", C.c_int32), ("sub_start", C.c_int32), ("sub_end", C.c_int32),
+                ("npilots", C.c_int32), ("pilots", C.c_int32 * MAX_PILOTS),
+                ("modulation", C.c_int32), ("repetition", C.c_int32)]
+
+
+class Result(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("status", "preamble_idx", "coarse_idx", "frame_type", "aux", "nbytes",
+                                          "name_off", "name_len", "data_off", "data_len", "seq_num",
+                                          "total_chunks", "total_size", "chunk_size")] + \
+               [("expected_crc", C.c_uint32), ("actual_crc", C.c_uint32), ("crc_valid", C.c_int32),
+                ("nbits", C.c_int32), ("flags", C.c_int32), ("fine_metric", C.c_float),
+                ("reserved", C.c_int32 * 4)]
+
+
+DBG_BAND = 256
+DBG_SYMS = 256
+
+
+class Debug(C.Structure):
+    _fields_ = [("mean", C.c_double), ("mx", C.c_double), ("coarse_metric", C.c_double),
+                ("coarse_lo", C.c_int32), ("coarse_hi", C.c_int32), ("fine_metric", C.c_double),
+                ("fine_idx", C.c_int32), ("nsym", C.c_int32),
+                ("h_re", C.c_double * DBG_BAND), ("h_im", C.c_double * DBG_BAND),
+                ("x_re", C.c_double * DBG_BAND), ("x_im", C.c_double * DBG_BAND),
+                ("eq_re", C.c_double * DBG_BAND), ("eq_im", C.c_double * DBG_BAND),
+                ("phase", C.c_double * DBG_SYMS)]
+
+
+assert C.sizeof(Result) == 96, C.sizeof(Result)
+
+# (restype, argtypes) for every symbol the header declares
+_P = C.c_void_p
+SIGNATURES = {
+    "amod_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "amod_close": (C.c_int, [_P]),
+    "amod_last_error": (C.c_char_p, [_P]),
+    "amod_abi_version": (C.c_int, []),
+    "amod_config_preset": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(Cfg)]),
+    "amod_num_data_subs": (C.c_int32, [C.POINTER(Cfg)]),
+    "amod_estimate_frame_samples": (C.c_int32, [C.POINTER(Cfg), C.c_int32]),
+    "amod_payload_stride": (C.c_int64, [C.POINTER(Cfg), C.c_int64]),
+    "amod_reserve": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, C.c_int64]),
+    "amod_decode_device": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P, C.c_int64,
+                                     C.c_uint32, _P]),
+    "amod_decode_host": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P, _P,
+                                   C.c_int64, C.c_uint32]),
+    "amod_synchronize": (C.c_int, [_P]),
+    "amod_set_profiling": (C.c_int, [_P, C.c_int]),
+    "amod_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_int64)]),
+    "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,
+                                           C.c_int64, C.c_uint32, _P, _P]),
+    "amod_crc32": (C.c_uint32, [C.c_char_p, C.c_size_t]),
+    "amod_preamble1": (C.c_int, [C.POINTER(Cfg), _P]),
+    "amod_tx_legacy": (C.c_int64, [C.POINTER(Cfg), C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, _P]),
+    "amod_tx_meta": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P]),
+    "amod_tx_chunk": (C.c_int64, [C.POINTER(Cfg), C.c_char_p, C.c_int32, C.c_int32, _P]),
+    "amod_tx_test_signal": (C.c_int64, [C.POINTER(Cfg), _P]),
+    "amod_synth_payload": (None, [C.c_uint32, C.c_int32, _P]),
+    "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                            C.c_int32, _P, _P, _P, C.c_int32]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libamodem.so (built by __graft_entry__.build / `make -C audio-modem_amd/csrc`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libamodem.so not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.amod_abi_version() != 1:
+            raise ImportError("libamodem ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error(ctx=None) -> str:
+    s = load().amod_last_error(ctx)
+    return s.decode() if s else ""
+
+
+def check(rc: int, ctx=None):
+    if rc != 0:
+        raise RuntimeError(f"libamodem error {rc}: {last_error(ctx)}")
+    return rc

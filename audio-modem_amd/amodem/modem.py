@@ -1,0 +1,279 @@
+"""Python mirror of the modem.js function surface, backed by libamodem (HIP, gfx950).
+
+Names follow the reference (modem.js) in snake_case; semantics, argument meaning
+and error behaviour are the reference's:
+
+  set_ofdm_config(name)                     setOFDMConfig        modem.js:95-98
+  decode_received_signal(sig, mod, rep)     decodeReceivedSignal modem.js:557-654
+  decode_chunk_frame(frame, mod, rep)       decodeChunkFrame     modem.js:770-803
+  estimate_frame_samples(nbytes, mod, rep)  estimateFrameSamples modem.js:863-874
+  build_transmit_signal / build_metadata_frame / build_data_chunk_frame /
+  generate_test_signal / generate_preamble_symbol1 / crc32
+Signal-level failures come back as {'error': <exact reference string>} dicts;
+device failures raise RuntimeError. Results are plain dicts with bytes for data.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _lib as L
+
+OFDM_CONFIGS = {
+    "standard": dict(FFT_SIZE=512, CP_LEN=64, SYMBOL_LEN=576, SAMPLE_RATE=44100, SUB_START=12, SUB_END=232,
+                     PILOTS=[15, 29, 43, 57, 71, 85, 99, 113, 127, 141, 155, 169, 183, 197, 211, 225]),
+    "acoustic": dict(FFT_SIZE=512, CP_LEN=128, SYMBOL_LEN=640, SAMPLE_RATE=44100, SUB_START=23, SUB_END=93,
+                     PILOTS=[25, 35, 45, 55, 65, 75, 85]),
+    "narrowband": dict(FFT_SIZE=512, CP_LEN=256, SYMBOL_LEN=768, SAMPLE_RATE=44100, SUB_START=35, SUB_END=58,
+                       PILOTS=[37, 45, 53]),
+}
+OFDM = dict(OFDM_CONFIGS["standard"])  # mutable current config, like the reference global
+FRAME_META = 0xFE
+FRAME_DATA = 0xFF
+
+ERRORS = {
+    1: "Preamble not detected",
+    2: "Preamble not detected (low correlation)",
+    3: "Signal too short for CE",
+    4: "No data after CE",
+    5: "Decoded data too short",
+    6: "Decoded data too short for header",
+    8: "Metadata frame too short",
+    9: "Metadata frame truncated",
+    10: "Data chunk frame too short",
+    11: "Data chunk truncated",
+    12: "Frame too short for CE",
+}
+
+RESULT_DTYPE = np.dtype([(n, "<i4") for n in ("status", "preamble_idx", "coarse_idx", "frame_type", "aux", "nbytes",
+                                              "name_off", "name_len", "data_off", "data_len", "seq_num",
+                                              "total_chunks", "total_size", "chunk_size")] +
+                        [("expected_crc", "<u4"), ("actual_crc", "<u4"), ("crc_valid", "<i4"), ("nbits", "<i4"),
+                         ("flags", "<i4"), ("fine_metric", "<f4"), ("reserved", "<i4", (4,))])
+assert RESULT_DTYPE.itemsize == 96
+
+
+def set_ofdm_config(name: str):
+    """setOFDMConfig: unknown names fall back to 'standard' (modem.js:96)."""
+    OFDM.clear()
+    OFDM.update(OFDM_CONFIGS.get(name, OFDM_CONFIGS["standard"]))
+
+
+def _mod_id(mod: str) -> int:
+    if mod not in L.MODS:  # initConstellation on an unknown name throws (modem.js:108-109)
+        raise TypeError(f"Cannot read property 'points' of undefined (modulation {mod!r})")
+    return L.MODS[mod]
+
+
+def make_cfg(mod: str = "QPSK", rep: int = 1, ofdm: dict | None = None) -> L.Cfg:
+    o = OFDM if ofdm is None else ofdm
+    c = L.Cfg()
+    c.fft_size, c.cp_len, c.symbol_len = o["FFT_SIZE"], o["CP_LEN"], o["SYMBOL_LEN"]
+    c.sample_rate, c.sub_start, c.sub_end = o["SAMPLE_RATE"], o["SUB_START"], o["SUB_END"]
+    c.npilots = len(o["PILOTS"])
+    for i, p in enumerate(o["PILOTS"]):
+        c.pilots[i] = p
+    c.modulation = _mod_id(mod)
+    c.repetition = max(1, int(rep or 1))
+    return c
+
+
+def preset(name: str, mod: str = "QPSK", rep: int = 1) -> L.Cfg:
+    c = L.Cfg()
+    L.check(L.load().amod_config_preset(name.encode(), _mod_id(mod), int(rep or 1), C.byref(c)))
+    return c
+
+
+def text_decode(b: bytes) -> str:
+    """TextDecoder().decode: UTF-8 with replacement characters, leading BOM removed."""
+    if b[:3] == b"\xef\xbb\xbf":
+        b = b[3:]
+    return b.decode("utf-8", errors="replace")
+
+
+def to_reference(rec, slot: bytes, via_legacy: bool) -> dict:
+    """Format one amod_result the way modem.js returns it."""
+    st, ft = int(rec["status"]), int(rec["frame_type"])
+    if st == L.E_CAPACITY:
+        raise RuntimeError("frame exceeds the reserved decode workspace (amod_reserve)")
+    if st == 0:
+        if ft == FRAME_META:
+            out = {"frameType": FRAME_META, "totalChunks": int(rec["total_chunks"]),
+                   "totalFileSize": int(rec["total_size"]), "chunkSize": int(rec["chunk_size"]),
+                   "fileName": text_decode(slot[rec["name_off"]:rec["name_off"] + rec["name_len"]])}
+        elif ft == FRAME_DATA:
+            out = {"frameType": FRAME_DATA, "seqNum": int(rec["seq_num"]),
+                   "data": bytes(slot[rec["data_off"]:rec["data_off"] + rec["data_len"]]),
+                   "dataLen": int(rec["data_len"])}
+        else:
+            out = {"data": bytes(slot[rec["data_off"]:rec["data_off"] + rec["data_len"]]),
+                   "dataLen": int(rec["data_len"]),
+                   "fileName": text_decode(slot[rec["name_off"]:rec["name_off"] + rec["name_len"]])}
+        out.update(crcValid=bool(rec["crc_valid"]), expectedCRC=int(rec["expected_crc"]),
+                   actualCRC=int(rec["actual_crc"]))
+        if ft == 0:
+            out.update(preambleIdx=int(rec["preamble_idx"]), frameType="legacy")
+        elif via_legacy:
+            out["preambleIdx"] = int(rec["preamble_idx"])
+        return out
+    if st == 7:
+        return {"error": f"Invalid data length: {int(rec['aux'])}"}
+    if st == 13:
+        return {"error": f"Unknown frame type: 0x{int(rec['aux']):x}", "frameType": int(rec["aux"])}
+    out = {"error": ERRORS[st]}
+    if via_legacy and ft in (FRAME_META, FRAME_DATA) and st in (8, 9, 10, 11):
+        out["preambleIdx"] = int(rec["preamble_idx"])
+    return out
+
+
+class Demodulator:
+    """One HIP device context (stream + workspace) of libamodem."""
+
+    def __init__(self, device: int = 0):
+        self._L = L.load()
+        h = C.c_void_p()
+        L.check(self._L.amod_open(int(device), C.byref(h)))
+        self.ctx = h
+        self.device = device
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self.ctx:
+            self._L.amod_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- host path
+    def decode_batch(self, samples: np.ndarray, offsets, lengths, mod="QPSK", rep=1, mode=L.MODE_RECEIVED,
+                     cfg: L.Cfg | None = None, options: int = 0):
+        """Decode frames samples[off:off+len] (host memory, PCIe round trip).
+        Returns (records: RESULT_DTYPE array, payload: uint8 [nframes, stride])."""
+        samples = np.ascontiguousarray(samples, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        lengths = np.ascontiguousarray(lengths, np.int32)
+        cfg = cfg or make_cfg(mod, rep)
+        n = len(offsets)
+        stride = int(self._L.amod_payload_stride(C.byref(cfg), int(lengths.max()) if n else 0))
+        rec = np.zeros(n, RESULT_DTYPE)
+        pay = np.zeros((n, stride), np.uint8)
+        with self._lock:
+            L.check(self._L.amod_decode_host(self.ctx, C.byref(cfg), mode,
+                                             samples.ctypes.data if samples.size else None, samples.size,
+                                             offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data,
+                                             pay.ctypes.data, stride, options), self.ctx)
+        return rec, pay
+
+    def decode_received_signal(self, signal, mod="QPSK", rep=1, options=0) -> dict:
+        sig = np.ascontiguousarray(signal, np.float32)
+        rec, pay = self.decode_batch(sig, [0], [len(sig)], mod, rep or 1, L.MODE_RECEIVED, options=options)
+        return to_reference(rec[0], pay[0].tobytes(), via_legacy=True)
+
+    def decode_chunk_frame(self, frame, mod="QPSK", rep=1, options=0) -> dict:
+        fr = np.ascontiguousarray(frame, np.float32)
+        rec, pay = self.decode_batch(fr, [0], [len(fr)], mod, rep or 1, L.MODE_CHUNK, options=options)
+        return to_reference(rec[0], pay[0].tobytes(), via_legacy=False)
+
+    # -------------------------------------------------------------- device path
+    def reserve(self, cfg: L.Cfg, nframes: int, max_len: int):
+        L.check(self._L.amod_reserve(self.ctx, C.byref(cfg), int(nframes), int(max_len)), self.ctx)
+
+    def decode_device(self, cfg: L.Cfg, mode: int, samples_ptr: int, offsets_ptr: int, lengths_ptr: int,
+                      nframes: int, results_ptr: int, payload_ptr: int, stride: int, stream: int = 0,
+                      options: int = 0, debug_ptr: int = 0):
+        """Enqueue a decode of device-resident frames (raw device pointers, e.g.
+        torch tensor .data_ptr()) on `stream` (hipStream_t as int, 0 = own)."""
+        if debug_ptr:
+            rc = self._L.amod_decode_device_debug(self.ctx, C.byref(cfg), mode, samples_ptr, offsets_ptr,
+                                                  lengths_ptr, nframes, results_ptr, payload_ptr, stride, options,
+                                                  stream or None, debug_ptr)
+        else:
+            rc = self._L.amod_decode_device(self.ctx, C.byref(cfg), mode, samples_ptr, offsets_ptr, lengths_ptr,
+                                            nframes, results_ptr, payload_ptr, stride, options, stream or None)
+        L.check(rc, self.ctx)
+
+    def synchronize(self):
+        L.check(self._L.amod_synchronize(self.ctx), self.ctx)
+
+
+# ------------------------------------------------------------ host utilities --
+def crc32(data: bytes) -> int:
+    data = bytes(data)
+    return int(L.load().amod_crc32(data, len(data)))
+
+
+def payload_stride(cfg: L.Cfg, max_len: int) -> int:
+    return int(L.load().amod_payload_stride(C.byref(cfg), int(max_len)))
+
+
+def estimate_frame_samples(payload_bytes: int, mod: str = "QPSK", rep: int = 1) -> int:
+    cfg = make_cfg(mod, rep)
+    return int(L.load().amod_estimate_frame_samples(C.byref(cfg), int(payload_bytes)))
+
+
+def generate_preamble_symbol1(cfg: L.Cfg | None = None) -> np.ndarray:
+    cfg = cfg or make_cfg()
+    out = np.zeros(cfg.symbol_len, np.float32)
+    L.check(L.load().amod_preamble1(C.byref(cfg), out.ctypes.data))
+    return out
+
+
+def _tx(fn, *args) -> np.ndarray:
+    n = fn(*args, None)
+    if n < 0:
+        raise ValueError("invalid transmit arguments")
+    out = np.zeros(max(int(n), 1), np.float32)
+    fn(*args, out.ctypes.data)
+    return out[:n]
+
+
+def build_transmit_signal(data: bytes, mod="QPSK", file_name="file", rep=1, cfg=None) -> np.ndarray:
+    cfg = cfg or make_cfg(mod, rep)
+    data = bytes(data)
+    name = (file_name or "file").encode("utf-8")
+    return _tx(L.load().amod_tx_legacy, C.byref(cfg), data, len(data), name, len(name))
+
+
+def build_metadata_frame(total_chunks, total_size, chunk_size, file_name, mod="QPSK", rep=1, cfg=None):
+    cfg = cfg or make_cfg(mod, rep)
+    name = (file_name or "file").encode("utf-8")
+    return _tx(L.load().amod_tx_meta, C.byref(cfg), int(total_chunks), int(total_size), int(chunk_size), name,
+               len(name))
+
+
+def build_data_chunk_frame(data: bytes, seq: int, mod="QPSK", rep=1, cfg=None):
+    cfg = cfg or make_cfg(mod, rep)
+    data = bytes(data)
+    return _tx(L.load().amod_tx_chunk, C.byref(cfg), data, len(data), int(seq))
+
+
+def generate_test_signal(mod="QPSK", rep=1, cfg=None):
+    cfg = cfg or make_cfg(mod, rep)
+    return _tx(L.load().amod_tx_test_signal, C.byref(cfg)), bytes(range(16))
+
+
+def synth_payload(seed: int, length: int) -> bytes:
+    out = np.zeros(max(length, 1), np.uint8)
+    L.load().amod_synth_payload(seed & 0xFFFFFFFF, int(length), out.ctypes.data)
+    return out[:length].tobytes()
+
+
+def synth_legacy_batch(cfg: L.Cfg, nframes: int, payload_len: int = 1024, name: str = "f.bin", first: int = 0,
+                       threads: int = 0, out: np.ndarray | None = None):
+    """nframes legacy frames back to back (payload seed 0x9E3779B9 ^ frame index)."""
+    lib = L.load()
+    nm = name.encode()
+    total = lib.amod_synth_legacy_batch(C.byref(cfg), nframes, first, payload_len, nm, len(nm), None, None, None, 0)
+    if out is None:
+        out = np.empty(int(total), np.float32)
+    offs = np.zeros(nframes, np.int64)
+    lens = np.zeros(nframes, np.int32)
+    lib.amod_synth_legacy_batch(C.byref(cfg), nframes, first, payload_len, nm, len(nm), out.ctypes.data,
+                                offs.ctypes.data, lens.ctypes.data, threads)
+    return out, offs, lens

@@ -1,0 +1,290 @@
+// amodem_internal.h — shared host/device definitions of the MI355X demodulator.
+//
+// Frame pipeline (per frame, mirrors modem.js decodeReceivedSignal 557-654 and
+// decodeChunkFrame 770-803):
+//   k_decode_fast  (k_decode_fast.hip)  one 1024-thread workgroup per frame, frame
+//                   resident in LDS, fp32 arithmetic with guard bands on every
+//                   discrete decision; a frame whose decision falls inside a guard
+//                   band (or that does not fit LDS) is appended to the exact list.
+//   k_decode_exact (k_decode_exact.hip) replays the reference arithmetic in IEEE
+//                   double, operation for operation, for the listed frames.
+// Both end in finish_frame() below: majority vote, MSB-first byte packing, frame
+// parsing and CRC-32 — integer work, bit-exact by construction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "amodem.h"
+
+namespace amod {
+
+constexpr int kFft = 512;
+constexpr int kMaxBand = 256;  // sub_end < fft/2
+constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
+constexpr int kCrcChunk = 16;
+constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
+
+// Device-resident tables, built once per configuration by the runtime.
+struct DevTables {
+  const float *pre1;       // [symbol_len] preamble 1 (f32, generatePreambleSymbol1)
+  const float2 *tw1;       // [8][64] e^{-2πi l q/512}, pass-1 twiddles (row 0 unused)
+  const float2 *tw2;       // [8][8]  e^{-2πi 8 l1 p1/512}, pass-2 twiddles
+  const double2 *tw_exact; // [511] per-stage recurrence twiddles (fftIterative 34-44)
+  const float *known;      // [nband] CE symbol values ±1 (generateChannelEstSymbol)
+  const int16_t *band_di;  // [nband] data-subcarrier index, -1 for pilots
+  const uint32_t *crc_s4;  // [4][256] slice-by-4 CRC tables
+  const uint32_t *crc_m1;  // [32][4][256] shift-by-(16*q) zero-byte operators, q<32
+  const uint32_t *crc_m2;  // [32][4][256] shift-by-(512*q) operators, q<32
+  const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
+  const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
+};
+
+struct DevCfg {
+  int32_t cp, sym, sub_start, sub_end, nband, npilots, ndata, bps, mod, rep;
+  int32_t origin_idx;  // constellationDemap(0,0): decision for an all-zero spectrum
+  int32_t mode;        // AMOD_MODE_*
+  int32_t pilots[AMOD_MAX_PILOTS];
+  double te;           // sum pre1^2 in reference order (f64)
+  float te_f;
+  float guard;         // fast-path guard scale (1 = default)
+  DevTables t;
+};
+
+struct DevWork {
+  const float *samples;
+  const int64_t *off;
+  const int32_t *len;
+  int32_t nframes;
+  amod_result *res;
+  uint8_t *payload;
+  int64_t stride;
+  amod_debug *dbg;
+  int32_t *fb_count; // exact-kernel work list
+  int32_t *fb_list;
+  int32_t *fb_flags;
+  float *xs;          // exact kernel: per-slot normalised samples
+  uint32_t *bits;     // exact kernel: per-slot bit arrays
+  int64_t xs_stride;  // floats per slot
+  int64_t bits_stride;// words per slot
+  uint32_t options;
+};
+
+// ---------------------------------------------------------------- helpers --
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+template <typename T> __device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename T> __device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = w > v ? w : v; }
+  return v;
+}
+template <typename T> __device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = w < v ? w : v; }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_or(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+
+// byte i of an MSB-first packed bit stream (word w holds bytes 4w..4w+3, big-endian)
+__device__ __forceinline__ uint32_t stream_byte(const uint32_t *w, int i) {
+  return (w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFFu;
+}
+__device__ __forceinline__ int32_t be32_at(const uint32_t *w, int i) {
+  return (int32_t)((stream_byte(w, i) << 24) | (stream_byte(w, i + 1) << 16) |
+                   (stream_byte(w, i + 2) << 8) | stream_byte(w, i + 3));
+}
+
+// apply a zero-byte shift operator stored as 4 byte tables
+__device__ __forceinline__ uint32_t crc_apply(const uint32_t *op, uint32_t r) {
+  return op[r & 0xFF] ^ op[256 + ((r >> 8) & 0xFF)] ^ op[512 + ((r >> 16) & 0xFF)] ^ op[768 + (r >> 24)];
+}
+
+// Per-frame parse, modem.js:607-653 (legacy), 805-849 (meta/data), 793-802 (chunk).
+// Fills r (status, offsets, header fields); returns the CRC range length or -1.
+__device__ inline int parse_stream(const uint32_t *v, int nbytes, int mode, amod_result &r) {
+  r.nbytes = nbytes;
+  const int min_bytes = mode == AMOD_MODE_CHUNK ? 6 : 10;
+  if (nbytes < min_bytes) { r.status = AMOD_E_DECODED_SHORT; r.frame_type = -1; return -1; }
+  const int t = (int)stream_byte(v, 0);
+  if (t == 0xFE) {
+    r.frame_type = 0xFE;
+    if (nbytes < 16) { r.status = AMOD_E_META_SHORT; return -1; }
+    r.total_chunks = be32_at(v, 1);
+    r.total_size = be32_at(v, 5);
+    r.chunk_size = (int32_t)((stream_byte(v, 9) << 8) | stream_byte(v, 10));
+    const int nl = (int)stream_byte(v, 11);
+    int off = 12;
+    if (off + nl + 4 > nbytes) { r.status = AMOD_E_META_TRUNC; return -1; }
+    r.name_off = off; r.name_len = nl;
+    off += nl;
+    r.expected_crc = (uint32_t)be32_at(v, off);
+    r.status = AMOD_OK;
+    return off;
+  }
+  if (t == 0xFF) {
+    r.frame_type = 0xFF;
+    if (nbytes < 11) { r.status = AMOD_E_CHUNK_SHORT; return -1; }
+    r.seq_num = be32_at(v, 1);
+    const int dl = (int)((stream_byte(v, 5) << 8) | stream_byte(v, 6));
+    int off = 7;
+    if (off + dl + 4 > nbytes) { r.status = AMOD_E_CHUNK_TRUNC; return -1; }
+    r.data_off = off; r.data_len = dl;
+    off += dl;
+    r.expected_crc = (uint32_t)be32_at(v, off);
+    r.status = AMOD_OK;
+    return off;
+  }
+  if (mode == AMOD_MODE_CHUNK) { r.frame_type = t; r.aux = t; r.status = AMOD_E_UNKNOWN_TYPE; return -1; }
+  r.frame_type = 0;
+  const int nl = t;
+  int off = 1;
+  if (off + nl + 4 + 4 > nbytes) { r.status = AMOD_E_SHORT_HEADER; return -1; }
+  r.name_off = off; r.name_len = nl;
+  off += nl;
+  const int32_t dl = be32_at(v, off);
+  off += 4;
+  if (dl <= 0 || (int64_t)off + dl + 4 > nbytes) { r.status = AMOD_E_INVALID_LEN; r.aux = dl; return -1; }
+  r.data_off = off; r.data_len = dl;
+  off += dl;
+  r.expected_crc = (uint32_t)be32_at(v, off);
+  r.status = AMOD_OK;
+  return off;
+}
+
+// Workgroup CRC-32 (modem.js:443-457) of bytes [0, L) of stream v.
+// 256 threads each hash one 16-byte chunk with slice-by-4 tables; the chunk
+// registers are moved to the end of the message with precomputed zero-byte
+// shift operators and XOR-combined (CRC linearity). `red` is >= 8 words of LDS.
+__device__ inline uint32_t block_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *red) {
+  const int tid = threadIdx.x;
+  uint32_t reg = 0xFFFFFFFFu; // register carried between 4096-byte passes (uniform)
+  const int npass = (L + kCrcBlock - 1) / kCrcBlock;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int p0 = pass * kCrcBlock;
+    const int plen = min(kCrcBlock, L - p0);
+    const int nch = (plen + kCrcChunk - 1) / kCrcChunk; // chunks, right-aligned
+    uint32_t contrib = 0;
+    if (tid < kCrcLanes) {
+      const int j = tid - (kCrcLanes - nch); // chunk index from the left, may be negative
+      if (j >= 0) {
+        const int end = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
+        const int beg = max(0, end - kCrcChunk);
+        uint32_t c = (j == 0) ? reg : 0u;
+        int i = beg;
+        for (; i + 4 <= end; i += 4) {
+          c ^= (stream_byte(v, p0 + i) | (stream_byte(v, p0 + i + 1) << 8) |
+                (stream_byte(v, p0 + i + 2) << 16) | (stream_byte(v, p0 + i + 3) << 24));
+          c = t.crc_s4[768 + (c & 0xFF)] ^ t.crc_s4[512 + ((c >> 8) & 0xFF)] ^
+              t.crc_s4[256 + ((c >> 16) & 0xFF)] ^ t.crc_s4[c >> 24];
+        }
+        for (; i < end; ++i) c = t.crc_s4[(c ^ stream_byte(v, p0 + i)) & 0xFF] ^ (c >> 8);
+        const int q = nch - 1 - j; // chunks to its right -> shift by 16q bytes
+        if (q & 31) c = crc_apply(t.crc_m1 + (q & 31) * 1024, c);
+        if (q >> 5) c = crc_apply(t.crc_m2 + (q >> 5) * 1024, c);
+        contrib = c;
+      }
+    }
+    contrib = wave_xor(contrib);
+    __syncthreads();
+    if ((tid & 63) == 0 && tid < kCrcLanes) red[tid >> 6] = contrib;
+    __syncthreads();
+    reg = red[0] ^ red[1] ^ red[2] ^ red[3];
+    __syncthreads();
+  }
+  return reg ^ 0xFFFFFFFFu;
+}
+
+// Majority vote (modem.js:487-495) of the bit stream `bits` (nbits) into `voted`
+// (words), returns the voted bit count. rep == 1 is a pass-through handled by
+// the caller. Whole workgroup.
+__device__ inline int block_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
+  const int nv = nbits / rep;
+  const int nw = (nv + 31) >> 5;
+  const int thr = (rep + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
+  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+    uint32_t word = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int j = w * 32 + b;
+      if (j >= nv) break;
+      int sum = 0;
+      for (int u = 0; u < rep; ++u) {
+        const int pos = j * rep + u;
+        sum += (bits[pos >> 5] >> (31 - (pos & 31))) & 1;
+      }
+      word |= (uint32_t)(sum >= thr) << (31 - b);
+    }
+    voted[w] = word;
+  }
+  return nv;
+}
+
+// Parse + CRC + store of one frame whose (voted) bit stream is in `v`.
+// r must already hold status = AMOD_OK and the detection fields. Whole workgroup.
+__device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg &cfg, amod_result &r_in,
+                                    amod_result *out, uint8_t *slot, int64_t stride, uint32_t *red,
+                                    int *shared_status) {
+  const int nbytes = nvoted >> 3;
+  __shared__ amod_result r_sh;
+  __shared__ int crc_len;
+  if (threadIdx.x == 0) {
+    r_sh = r_in;
+    crc_len = parse_stream(v, nbytes, cfg.mode, r_sh);
+    if (cfg.mode == AMOD_MODE_RECEIVED) {
+      // preambleIdx is reported on legacy success and on every 0xFE/0xFF result (609-620)
+      const bool keep = (r_sh.frame_type == 0xFE || r_sh.frame_type == 0xFF) ||
+                        (r_sh.frame_type == 0 && r_sh.status == AMOD_OK);
+      if (!keep) r_sh.preamble_idx = -1;
+    } else {
+      r_sh.preamble_idx = -1;
+    }
+  }
+  __syncthreads();
+  const int L = crc_len;
+  if (L >= 0) {
+    const uint32_t crc = block_crc32(v, L, cfg.t, red);
+    if (threadIdx.x == 0) {
+      r_sh.actual_crc = crc;
+      r_sh.crc_valid = r_sh.expected_crc == crc;
+    }
+  }
+  // payload bytes, big-endian words -> memory order
+  const int nw = (nbytes + 3) >> 2;
+  uint32_t *dst = reinterpret_cast<uint32_t *>(slot);
+  const int cap_w = (int)(stride >> 2);
+  for (int w = threadIdx.x; w < nw && w < cap_w; w += blockDim.x) dst[w] = __builtin_bswap32(v[w]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *out = r_sh;
+    if (shared_status) *shared_status = r_sh.status;
+  }
+}
+
+__device__ inline void init_result(amod_result &r) {
+  r.status = AMOD_OK; r.preamble_idx = -1; r.coarse_idx = -1; r.frame_type = -1; r.aux = 0;
+  r.nbytes = 0; r.name_off = 0; r.name_len = 0; r.data_off = 0; r.data_len = 0;
+  r.seq_num = 0; r.total_chunks = 0; r.total_size = 0; r.chunk_size = 0;
+  r.expected_crc = 0; r.actual_crc = 0; r.crc_valid = 0; r.nbits = 0; r.flags = 0;
+  r.fine_metric = 0.f; r.reserved[0] = r.reserved[1] = r.reserved[2] = r.reserved[3] = 0;
+}
+
+} // namespace amod
+
+// kernels (defined in k_decode_fast.hip / k_decode_exact.hip)
+extern "C" {
+hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s);
+hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
+int amod_fast_capacity(void); // max samples per frame of the LDS-resident kernel
+}

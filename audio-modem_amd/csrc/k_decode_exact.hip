@@ -1,0 +1,340 @@
+// k_decode_exact.hip — exact-replica path of the receive chain (gfx950).
+//
+// Replays modem.js in IEEE double, operation for operation (this file is built
+// with -ffp-contract=off; fp64 add/mul/div/sqrt are correctly rounded), so every
+// intermediate equals the reference bit for bit:
+//   mean        sequential sum (preprocessSignal 215-217), one lane over LDS chunks
+//   Schmidl-Cox sequential sliding recurrence (detectPreamble 292-316), one lane
+//   fine timing one lane per candidate offset, sequential 576-tap sums (576-587)
+//   FFT         radix-2 DIT stages with the reference's per-stage twiddle
+//               recurrence tabulated on the host (fftIterative 26-47); each stage's
+//               butterflies are independent, so 256 lanes run them in parallel
+//               without changing a single rounding
+//   equaliser / pilot phase / demap  as demodulateOFDM 386-413 (joint argmin)
+// It runs for frames the fast kernel routes here (guard band hit, NaN/Inf, too
+// long for LDS, or AMOD_OPT_FORCE_EXACT), one 256-thread workgroup per frame.
+#include "amodem_internal.h"
+
+namespace amod {
+namespace {
+
+constexpr int XT = 256;     // threads per workgroup
+constexpr int CH = 4096;    // sample chunk staged in LDS for the sequential lanes
+
+struct alignas(16) XSmem {
+  float chunk[CH + 520];
+  double re[kFft], im[kFft];
+  double hr[kFft], hi[kFft];
+  double er[kFft], ei[kFft];
+  double rd[XT / 64 + 4];
+  float rf[XT / 64];
+  int ri[XT / 64 + 4];
+  uint32_t ru[16];
+  double mean, mx, best, phase;
+  int coarse, start, status;
+};
+
+__device__ __forceinline__ double or_zero(float v) { return (v != v || v == 0.0f) ? 0.0 : (double)v; } // `x || 0`
+__device__ __forceinline__ int rev9(int i) { return (int)(__brev((unsigned)i) >> 23); }
+
+// fft(re, 0) of 512 real samples src[0..511] (modem.js:6-13, 26-66), result in sm.re/sm.im
+__device__ void fft_exact(const float *src, XSmem &sm, const double2 *tw) {
+  const int tid = threadIdx.x;
+  for (int j = tid; j < kFft; j += XT) { sm.re[j] = or_zero(src[rev9(j)]); sm.im[j] = 0.0; }
+  __syncthreads();
+  for (int half = 1; half < kFft; half <<= 1) {
+    const int t = tid; // 256 butterflies per stage
+    const int blk = t / half, j = t - blk * half;
+    const int a = blk * 2 * half + j, b = a + half;
+    const double2 w = tw[half - 1 + j];
+    const double t_re = w.x * sm.re[b] - w.y * sm.im[b];
+    const double t_im = w.x * sm.im[b] + w.y * sm.re[b];
+    sm.re[b] = sm.re[a] - t_re;
+    sm.im[b] = sm.im[a] - t_im;
+    sm.re[a] = sm.re[a] + t_re;
+    sm.im[a] = sm.im[a] + t_im;
+    __syncthreads();
+  }
+}
+
+// Make this workgroup's global stores (plain or atomic) visible to its own later
+// plain loads: drain them to L2, barrier, then drop this CU's L1 copies.
+__device__ __forceinline__ void wg_global_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ double js_max(double a, double b) { // Math.max, NaN-propagating
+  if (a != a || b != b) return __builtin_nan("");
+  return b > a ? b : a;
+}
+
+__global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const DevWork w) {
+  __shared__ XSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int count = *w.fb_count;
+  const int SYM = cfg.sym, CP = cfg.cp;
+  for (int item = blockIdx.x; item < count; item += gridDim.x) {
+    const int f = w.fb_list[item];
+    const int flags0 = w.fb_flags[item];
+    const float *xr = w.samples + w.off[f];
+    const int N = w.len[f];
+    float *xs = w.xs + (int64_t)blockIdx.x * w.xs_stride;
+    uint32_t *bits = w.bits + (int64_t)blockIdx.x * w.bits_stride;
+    amod_debug *D = w.dbg ? w.dbg + f : nullptr;
+    amod_result r;
+    init_result(r);
+    r.flags = flags0 | AMOD_FLAG_EXACT;
+    {
+      const int64_t need_bits = (int64_t)(N / SYM) * cfg.ndata * cfg.bps;
+      if ((int64_t)N > w.xs_stride || 2 * ((need_bits + 31) / 32) + 16 > w.bits_stride) {
+        if (tid == 0) { r.status = AMOD_E_CAPACITY; w.res[f] = r; }
+        __syncthreads();
+        continue;
+      }
+    }
+    int status = AMOD_OK;
+    int start = 0;
+    const float *sig = xr; // samples the demodulator reads
+
+    if (cfg.mode == AMOD_MODE_RECEIVED) {
+      // ---- preprocessSignal: sequential mean, then |f32(x - mean)| max, then scale
+      double sum = 0.0;
+      for (int c0 = 0; c0 < N; c0 += CH) {
+        const int n = min(CH, N - c0);
+        for (int i = tid; i < n; i += XT) sm.chunk[i] = xr[c0 + i];
+        __syncthreads();
+        if (tid == 0) for (int i = 0; i < n; ++i) sum += (double)sm.chunk[i];
+        __syncthreads();
+      }
+      if (tid == 0) sm.mean = sum / (double)N;
+      __syncthreads();
+      const double mean = sm.mean;
+      double mx = 0.0;
+      for (int i = tid; i < N; i += XT) {
+        const float o = (float)((double)xr[i] - mean);
+        xs[i] = o;
+        mx = js_max(mx, fabs((double)o));
+      }
+      for (int o = 32; o > 0; o >>= 1) mx = js_max(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0) sm.rd[wave] = mx;
+      __syncthreads();
+      if (tid == 0) {
+        double m = 0.0;
+        for (int i = 0; i < XT / 64; ++i) m = js_max(m, sm.rd[i]);
+        sm.mx = m;
+        if (D) { D->mean = mean; D->mx = m; }
+      }
+      __syncthreads();
+      mx = sm.mx;
+      if (mx > 1e-6)
+        for (int i = tid; i < N; i += XT) xs[i] = (float)((double)xs[i] / mx);
+      wg_global_sync();
+      sig = xs;
+
+      // ---- detectPreamble: sequential recurrence, one lane
+      const int half = kFft / 2;
+      int coarse = -1;
+      double best = 0.0;
+      if (N >= 2 * half) {
+        const int end = N - 2 * half;
+        double p = 0.0, ra = 0.0, rb = 0.0;
+        for (int c0 = 0; c0 <= end; c0 += CH) {
+          const int n = min(CH + 2 * half + 1, N - c0);
+          for (int i = tid; i < n; i += XT) sm.chunk[i] = xs[c0 + i];
+          __syncthreads();
+          if (tid == 0) {
+            if (c0 == 0) {
+              for (int m = 0; m < half; ++m) {
+                const double a = sm.chunk[m], b = sm.chunk[m + half];
+                p += a * b; ra += a * a; rb += b * b;
+              }
+            }
+            const int dlast = min(c0 + CH - 1, end);
+            for (int d = c0; d <= dlast; ++d) {
+              if (ra > 0.01 && rb > 0.01) {
+                const double metric = (p * p) / (ra * rb);
+                if (metric > best) { best = metric; coarse = d; }
+              }
+              if (d < end) {
+                const int k = d - c0;
+                const double a_out = sm.chunk[k], mid = sm.chunk[k + half], b_in = sm.chunk[k + 2 * half];
+                p += mid * b_in - a_out * mid;
+                ra += mid * mid - a_out * a_out;
+                rb += b_in * b_in - mid * mid;
+              }
+            }
+          }
+          __syncthreads();
+        }
+        if (tid == 0) { sm.best = best; sm.coarse = best > 0.5 ? coarse : -1; }
+      } else if (tid == 0) {
+        sm.best = 0.0; sm.coarse = -1;
+      }
+      __syncthreads();
+      coarse = sm.coarse;
+      r.coarse_idx = coarse;
+      if (D && tid == 0) { D->coarse_metric = sm.best; D->coarse_lo = coarse; D->coarse_hi = coarse; }
+      if (coarse < 0) {
+        status = AMOD_E_PREAMBLE;
+      } else {
+        // ---- fine timing: one lane per offset, sequential sums (modem.js:567-588)
+        const int R = CP * 3;
+        const int lo = max(0, coarse - R), hi = min(N - SYM, coarse + R);
+        double bm = -__builtin_inf();
+        int bi = 0x7fffffff;
+        for (int d = lo + tid; d <= hi; d += XT) {
+          double corr = 0.0, se = 0.0;
+          for (int i = 0; i < SYM; ++i) {
+            const double sv = xs[d + i];
+            corr += sv * (double)cfg.t.pre1[i];
+            se += sv * sv;
+          }
+          const double den = sqrt(se * cfg.te);
+          if (den > 0.001) {
+            const double m = corr / den;
+            if (m > bm) { bm = m; bi = d; }
+          }
+        }
+        // argmax over lanes: highest metric, then lowest offset (strict '>' in order)
+        for (int o = 32; o > 0; o >>= 1) {
+          const double om = __shfl_xor(bm, o, 64);
+          const int oi = __shfl_xor(bi, o, 64);
+          if (om > bm || (om == bm && oi < bi)) { bm = om; bi = oi; }
+        }
+        if (lane == 0) { sm.rd[wave] = bm; sm.ri[wave] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+          double B = -__builtin_inf();
+          int I = 0x7fffffff;
+          for (int i = 0; i < XT / 64; ++i)
+            if (sm.rd[i] > B || (sm.rd[i] == B && sm.ri[i] < I)) { B = sm.rd[i]; I = sm.ri[i]; }
+          sm.best = B;
+          sm.start = I == 0x7fffffff ? coarse : I;
+          if (D) { D->fine_metric = B; D->fine_idx = sm.start; }
+        }
+        __syncthreads();
+        start = sm.start;
+        r.fine_metric = (float)sm.best;
+        if (sm.best < 0.1) status = AMOD_E_LOW_CORR;
+        else if (start + 3 * SYM > N) status = AMOD_E_SHORT_CE;
+        else if (start + 3 * SYM >= N) status = AMOD_E_NO_DATA;
+        r.preamble_idx = start;
+      }
+    } else {
+      if (3 * SYM > N) status = AMOD_E_FRAME_SHORT_CE;
+      else if (3 * SYM >= N) status = AMOD_E_NO_DATA;
+    }
+
+    if (status != AMOD_OK) {
+      if (tid == 0) {
+        r.status = status;
+        r.preamble_idx = -1;
+        w.res[f] = r;
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // ---- channel estimate (estimateChannel, modem.js:421-440)
+    const int ce0 = start + 2 * SYM, data0 = start + 3 * SYM;
+    fft_exact(sig + ce0 + CP, sm, cfg.t.tw_exact);
+    for (int k = tid; k < kFft; k += XT) {
+      double hr = 0.0, hi = 0.0;
+      if (k >= cfg.sub_start && k <= cfg.sub_end) {
+        const double xr_ = (double)cfg.t.known[k - cfg.sub_start], xi_ = 0.0;
+        const double d = xr_ * xr_ + xi_ * xi_;
+        if (d > 1e-10) {
+          hr = (sm.re[k] * xr_ + sm.im[k] * xi_) / d;
+          hi = (sm.im[k] * xr_ - sm.re[k] * xi_) / d;
+        }
+        if (D) { D->h_re[k - cfg.sub_start] = hr; D->h_im[k - cfg.sub_start] = hi; }
+      }
+      sm.hr[k] = hr; sm.hi[k] = hi;
+    }
+    __syncthreads();
+
+    // ---- demodulateOFDM (modem.js:365-418)
+    const int M = (N - data0) / SYM;
+    const int nbits = M * cfg.ndata * cfg.bps;
+    const int nwords = (nbits + 31) >> 5;
+    for (int i = tid; i < nwords + 8; i += XT) bits[i] = 0u;
+    wg_global_sync();
+    const int npts = cfg.mod == AMOD_BPSK ? 2 : (cfg.mod == AMOD_QPSK ? 4 : 16);
+    for (int s = 0; s < M; ++s) {
+      __syncthreads();
+      fft_exact(sig + data0 + s * SYM + CP, sm, cfg.t.tw_exact);
+      for (int k = tid; k < kFft; k += XT) {
+        double er = 0.0, ei = 0.0;
+        if (k >= cfg.sub_start && k <= cfg.sub_end) {
+          const double hr = sm.hr[k], hi = sm.hi[k];
+          const double hmag = hr * hr + hi * hi;
+          if (hmag > 1e-10) {
+            er = (sm.re[k] * hr + sm.im[k] * hi) / hmag;
+            ei = (sm.im[k] * hr - sm.re[k] * hi) / hmag;
+          } else {
+            er = sm.re[k]; ei = sm.im[k];
+          }
+          if (D && s == 0) {
+            const int b = k - cfg.sub_start;
+            D->x_re[b] = sm.re[k]; D->x_im[b] = sm.im[k]; D->eq_re[b] = er; D->eq_im[b] = ei;
+          }
+        }
+        sm.er[k] = er; sm.ei[k] = ei;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double ps = 0.0;
+        int pc = 0;
+        for (int i = 0; i < cfg.npilots; ++i) {
+          const int p = cfg.pilots[i];
+          if (p >= cfg.sub_start && p <= cfg.sub_end && fabs(sm.er[p]) > 1e-6) { ps += sm.ei[p] / sm.er[p]; pc++; }
+        }
+        sm.phase = pc > 0 ? ps / (double)pc : 0.0;
+        if (D && s < AMOD_DBG_SYMS) D->phase[s] = sm.phase;
+      }
+      __syncthreads();
+      const double ph = sm.phase;
+      for (int b = tid; b < cfg.nband; b += XT) {
+        const int di = cfg.t.band_di[b];
+        if (di < 0) continue;
+        const int k = cfg.sub_start + b;
+        const double cr = sm.er[k] + sm.ei[k] * ph;
+        const double ci = sm.ei[k] - sm.er[k] * ph;
+        double md = __builtin_inf();
+        int mi = 0;
+        for (int i = 0; i < npts; ++i) {
+          const double dr = cr - cfg.t.points[i].x, dd = ci - cfg.t.points[i].y;
+          const double dist = dr * dr + dd * dd;
+          if (dist < md) { md = dist; mi = i; }
+        }
+        const int pos = (s * cfg.ndata + di) * cfg.bps;
+        const uint32_t val = (uint32_t)mi << (32 - cfg.bps - (pos & 31));
+        if (val) atomicOr(&bits[pos >> 5], val);
+      }
+    }
+    wg_global_sync();
+    if (D && tid == 0) D->nsym = M;
+    r.nbits = nbits;
+    const uint32_t *v = bits;
+    int nv = nbits;
+    if (cfg.rep > 1) {
+      uint32_t *voted = bits + ((nwords + 3) & ~3);
+      nv = block_vote(bits, nbits, cfg.rep, voted);
+      wg_global_sync();
+      v = voted;
+    }
+    finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr);
+    __syncthreads();
+  }
+}
+
+} // namespace
+} // namespace amod
+
+extern "C" hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s) {
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amod::k_decode_exact, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
+  return hipGetLastError();
+}

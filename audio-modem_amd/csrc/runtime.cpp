@@ -1,0 +1,786 @@
+// runtime.cpp — host side of libamodem.so: the C ABI declared in include/amodem.h.
+//
+// Owns one HIP stream and a grow-only device workspace per context, builds the
+// per-configuration device tables (preamble template, CE signs, FFT twiddles,
+// CRC operators, constellation), and enqueues k_decode_fast followed by
+// k_decode_exact. Also carries the reference-equivalent transmit builders used
+// to synthesise benchmark input (modem.js buildTransmitSignal & co.).
+// Built with -ffp-contract=off: the template/twiddle arithmetic must round
+// exactly like modem.js.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "amodem.h"
+#include "amodem_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// ------------------------------------------------------------ reference math
+// seededRandom (modem.js:153-156): product and sum in double, ToInt32, & 0x7fffffff
+struct SeededRandom {
+  double s;
+  explicit SeededRandom(double seed) : s(seed) {}
+  double next() {
+    const double prod = s * 1103515245.0;
+    const double sum = prod + 12345.0;
+    const uint64_t as_u = (uint64_t)std::fmod(sum, 18446744073709551616.0);
+    const uint32_t v = (uint32_t)as_u & 0x7fffffffu;
+    s = (double)v;
+    return (double)v / 2147483647.0;
+  }
+};
+
+// per-stage twiddle recurrence of fftIterative (modem.js:28-44), 511 entries:
+// stage with half-size h uses entries [h-1, 2h-1)
+std::vector<double> stage_twiddles(bool inverse) {
+  std::vector<double> t(2 * 511);
+  for (int size = 2; size <= amod::kFft; size <<= 1) {
+    const int half = size >> 1;
+    const double sign = inverse ? 1.0 : -1.0;
+    const double angle = sign * 2.0 * M_PI / (double)size;
+    const double wn_re = std::cos(angle), wn_im = std::sin(angle);
+    double w_re = 1.0, w_im = 0.0;
+    for (int j = 0; j < half; ++j) {
+      t[2 * (half - 1 + j)] = w_re;
+      t[2 * (half - 1 + j) + 1] = w_im;
+      const double nw = w_re * wn_re - w_im * wn_im;
+      w_im = w_re * wn_im + w_im * wn_re;
+      w_re = nw;
+    }
+  }
+  return t;
+}
+
+// 512-point transform with the reference's exact rounding (bitReverse + stages)
+void ref_fft512(double *re, double *im, bool inverse) {
+  static const std::vector<double> fw = stage_twiddles(false), bw = stage_twiddles(true);
+  const std::vector<double> &tw = inverse ? bw : fw;
+  const int n = amod::kFft;
+  for (int i = 0; i < n; ++i) {
+    int j = 0;
+    for (int b = 0, x = i; b < 9; ++b, x >>= 1) j = (j << 1) | (x & 1);
+    if (i < j) { std::swap(re[i], re[j]); std::swap(im[i], im[j]); }
+  }
+  for (int half = 1; half < n; half <<= 1) {
+    for (int start = 0; start < n; start += 2 * half) {
+      for (int j = 0; j < half; ++j) {
+        const double wr = tw[2 * (half - 1 + j)], wi = tw[2 * (half - 1 + j) + 1];
+        const int a = start + j, b = a + half;
+        const double tr = wr * re[b] - wi * im[b];
+        const double ti = wr * im[b] + wi * re[b];
+        re[b] = re[a] - tr; im[b] = im[a] - ti;
+        re[a] += tr; im[a] += ti;
+      }
+    }
+  }
+  if (inverse) {
+    const double scale = 1.0 / (double)n;
+    for (int i = 0; i < n; ++i) { re[i] *= scale; im[i] *= scale; }
+  }
+}
+
+void constellation(int mod, int idx, double &re, double &im) { // initConstellation 107-131
+  if (mod == AMOD_BPSK) { re = idx == 0 ? 1.0 : -1.0; im = 0.0; return; }
+  if (mod == AMOD_QPSK) {
+    const double s = 1.0 / M_SQRT2;
+    re = (idx == 0 || idx == 3) ? s : -s;
+    im = (idx <= 1) ? s : -s;
+    return;
+  }
+  const int row = idx >> 2, col = idx & 3;
+  const int gr = row ^ (row >> 1), gc = col ^ (col >> 1);
+  const double s = 1.0 / std::sqrt(10.0);
+  re = (double)(2 * gc - 3) * s;
+  im = (double)(2 * gr - 3) * s;
+}
+int npoints(int mod) { return mod == AMOD_BPSK ? 2 : mod == AMOD_QPSK ? 4 : 16; }
+int bps_of(int mod) { return mod == AMOD_BPSK ? 1 : mod == AMOD_QPSK ? 2 : 4; }
+
+int demap_exact(int mod, double re, double im) { // constellationDemap 140-150
+  double best = INFINITY;
+  int bi = 0;
+  for (int i = 0; i < npoints(mod); ++i) {
+    double pr, pi;
+    constellation(mod, i, pr, pi);
+    const double dr = re - pr, di = im - pi, d = dr * dr + di * di;
+    if (d < best) { best = d; bi = i; }
+  }
+  return bi;
+}
+
+bool is_pilot(const amod_cfg &c, int k) {
+  for (int i = 0; i < c.npilots; ++i)
+    if (c.pilots[i] == k) return true;
+  return false;
+}
+
+// Hermitian-complete a half spectrum, IFFT, prepend the cyclic prefix (modem.js:166-169, 202-208)
+void symbol_from_spectrum(const amod_cfg &c, double *re, double *im, bool zero_dc_im, float *out) {
+  const int n = amod::kFft;
+  for (int k = 1; k < n / 2; ++k) { re[n - k] = re[k]; im[n - k] = -im[k]; }
+  re[0] = 0;
+  if (zero_dc_im) im[0] = 0;
+  else re[n / 2] = 0;
+  im[n / 2] = 0;
+  ref_fft512(re, im, true);
+  for (int i = 0; i < c.cp_len; ++i) out[i] = (float)re[n - c.cp_len + i];
+  for (int i = 0; i < n; ++i) out[c.cp_len + i] = (float)re[i];
+}
+
+// generatePreambleSymbol1/2 and generateChannelEstSymbol (modem.js:158-200)
+void template_symbol(const amod_cfg &c, double seed, int step, float *out, double *known) {
+  double re[amod::kFft] = {0}, im[amod::kFft] = {0};
+  SeededRandom rng(seed);
+  for (int k = c.sub_start; k <= c.sub_end; k += step) {
+    re[k] = rng.next() > 0.5 ? 1.0 : -1.0;
+    if (known) known[k] = re[k];
+  }
+  symbol_from_spectrum(c, re, im, false, out);
+}
+
+// ------------------------------------------------------------------- CRC ---
+uint32_t crc_step_zero(uint32_t r) { // feed one zero byte (reflected 0xEDB88320)
+  for (int j = 0; j < 8; ++j) r = (r & 1) ? (0xEDB88320u ^ (r >> 1)) : (r >> 1);
+  return r;
+}
+const uint32_t *crc_table() {
+  static uint32_t t[256];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (uint32_t i = 0; i < 256; ++i) t[i] = crc_step_zero(i);
+  });
+  return t;
+}
+// operator tables for "advance the register over n zero bytes"
+void shift_operator(int64_t nbytes, uint32_t *op /*4*256*/) {
+  // basis images of the 32 single-bit registers, then byte tables
+  uint32_t basis[32];
+  for (int b = 0; b < 32; ++b) {
+    uint32_t r = 1u << b;
+    for (int64_t i = 0; i < nbytes; ++i) r = crc_table()[r & 0xFF] ^ (r >> 8);
+    basis[b] = r;
+  }
+  for (int byte = 0; byte < 4; ++byte)
+    for (int v = 0; v < 256; ++v) {
+      uint32_t acc = 0;
+      for (int bit = 0; bit < 8; ++bit)
+        if (v & (1 << bit)) acc ^= basis[8 * byte + bit];
+      op[byte * 256 + v] = acc;
+    }
+}
+
+// ---------------------------------------------------------------- device ---
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      g_last_error = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+      return AMOD_ERR_HIP;                                                              \
+    }                                                                                   \
+  } while (0)
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
+    if (e == hipSuccess) n = std::max<size_t>(bytes, 256);
+    return e;
+  }
+};
+
+struct TableSet {
+  DevBuf buf;
+  amod::DevCfg cfg{};
+};
+
+using CfgKey = std::tuple<std::vector<int32_t>>;
+
+std::vector<int32_t> cfg_key(const amod_cfg &c) {
+  std::vector<int32_t> k = {c.fft_size, c.cp_len, c.symbol_len, c.sub_start, c.sub_end, c.npilots,
+                            c.modulation, c.repetition};
+  for (int i = 0; i < c.npilots; ++i) k.push_back(c.pilots[i]);
+  return k;
+}
+
+} // namespace
+
+struct amod_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<std::vector<int32_t>, std::unique_ptr<TableSet>> tables; // per cfg x mode-independent
+  DevBuf crc;          // shared CRC tables
+  DevBuf fb;           // fb_count + list + flags
+  DevBuf xs, bits;     // exact-kernel scratch
+  int64_t xs_stride = 0, bits_stride = 0;
+  int nslots = 0;
+  // host-path staging
+  DevBuf h_samples, h_off, h_len, h_res, h_payload;
+  std::mutex mu;
+  // kernel timing (amod_set_profiling)
+  bool profiling = false;
+  std::vector<std::array<hipEvent_t, 3>> ev_used, ev_free;
+};
+
+namespace {
+
+int fail(amod_ctx *ctx, const std::string &msg, int code) {
+  g_last_error = msg;
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int validate(const amod_cfg *c) {
+  if (!c) return 0;
+  if (c->fft_size != amod::kFft) return 0;
+  if (c->cp_len <= 0 || c->symbol_len != c->fft_size + c->cp_len) return 0;
+  if (c->symbol_len > 768 || c->symbol_len % 4 != 0) return 0; // fine stage tap split / template buffer
+  if (c->sub_start < 1 || c->sub_end >= c->fft_size / 2 || c->sub_start > c->sub_end) return 0;
+  if (c->npilots < 0 || c->npilots > AMOD_MAX_PILOTS) return 0;
+  if (c->modulation < AMOD_BPSK || c->modulation > AMOD_QAM16) return 0;
+  if (c->repetition < 1) return 0;
+  if (amod_num_data_subs(c) <= 0) return 0;
+  return 1;
+}
+
+int build_crc(amod_ctx *ctx) {
+  if (ctx->crc.p) return AMOD_SUCCESS;
+  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024);
+  uint32_t *s4 = h.data(), *m1 = s4 + 1024, *m2 = m1 + 32 * 1024, *mb = m2 + 32 * 1024;
+  const uint32_t *t0 = crc_table();
+  for (int i = 0; i < 256; ++i) s4[i] = t0[i];
+  for (int k = 1; k < 4; ++k)
+    for (int i = 0; i < 256; ++i) s4[k * 256 + i] = (s4[(k - 1) * 256 + i] >> 8) ^ t0[s4[(k - 1) * 256 + i] & 0xFF];
+  for (int q = 0; q < 32; ++q) {
+    shift_operator((int64_t)amod::kCrcChunk * q, m1 + q * 1024);
+    shift_operator((int64_t)amod::kCrcChunk * 32 * q, m2 + q * 1024);
+  }
+  shift_operator(amod::kCrcBlock, mb);
+  HIP_TRY(ctx->crc.ensure(h.size() * 4));
+  HIP_TRY(hipMemcpy(ctx->crc.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  return AMOD_SUCCESS;
+}
+
+int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
+  int rc = build_crc(ctx);
+  if (rc) return rc;
+  auto key = cfg_key(*c);
+  auto it = ctx->tables.find(key);
+  if (it == ctx->tables.end()) {
+    auto ts = std::make_unique<TableSet>();
+    amod::DevCfg &d = ts->cfg;
+    const int sym = c->symbol_len, nband = c->sub_end - c->sub_start + 1;
+    d.cp = c->cp_len; d.sym = sym; d.sub_start = c->sub_start; d.sub_end = c->sub_end; d.nband = nband;
+    d.npilots = c->npilots; d.ndata = amod_num_data_subs(c); d.bps = bps_of(c->modulation);
+    d.mod = c->modulation; d.rep = c->repetition;
+    for (int i = 0; i < c->npilots; ++i) d.pilots[i] = c->pilots[i];
+    d.origin_idx = demap_exact(c->modulation, 0.0, 0.0);
+    const char *g = getenv("AMOD_GUARD_SCALE");
+    d.guard = g ? (float)atof(g) : 1.0f;
+    // host images
+    std::vector<float> pre1(sym), ce(sym);
+    double known_full[amod::kFft] = {0};
+    template_symbol(*c, 42.0, 2, pre1.data(), nullptr);
+    template_symbol(*c, 44.0, 1, ce.data(), known_full);
+    double te = 0.0;
+    for (int i = 0; i < sym; ++i) te += (double)pre1[i] * (double)pre1[i];
+    d.te = te; d.te_f = (float)te;
+    std::vector<float> known(nband);
+    std::vector<int16_t> band_di(nband);
+    int di = 0;
+    for (int b = 0; b < nband; ++b) {
+      const int k = c->sub_start + b;
+      known[b] = (float)known_full[k];
+      band_di[b] = is_pilot(*c, k) ? (int16_t)-1 : (int16_t)di++;
+    }
+    std::vector<float> tw1(2 * 8 * 64), tw2(2 * 8 * 8);
+    for (int q = 0; q < 8; ++q)
+      for (int l = 0; l < 64; ++l) {
+        const double a = -2.0 * M_PI * (double)((l * q) % amod::kFft) / amod::kFft;
+        tw1[2 * (q * 64 + l)] = (float)std::cos(a); tw1[2 * (q * 64 + l) + 1] = (float)std::sin(a);
+      }
+    for (int p = 0; p < 8; ++p)
+      for (int l1 = 0; l1 < 8; ++l1) {
+        const double a = -2.0 * M_PI * (double)((8 * l1 * p) % amod::kFft) / amod::kFft;
+        tw2[2 * (p * 8 + l1)] = (float)std::cos(a); tw2[2 * (p * 8 + l1) + 1] = (float)std::sin(a);
+      }
+    const std::vector<double> twx = stage_twiddles(false);
+    std::vector<double> pts(2 * 16, 0.0);
+    for (int i = 0; i < npoints(c->modulation); ++i) constellation(c->modulation, i, pts[2 * i], pts[2 * i + 1]);
+    // one device allocation, 256-byte aligned pieces
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_pre1 = carve(sym * 4), o_tw1 = carve(tw1.size() * 4), o_tw2 = carve(tw2.size() * 4),
+                 o_twx = carve(twx.size() * 8), o_known = carve(nband * 4), o_di = carve(nband * 2),
+                 o_pts = carve(pts.size() * 8);
+    if (ts->buf.ensure(off) != hipSuccess) return fail(ctx, "hipMalloc(tables)", AMOD_ERR_NOMEM);
+    char *base = (char *)ts->buf.p;
+    HIP_TRY(hipMemcpy(base + o_pre1, pre1.data(), sym * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_tw1, tw1.data(), tw1.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_tw2, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_twx, twx.data(), twx.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_known, known.data(), nband * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_di, band_di.data(), nband * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_pts, pts.data(), pts.size() * 8, hipMemcpyHostToDevice));
+    d.t.pre1 = (const float *)(base + o_pre1);
+    d.t.tw1 = (const float2 *)(base + o_tw1);
+    d.t.tw2 = (const float2 *)(base + o_tw2);
+    d.t.tw_exact = (const double2 *)(base + o_twx);
+    d.t.known = (const float *)(base + o_known);
+    d.t.band_di = (const int16_t *)(base + o_di);
+    d.t.points = (const double2 *)(base + o_pts);
+    const uint32_t *crc = (const uint32_t *)ctx->crc.p;
+    d.t.crc_s4 = crc;
+    d.t.crc_m1 = crc + 1024;
+    d.t.crc_m2 = crc + 1024 + 32 * 1024;
+    d.t.crc_mb = crc + 1024 + 64 * 1024;
+    it = ctx->tables.emplace(key, std::move(ts)).first;
+  }
+  out = it->second->cfg;
+  return AMOD_SUCCESS;
+}
+
+int64_t max_bits_for(const amod_cfg *c, int64_t max_len) {
+  return (max_len / c->symbol_len) * (int64_t)amod_num_data_subs(c) * bps_of(c->modulation);
+}
+
+int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
+  if (max_len < 0) { // device path: keep what amod_reserve set up, or size from a default
+    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 2 * (size_t)std::max(nframes, 1))));
+    if (ctx->nslots > 0) return AMOD_SUCCESS;
+    max_len = 65536;
+  }
+  const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
+      std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
+  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 2 * (size_t)std::max(nframes, 1))));
+  const int64_t xs_stride = (max_len + 64) & ~int64_t(63);
+  const int64_t words = (max_bits_for(c, max_len) + 31) / 32;
+  const int64_t bits_stride = ((2 * words + 32) + 63) & ~int64_t(63);
+  if (ctx->nslots < nslots || ctx->xs_stride < xs_stride) {
+    HIP_TRY(ctx->xs.ensure(sizeof(float) * (size_t)(nslots * xs_stride)));
+    ctx->xs_stride = xs_stride;
+  }
+  if (ctx->nslots < nslots || ctx->bits_stride < bits_stride) {
+    HIP_TRY(ctx->bits.ensure(sizeof(uint32_t) * (size_t)(nslots * bits_stride)));
+    ctx->bits_stride = bits_stride;
+  }
+  ctx->nslots = std::max<int>(ctx->nslots, (int)nslots);
+  return AMOD_SUCCESS;
+}
+
+int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, const int64_t *offsets,
+                const int32_t *lengths, int32_t nframes, amod_result *results, uint8_t *payload,
+                int64_t payload_stride, uint32_t options, hipStream_t stream, amod_debug *debug,
+                int64_t max_len) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  if (!validate(cfg)) return fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  if (mode != AMOD_MODE_RECEIVED && mode != AMOD_MODE_CHUNK) return fail(ctx, "invalid mode", AMOD_ERR_ARG);
+  if (nframes < 0) return fail(ctx, "nframes < 0", AMOD_ERR_ARG);
+  if (nframes == 0) return AMOD_SUCCESS;
+  if (payload_stride < 16 || payload_stride % 16) return fail(ctx, "payload_stride must be a positive multiple of 16", AMOD_ERR_ARG);
+  HIP_TRY(hipSetDevice(ctx->device));
+  amod::DevCfg d;
+  int rc = get_tables(ctx, cfg, d);
+  if (rc) return rc;
+  d.mode = mode;
+  rc = reserve(ctx, cfg, nframes, max_len);
+  if (rc) return rc;
+  hipStream_t s = stream ? stream : ctx->stream;
+  amod::DevWork w{};
+  w.samples = samples; w.off = offsets; w.len = lengths; w.nframes = nframes;
+  w.res = results; w.payload = payload; w.stride = payload_stride; w.dbg = debug;
+  int32_t *fb = (int32_t *)ctx->fb.p;
+  w.fb_count = fb; w.fb_list = fb + 64; w.fb_flags = fb + 64 + nframes;
+  w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
+  w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
+  w.options = options;
+  HIP_TRY(hipMemsetAsync(fb, 0, 256, s));
+  std::array<hipEvent_t, 3> ev{};
+  if (ctx->profiling) {
+    if (ctx->ev_free.empty()) {
+      for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    } else {
+      ev = ctx->ev_free.back();
+      ctx->ev_free.pop_back();
+    }
+    HIP_TRY(hipEventRecord(ev[0], s));
+  }
+  HIP_TRY(amod_launch_fast(d, w, s));
+  if (ctx->profiling) HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(amod_launch_exact(d, w, std::min(ctx->nslots, nframes), s));
+  if (ctx->profiling) {
+    HIP_TRY(hipEventRecord(ev[2], s));
+    ctx->ev_used.push_back(ev);
+  }
+  return AMOD_SUCCESS;
+}
+
+// ----------------------------------------------------------------- TX -----
+// modulateOFDM (modem.js:322-362) of a bit vector; appends symbols to out
+void modulate(const amod_cfg &c, const std::vector<uint8_t> &bits, std::vector<float> &out) {
+  const int bps = bps_of(c.modulation), per_sym = amod_num_data_subs(&c) * bps;
+  const size_t nsym = (bits.size() + per_sym - 1) / per_sym;
+  const int n = amod::kFft;
+  for (size_t s = 0; s < nsym; ++s) {
+    double re[amod::kFft] = {0}, im[amod::kFft] = {0};
+    int di = 0;
+    for (int k = c.sub_start; k <= c.sub_end; ++k) {
+      if (is_pilot(c, k)) { re[k] = 1; im[k] = 0; continue; }
+      int idx = 0;
+      for (int b = 0; b < bps; ++b) {
+        const size_t pos = s * per_sym + (size_t)di * bps + b;
+        idx = (idx << 1) | (pos < bits.size() ? (bits[pos] & 1) : 0);
+      }
+      constellation(c.modulation, idx % npoints(c.modulation), re[k], im[k]);
+      ++di;
+    }
+    const size_t o = out.size();
+    out.resize(o + c.symbol_len);
+    (void)n;
+    symbol_from_spectrum(c, re, im, true, out.data() + o);
+  }
+}
+
+int64_t assemble_frame(const amod_cfg &c, const std::vector<uint8_t> &payload, int pre, int post, float *out) {
+  std::vector<uint8_t> bits;
+  bits.reserve(payload.size() * 8 * c.repetition);
+  for (uint8_t byte : payload)
+    for (int b = 7; b >= 0; --b)
+      for (int r = 0; r < c.repetition; ++r) bits.push_back((byte >> b) & 1);
+  const int bps = bps_of(c.modulation), per_sym = amod_num_data_subs(&c) * bps;
+  const int64_t nsym = ((int64_t)bits.size() + per_sym - 1) / per_sym;
+  const int64_t total = pre + (3 + nsym) * (int64_t)c.symbol_len + post;
+  if (!out) return total;
+  std::fill(out, out + total, 0.0f);
+  template_symbol(c, 42.0, 2, out + pre, nullptr);
+  template_symbol(c, 43.0, 1, out + pre + c.symbol_len, nullptr);
+  template_symbol(c, 44.0, 1, out + pre + 2 * c.symbol_len, nullptr);
+  std::vector<float> data;
+  modulate(c, bits, data);
+  std::copy(data.begin(), data.end(), out + pre + 3 * c.symbol_len);
+  double mx = 0.0;
+  for (int64_t i = 0; i < total; ++i) mx = std::max(mx, std::fabs((double)out[i]));
+  if (mx > 0) {
+    const double s = 0.8 / mx;
+    for (int64_t i = 0; i < total; ++i) out[i] = (float)((double)out[i] * s);
+  }
+  return total;
+}
+
+void put_be32(std::vector<uint8_t> &p, int32_t v) {
+  p.push_back((uint8_t)((v >> 24) & 0xFF)); p.push_back((uint8_t)((v >> 16) & 0xFF));
+  p.push_back((uint8_t)((v >> 8) & 0xFF)); p.push_back((uint8_t)(v & 0xFF));
+}
+
+std::vector<uint8_t> legacy_packet(const uint8_t *data, int32_t len, const uint8_t *name, int32_t name_len) {
+  name_len = std::min(name_len, 255);
+  std::vector<uint8_t> p;
+  p.reserve(1 + name_len + 8 + len);
+  p.push_back((uint8_t)name_len);
+  p.insert(p.end(), name, name + name_len);
+  put_be32(p, len);
+  p.insert(p.end(), data, data + len);
+  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
+  return p;
+}
+
+int silence_len(const amod_cfg &c, double seconds_std, double seconds_ac) {
+  return (int)((double)c.sample_rate * (c.cp_len >= 128 ? seconds_ac : seconds_std));
+}
+int rounded_silence(const amod_cfg &c, double seconds) {
+  return (int)std::floor((double)c.sample_rate * seconds + 0.5);
+}
+
+} // namespace
+
+// =============================================================== C ABI =====
+extern "C" {
+
+int amod_abi_version(void) { return AMOD_ABI_VERSION; }
+
+int amod_open(int device, amod_ctx **out) {
+  if (!out) return fail(nullptr, "null out", AMOD_ERR_ARG);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(nullptr, "no HIP device", AMOD_ERR_NODEV);
+  if (device < 0 || device >= n) return fail(nullptr, "device index out of range", AMOD_ERR_NODEV);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(nullptr, std::string("device is ") + prop.gcnArchName + ", libamodem is built for gfx950", AMOD_ERR_NODEV);
+  HIP_TRY(hipSetDevice(device));
+  auto *ctx = new amod_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return fail(nullptr, "hipStreamCreate failed", AMOD_ERR_HIP);
+  }
+  *out = ctx;
+  return AMOD_SUCCESS;
+}
+
+int amod_close(amod_ctx *ctx) {
+  if (!ctx) return AMOD_SUCCESS;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return AMOD_SUCCESS;
+}
+
+const char *amod_last_error(const amod_ctx *ctx) {
+  if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+  return g_last_error.c_str();
+}
+
+int amod_config_preset(const char *name, int32_t modulation, int32_t repetition, amod_cfg *out) {
+  if (!out) return fail(nullptr, "null out", AMOD_ERR_ARG);
+  if (modulation < AMOD_BPSK || modulation > AMOD_QAM16) return fail(nullptr, "bad modulation", AMOD_ERR_ARG);
+  std::memset(out, 0, sizeof *out);
+  static const int std_p[] = {15, 29, 43, 57, 71, 85, 99, 113, 127, 141, 155, 169, 183, 197, 211, 225};
+  static const int ac_p[] = {25, 35, 45, 55, 65, 75, 85};
+  static const int nb_p[] = {37, 45, 53};
+  const int *p = std_p;
+  int np = 16;
+  out->fft_size = 512;
+  out->sample_rate = 44100;
+  const std::string n = name ? name : "";
+  if (n == "acoustic") { out->cp_len = 128; out->sub_start = 23; out->sub_end = 93; p = ac_p; np = 7; }
+  else if (n == "narrowband") { out->cp_len = 256; out->sub_start = 35; out->sub_end = 58; p = nb_p; np = 3; }
+  else { out->cp_len = 64; out->sub_start = 12; out->sub_end = 232; }
+  out->symbol_len = out->fft_size + out->cp_len;
+  out->npilots = np;
+  for (int i = 0; i < np; ++i) out->pilots[i] = p[i];
+  out->modulation = modulation;
+  out->repetition = repetition < 1 ? 1 : repetition;
+  return AMOD_SUCCESS;
+}
+
+int32_t amod_num_data_subs(const amod_cfg *c) {
+  if (!c) return 0;
+  int32_t n = 0;
+  for (int k = c->sub_start; k <= c->sub_end; ++k) n += !is_pilot(*c, k);
+  return n;
+}
+
+int32_t amod_estimate_frame_samples(const amod_cfg *c, int32_t payload_bytes) {
+  if (!c) return 0;
+  const double per_sym = (double)amod_num_data_subs(c) * bps_of(c->modulation);
+  const double total = (double)payload_bytes * 8.0 * (double)std::max(1, c->repetition);
+  return (3 + (int32_t)std::ceil(total / per_sym)) * c->symbol_len;
+}
+
+int64_t amod_payload_stride(const amod_cfg *c, int64_t max_len) {
+  if (!c || max_len < 0) return 16;
+  const int64_t bytes = max_bits_for(c, max_len) / 8 + 16;
+  return (bytes + 15) & ~int64_t(15);
+}
+
+int amod_reserve(amod_ctx *ctx, const amod_cfg *cfg, int32_t nframes, int64_t max_len) {
+  if (!ctx || !validate(cfg)) return fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  amod::DevCfg d;
+  int rc = get_tables(ctx, cfg, d);
+  if (rc) return rc;
+  return reserve(ctx, cfg, nframes, max_len);
+}
+
+int amod_decode_device(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                       const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
+                       uint8_t *payload, int64_t payload_stride, uint32_t options, void *stream) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return decode_impl(ctx, cfg, mode, samples, offsets, lengths, nframes, results, payload, payload_stride, options,
+                     (hipStream_t)stream, nullptr, -1);
+}
+
+int amod_decode_device_debug(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                             const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                             amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options,
+                             void *stream, amod_debug *debug) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return decode_impl(ctx, cfg, mode, samples, offsets, lengths, nframes, results, payload, payload_stride, options,
+                     (hipStream_t)stream, debug, -1);
+}
+
+int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, int64_t nsamples,
+                     const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
+                     uint8_t *payload, int64_t payload_stride, uint32_t options) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  if (nframes < 0 || nsamples < 0) return fail(ctx, "negative size", AMOD_ERR_ARG);
+  for (int32_t i = 0; i < nframes; ++i)
+    if (offsets[i] < 0 || lengths[i] < 0 || offsets[i] + lengths[i] > nsamples)
+      return fail(ctx, "frame " + std::to_string(i) + " lies outside the sample buffer", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (nframes == 0) return AMOD_SUCCESS;
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(ctx->h_samples.ensure(sizeof(float) * (size_t)(nsamples + 4)));
+  HIP_TRY(ctx->h_off.ensure(sizeof(int64_t) * (size_t)nframes));
+  HIP_TRY(ctx->h_len.ensure(sizeof(int32_t) * (size_t)nframes));
+  HIP_TRY(ctx->h_res.ensure(sizeof(amod_result) * (size_t)nframes));
+  HIP_TRY(ctx->h_payload.ensure((size_t)payload_stride * (size_t)nframes));
+  hipStream_t s = ctx->stream;
+  if (nsamples) HIP_TRY(hipMemcpyAsync(ctx->h_samples.p, samples, sizeof(float) * nsamples, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_off.p, offsets, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_len.p, lengths, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
+  int64_t max_len = 0;
+  for (int32_t i = 0; i < nframes; ++i) max_len = std::max<int64_t>(max_len, lengths[i]);
+  int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p,
+                       (const int32_t *)ctx->h_len.p, nframes, (amod_result *)ctx->h_res.p,
+                       (uint8_t *)ctx->h_payload.p, payload_stride, options, s, nullptr, max_len);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(results, ctx->h_res.p, sizeof(amod_result) * nframes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(payload, ctx->h_payload.p, (size_t)payload_stride * nframes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return AMOD_SUCCESS;
+}
+
+int amod_synchronize(amod_ctx *ctx) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return AMOD_SUCCESS;
+}
+
+int amod_set_profiling(amod_ctx *ctx, int enable) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->profiling = enable != 0;
+  return AMOD_SUCCESS;
+}
+
+int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_n, double *exact_ms, int64_t *exact_n) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  double f = 0, x = 0;
+  for (auto &ev : ctx->ev_used) {
+    HIP_TRY(hipEventSynchronize(ev[2]));
+    float a = 0, b = 0;
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    f += a; x += b;
+    ctx->ev_free.push_back(ev);
+  }
+  if (fast_ms) *fast_ms = f;
+  if (exact_ms) *exact_ms = x;
+  if (fast_n) *fast_n = (int64_t)ctx->ev_used.size();
+  if (exact_n) *exact_n = (int64_t)ctx->ev_used.size();
+  ctx->ev_used.clear();
+  return AMOD_SUCCESS;
+}
+
+uint32_t amod_crc32(const uint8_t *d, size_t n) {
+  const uint32_t *t = crc_table();
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = t[(c ^ d[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+int amod_preamble1(const amod_cfg *cfg, float *out) {
+  if (!validate(cfg) || !out) return fail(nullptr, "invalid argument", AMOD_ERR_ARG);
+  template_symbol(*cfg, 42.0, 2, out, nullptr);
+  return AMOD_SUCCESS;
+}
+
+int64_t amod_tx_legacy(const amod_cfg *cfg, const uint8_t *data, int32_t len, const uint8_t *name, int32_t name_len,
+                       float *out) {
+  if (!validate(cfg) || len < 0 || name_len < 0) return AMOD_ERR_ARG;
+  const auto p = legacy_packet(data, len, name, name_len);
+  return assemble_frame(*cfg, p, silence_len(*cfg, 0.3, 0.5), silence_len(*cfg, 0.2, 0.5), out);
+}
+
+int64_t amod_tx_meta(const amod_cfg *cfg, int32_t total_chunks, int32_t total_size, int32_t chunk_size,
+                     const uint8_t *name, int32_t name_len, float *out) {
+  if (!validate(cfg) || name_len < 0) return AMOD_ERR_ARG;
+  name_len = std::min(name_len, 255);
+  std::vector<uint8_t> p = {0xFE};
+  put_be32(p, total_chunks);
+  put_be32(p, total_size);
+  p.push_back((uint8_t)((chunk_size >> 8) & 0xFF));
+  p.push_back((uint8_t)(chunk_size & 0xFF));
+  p.push_back((uint8_t)name_len);
+  p.insert(p.end(), name, name + name_len);
+  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
+  const int pre = rounded_silence(*cfg, cfg->cp_len >= 128 ? 0.5 : 0.3);
+  return assemble_frame(*cfg, p, pre, rounded_silence(*cfg, 0.02), out);
+}
+
+int64_t amod_tx_chunk(const amod_cfg *cfg, const uint8_t *data, int32_t len, int32_t seq, float *out) {
+  if (!validate(cfg) || len < 0) return AMOD_ERR_ARG;
+  std::vector<uint8_t> p = {0xFF};
+  put_be32(p, seq);
+  p.push_back((uint8_t)((len >> 8) & 0xFF));
+  p.push_back((uint8_t)(len & 0xFF));
+  p.insert(p.end(), data, data + len);
+  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
+  return assemble_frame(*cfg, p, rounded_silence(*cfg, 0.05), rounded_silence(*cfg, 0.02), out);
+}
+
+int64_t amod_tx_test_signal(const amod_cfg *cfg, float *out) {
+  uint8_t d[16];
+  for (int i = 0; i < 16; ++i) d[i] = (uint8_t)i;
+  return amod_tx_legacy(cfg, d, 16, (const uint8_t *)"test", 4, out);
+}
+
+void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out) {
+  uint32_t s = seed;
+  for (int32_t i = 0; i < len; ++i) {
+    if ((i & 3) == 0) { s ^= s << 13; s ^= s >> 17; s ^= s << 5; }
+    out[i] = (uint8_t)((s >> (8 * (i & 3))) & 0xFF);
+  }
+}
+
+int64_t amod_synth_legacy_batch(const amod_cfg *cfg, int32_t nframes, int32_t first, int32_t payload_len,
+                                const uint8_t *name, int32_t name_len, float *out, int64_t *offsets,
+                                int32_t *lengths, int32_t threads) {
+  if (!validate(cfg) || nframes < 0 || payload_len < 0) return AMOD_ERR_ARG;
+  // every frame has the same length (same payload size and name)
+  std::vector<uint8_t> tmp(payload_len);
+  const auto probe = legacy_packet(tmp.data(), payload_len, name, name_len);
+  const int64_t flen = amod_tx_legacy(cfg, tmp.data(), payload_len, name, name_len, nullptr);
+  (void)probe;
+  const int64_t total = flen * nframes;
+  if (!out) return total;
+  for (int32_t i = 0; i < nframes; ++i) { offsets[i] = flen * i; lengths[i] = (int32_t)flen; }
+  int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = std::min<int>(nt, std::max(1, nframes));
+  std::atomic<int32_t> next{0};
+  auto work = [&] {
+    std::vector<uint8_t> data(payload_len);
+    for (;;) {
+      const int32_t i = next.fetch_add(1);
+      if (i >= nframes) break;
+      amod_synth_payload(0x9E3779B9u ^ (uint32_t)(first + i), payload_len, data.data());
+      amod_tx_legacy(cfg, data.data(), payload_len, name, name_len, out + flen * i);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto &t : pool) t.join();
+  return total;
+}
+
+} // extern "C"

@@ -1,0 +1,199 @@
+/*
+ * amodem.h — C ABI of the MI355X-native OFDM demodulator (libamodem.so).
+ *
+ * Drop-in engine behind the receive half of playok/audio-modem's modem.js.
+ * Plain C types only; no exceptions, no torch types. Every entry point returns
+ * an int status (AMOD_SUCCESS or a negative AMOD_ERR_*); per-frame decode
+ * outcomes are reported in amod_result.status using the reference's error set.
+ *
+ * Reference interfaces each entry point replaces (file:line in modem.js):
+ *   amod_decode_*(mode = AMOD_MODE_RECEIVED) ... decodeReceivedSignal   modem.js:557-654
+ *   amod_decode_*(mode = AMOD_MODE_CHUNK)    ... decodeChunkFrame       modem.js:770-803
+ *   amod_config_preset                       ... OFDM_CONFIGS / setOFDMConfig modem.js:69-98
+ *   amod_estimate_frame_samples              ... estimateFrameSamples   modem.js:863-874
+ *   amod_crc32                               ... crc32                  modem.js:443-457
+ *   amod_tx_legacy / amod_tx_meta / amod_tx_chunk / amod_tx_test_signal
+ *                                            ... buildTransmitSignal 498-555, buildMetadataFrame 758,
+ *                                                buildDataChunkFrame 763, generateTestSignal 914-973
+ *   amod_preamble1                           ... generatePreambleSymbol1 modem.js:158-170
+ * The reference's JS binds none of these today; INTEGRATION.md shows the N-API
+ * binding (audio-modem_amd/csrc/napi_amodem.c) a maintainer adds.
+ */
+#ifndef AMODEM_H
+#define AMODEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMOD_ABI_VERSION 1
+#define AMOD_MAX_PILOTS 32
+
+/* ---- API status (return values) ---- */
+#define AMOD_SUCCESS 0
+#define AMOD_ERR_ARG (-1)     /* invalid argument / config                     */
+#define AMOD_ERR_HIP (-2)     /* HIP runtime failure (see amod_last_error)     */
+#define AMOD_ERR_NOMEM (-3)   /* device or host allocation failed              */
+#define AMOD_ERR_NODEV (-4)   /* no usable gfx950 device                       */
+
+/* ---- modulations (Constellations, modem.js:101-105) ---- */
+#define AMOD_BPSK 0
+#define AMOD_QPSK 1
+#define AMOD_QAM16 2
+
+/* ---- decode modes ---- */
+#define AMOD_MODE_RECEIVED 0 /* decodeReceivedSignal: preprocess + detect + demod + parse */
+#define AMOD_MODE_CHUNK 1    /* decodeChunkFrame: frame starts at preamble 1             */
+
+/* ---- decode option bits ---- */
+#define AMOD_OPT_FORCE_EXACT 1u /* run every frame through the exact-replica kernel */
+
+/* ---- per-frame status (the reference's error strings, modem.js) ---- */
+#define AMOD_OK 0
+#define AMOD_E_PREAMBLE 1        /* 'Preamble not detected'                     */
+#define AMOD_E_LOW_CORR 2        /* 'Preamble not detected (low correlation)'   */
+#define AMOD_E_SHORT_CE 3        /* 'Signal too short for CE'                   */
+#define AMOD_E_NO_DATA 4         /* 'No data after CE'                          */
+#define AMOD_E_DECODED_SHORT 5   /* 'Decoded data too short'                    */
+#define AMOD_E_SHORT_HEADER 6    /* 'Decoded data too short for header'         */
+#define AMOD_E_INVALID_LEN 7     /* `Invalid data length: ${aux}`               */
+#define AMOD_E_META_SHORT 8      /* 'Metadata frame too short'                  */
+#define AMOD_E_META_TRUNC 9      /* 'Metadata frame truncated'                  */
+#define AMOD_E_CHUNK_SHORT 10    /* 'Data chunk frame too short'                */
+#define AMOD_E_CHUNK_TRUNC 11    /* 'Data chunk truncated'                      */
+#define AMOD_E_FRAME_SHORT_CE 12 /* 'Frame too short for CE'                    */
+#define AMOD_E_UNKNOWN_TYPE 13   /* `Unknown frame type: 0x${aux.toString(16)}` */
+#define AMOD_E_CAPACITY 100      /* not a reference outcome: the frame exceeds the workspace
+                                    reserved by amod_reserve (device path); reserve more  */
+
+/* ---- amod_result.flags: why a frame was (re)decoded by the exact kernel ---- */
+#define AMOD_FLAG_FORCED (1 << 0)    /* AMOD_OPT_FORCE_EXACT                        */
+#define AMOD_FLAG_NONFINITE (1 << 1) /* NaN/Inf samples                             */
+#define AMOD_FLAG_BIG (1 << 2)       /* frame longer than the LDS-resident capacity */
+#define AMOD_FLAG_COARSE (1 << 3)    /* Schmidl-Cox decision within guard band      */
+#define AMOD_FLAG_FINE (1 << 4)      /* fine-timing argmax within guard band        */
+#define AMOD_FLAG_CHANNEL (1 << 5)   /* |H|^2 near the 1e-10 threshold              */
+#define AMOD_FLAG_PHASE (1 << 6)     /* pilot |eqRe| near the 1e-6 threshold        */
+#define AMOD_FLAG_DEMAP (1 << 7)     /* a constellation decision within guard band  */
+#define AMOD_FLAG_THRESH (1 << 8)    /* preprocess peak near the 1e-6 threshold     */
+#define AMOD_FLAG_EXACT (1 << 15)    /* result produced by the exact-replica kernel */
+
+/* OFDM parameters + modulation; mirrors OFDM (modem.js:69-98) */
+typedef struct amod_cfg {
+  int32_t fft_size; /* must be 512 */
+  int32_t cp_len;
+  int32_t symbol_len; /* fft_size + cp_len */
+  int32_t sample_rate;
+  int32_t sub_start, sub_end; /* in-band subcarriers, inclusive; sub_end < fft_size/2 */
+  int32_t npilots;
+  int32_t pilots[AMOD_MAX_PILOTS];
+  int32_t modulation; /* AMOD_BPSK / AMOD_QPSK / AMOD_QAM16 */
+  int32_t repetition; /* >= 1 (majorityVote n) */
+} amod_cfg;
+
+/* One record per frame (96 bytes). Offsets index the frame's payload slot. */
+typedef struct amod_result {
+  int32_t status;       /* AMOD_OK or AMOD_E_*                                           */
+  int32_t preamble_idx; /* startIdx (RECEIVED mode); -1 when the reference omits it      */
+  int32_t coarse_idx;   /* Schmidl-Cox index (exact kernel: bit-exact; fast: in plateau) */
+  int32_t frame_type;   /* 0 legacy, 0xFE meta, 0xFF data, other byte / -1 if none       */
+  int32_t aux;          /* dataLen for AMOD_E_INVALID_LEN, type byte for UNKNOWN_TYPE    */
+  int32_t nbytes;       /* decoded bytes (after vote) stored in the payload slot         */
+  int32_t name_off, name_len;
+  int32_t data_off, data_len;
+  int32_t seq_num, total_chunks, total_size, chunk_size;
+  uint32_t expected_crc, actual_crc;
+  int32_t crc_valid;
+  int32_t nbits;       /* demodulated bits before vote                                  */
+  int32_t flags;       /* AMOD_FLAG_*                                                   */
+  float fine_metric;   /* best normalised cross-correlation                             */
+  int32_t reserved[4];
+} amod_result;
+
+typedef struct amod_ctx amod_ctx;
+
+/* ---- lifecycle ---- */
+int amod_open(int device, amod_ctx **out); /* binds a HIP device; own stream + workspace */
+int amod_close(amod_ctx *ctx);
+const char *amod_last_error(const amod_ctx *ctx); /* NULL ctx: last global error */
+int amod_abi_version(void);
+
+/* ---- configuration & sizing ---- */
+/* name: 'standard' | 'acoustic' | 'narrowband' (unknown -> standard, modem.js:96) */
+int amod_config_preset(const char *name, int32_t modulation, int32_t repetition, amod_cfg *out);
+int32_t amod_num_data_subs(const amod_cfg *cfg);
+int32_t amod_estimate_frame_samples(const amod_cfg *cfg, int32_t payload_bytes);
+/* bytes each frame's payload slot needs for frames up to max_frame_len samples */
+int64_t amod_payload_stride(const amod_cfg *cfg, int64_t max_frame_len);
+/* pre-size the workspace so a later decode of this shape allocates nothing
+   (required before capturing amod_decode_device into a hipGraph) */
+int amod_reserve(amod_ctx *ctx, const amod_cfg *cfg, int32_t nframes, int64_t max_frame_len);
+
+/* ---- decode ----
+ * Frames are slices [offsets[i], offsets[i]+lengths[i]) of one float32 sample
+ * buffer. Results go to results[i]; decoded bytes to payload + i*payload_stride.
+ * amod_decode_device: every pointer is device memory; enqueued on `stream`
+ * (hipStream_t, NULL = the context's stream); returns without synchronising.
+ * amod_decode_host: host pointers; copies over PCIe and synchronises.
+ * debug (device, optional): per-frame amod_debug records for parity tests.   */
+int amod_decode_device(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                       const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                       amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options,
+                       void *stream);
+int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                     int64_t nsamples, const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                     amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options);
+int amod_synchronize(amod_ctx *ctx);
+
+/* kernel timing: when enabled, every decode brackets k_decode_fast and
+   k_decode_exact with hipEvents on the launch stream; amod_kernel_times waits
+   for them, returns the accumulated milliseconds and launch counts, and resets */
+int amod_set_profiling(amod_ctx *ctx, int enable);
+int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_launches, double *exact_ms,
+                      int64_t *exact_launches);
+
+/* parity-test view of one frame's intermediates (filled when debug != NULL) */
+#define AMOD_DBG_BAND 256
+#define AMOD_DBG_SYMS 256
+typedef struct amod_debug {
+  double mean, mx;             /* preprocess                                    */
+  double coarse_metric;        /* best Schmidl-Cox metric                       */
+  int32_t coarse_lo, coarse_hi; /* candidate plateau [lo, hi]                   */
+  double fine_metric;
+  int32_t fine_idx, nsym;
+  double h_re[AMOD_DBG_BAND], h_im[AMOD_DBG_BAND];   /* channel estimate, band order */
+  double x_re[AMOD_DBG_BAND], x_im[AMOD_DBG_BAND];   /* FFT of data symbol 0 (band)  */
+  double eq_re[AMOD_DBG_BAND], eq_im[AMOD_DBG_BAND]; /* equalised symbol 0 (band)    */
+  double phase[AMOD_DBG_SYMS];                       /* pilot phase per data symbol  */
+} amod_debug;
+int amod_decode_device_debug(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                             const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                             amod_result *results, uint8_t *payload, int64_t payload_stride,
+                             uint32_t options, void *stream, amod_debug *debug);
+
+/* ---- host utilities (reference-equivalent, bit-exact) ---- */
+uint32_t amod_crc32(const uint8_t *data, size_t n);
+int amod_preamble1(const amod_cfg *cfg, float *out); /* symbol_len floats */
+/* transmit builders for synthetic input; return sample count, out may be NULL to size */
+int64_t amod_tx_legacy(const amod_cfg *cfg, const uint8_t *data, int32_t len, const uint8_t *name,
+                       int32_t name_len, float *out);
+int64_t amod_tx_meta(const amod_cfg *cfg, int32_t total_chunks, int32_t total_size, int32_t chunk_size,
+                     const uint8_t *name, int32_t name_len, float *out);
+int64_t amod_tx_chunk(const amod_cfg *cfg, const uint8_t *data, int32_t len, int32_t seq, float *out);
+int64_t amod_tx_test_signal(const amod_cfg *cfg, float *out);
+/* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
+void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
+/* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),
+   laid out back to back in out; offsets/lengths filled; threads <= 0 -> hardware threads.
+   Returns total samples (out NULL: sizing only). */
+int64_t amod_synth_legacy_batch(const amod_cfg *cfg, int32_t nframes, int32_t first, int32_t payload_len,
+                                const uint8_t *name, int32_t name_len, float *out, int64_t *offsets,
+                                int32_t *lengths, int32_t threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMODEM_H */

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP decoder (fast path and exact-replica path) against the
+reference's golden outputs and the CPU oracle, through the C ABI.
+
+Bar: result objects, payload bytes, CRCs and preamble indices bit-exact;
+intermediates (FFT bins, channel estimate, equalised IQ, pilot phase) of the
+fp32 fast path within ABS_TOL of the fp64 reference; the exact path bit-exact
+in every intermediate, the Schmidl-Cox coarse index included.
+"""
+import numpy as np
+import pytest
+
+from helpers import frames, ref_dict, struct_to_dict
+
+import amodem
+from amodem import _lib as L
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ABS_TOL = 1e-5  # fp32 FFT/equaliser vs fp64 reference, |X| <= ~4 (SURVEY.md §8a tolerance table)
+
+
+@pytest.fixture(scope="module")
+def dm():
+    d = amodem.Demodulator(0)
+    yield d
+    d.close()
+
+
+def golden_expected(case):
+    return case["result"]
+
+
+def as_golden(d: dict) -> dict:
+    return {k: ({"hex": v.hex()} if isinstance(v, (bytes, bytearray)) else v) for k, v in d.items()}
+
+
+def decode(dm, case, x, options=0):
+    cfg = amodem.preset(case["config"], case["mod"], case["rep"])
+    mode = L.MODE_CHUNK if case["rx"] == "chunk" else L.MODE_RECEIVED
+    rec, pay = dm.decode_batch(x, [0], [len(x)], cfg=cfg, mode=mode, options=options)
+    return rec[0], pay[0]
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["fast", "exact"])
+@pytest.mark.parametrize("case", frames(), ids=lambda c: c["name"])
+def test_golden_frames(dm, case, exact):
+    x = O.build_case(case)
+    rec, pay = decode(dm, case, x, L.OPT_FORCE_EXACT if exact else 0)
+    got = amodem.to_reference(rec, pay.tobytes(), via_legacy=case["rx"] == "legacy")
+    assert as_golden(got) == case["result"]
+    inter = case["inter"]
+    if "bytesHex" in inter:
+        nb = len(inter["bytesHex"]) // 2
+        assert int(rec["nbytes"]) == nb
+        assert pay[:nb].tobytes().hex() == inter["bytesHex"]
+    if exact:
+        assert rec["flags"] & L.FLAG_EXACT
+        if case["rx"] == "legacy" and "coarseIdx" in inter and inter["coarseIdx"] >= 0:
+            assert int(rec["coarse_idx"]) == inter["coarseIdx"]
+
+
+def _debug_decode(dm, case, x, options):
+    import torch
+    cfg = amodem.preset(case["config"], case["mod"], case["rep"])
+    mode = L.MODE_CHUNK if case["rx"] == "chunk" else L.MODE_RECEIVED
+    dev = torch.device("cuda", 0)
+    xs = torch.from_numpy(np.concatenate([x, np.zeros(4, np.float32)])).to(dev)
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    ln = torch.tensor([len(x)], dtype=torch.int32, device=dev)
+    stride = amodem.payload_stride(cfg, len(x))
+    res = torch.zeros(96, dtype=torch.uint8, device=dev)
+    pay = torch.zeros(stride, dtype=torch.uint8, device=dev)
+    dbg = torch.zeros(L.C.sizeof(L.Debug), dtype=torch.uint8, device=dev)
+    dm.reserve(cfg, 1, len(x))
+    torch.cuda.synchronize()
+    dm.decode_device(cfg, mode, xs.data_ptr(), off.data_ptr(), ln.data_ptr(), 1, res.data_ptr(), pay.data_ptr(),
+                     stride, options=options, debug_ptr=dbg.data_ptr())
+    dm.synchronize()
+    d = L.Debug.from_buffer_copy(dbg.cpu().numpy().tobytes())
+    r = np.frombuffer(res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)[0]
+    return d, r
+
+
+DEBUG_CASES = [c for c in frames() if "sym0" in c["inter"]]
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["fast", "exact"])
+@pytest.mark.parametrize("case", DEBUG_CASES, ids=lambda c: c["name"])
+def test_intermediates(dm, case, exact):
+    x = O.build_case(case)
+    d, r = _debug_decode(dm, case, x, L.OPT_FORCE_EXACT if exact else 0)
+    inter = case["inter"]
+    nb = len(inter["H"]["re"])
+    arr = lambda a: np.array(a[:nb])
+    h = arr(d.h_re) + 1j * arr(d.h_im)
+    href = np.array(inter["H"]["re"]) + 1j * np.array(inter["H"]["im"])
+    x0 = arr(d.x_re) + 1j * arr(d.x_im)
+    x0ref = np.array(inter["sym0"]["fftRe"]) + 1j * np.array(inter["sym0"]["fftIm"])
+    eq = arr(d.eq_re) + 1j * arr(d.eq_im)
+    eqref = np.array(inter["sym0"]["eqRe"]) + 1j * np.array(inter["sym0"]["eqIm"])
+    nph = min(len(inter["phases"]), L.DBG_SYMS)
+    ph = np.array(d.phase[:nph])
+    phref = np.array(inter["phases"][:nph])
+    if exact or (r["flags"] & L.FLAG_EXACT):
+        assert np.array_equal(h, href) and np.array_equal(x0, x0ref) and np.array_equal(eq, eqref)
+        assert np.array_equal(ph, phref)
+        if case["rx"] == "legacy":
+            assert d.mean == inter["mean"] and d.mx == inter["mx"]
+            assert d.coarse_lo == inter["coarseIdx"] and d.fine_idx == inter["startIdx"]
+            assert d.fine_metric == inter["fineMetric"]
+    else:
+        scale = max(1.0, float(np.abs(href).max()))
+        assert np.abs(h - href).max() <= ABS_TOL * scale
+        assert np.abs(x0 - x0ref).max() <= ABS_TOL * scale
+        assert np.abs(eq - eqref).max() <= ABS_TOL
+        assert np.abs(ph - phref).max() <= ABS_TOL
+        if case["rx"] == "legacy":
+            assert abs(d.mean - inter["mean"]) <= 1e-12 * max(1.0, abs(inter["mean"]))
+            assert abs(d.mx - inter["mx"]) <= 1e-7 * inter["mx"]
+            assert d.coarse_lo <= inter["coarseIdx"] <= d.coarse_hi
+            assert d.fine_idx == inter["startIdx"]
+            assert abs(d.fine_metric - inter["fineMetric"]) <= 1e-4
+
+
+# ----------------------------------------------------------------- batches --
+def _oracle_ref(cfg_name, mod, rep, x, chunk):
+    c = O.cfg(cfg_name)
+    r, pay = O.decode(c, x, mod, rep, chunk)
+    return ref_dict(struct_to_dict(r), pay.tobytes(), via_legacy=not chunk), pay
+
+
+def test_clean_batch_c2_shape(dm):
+    """512 distinct QPSK 1 KB legacy frames (BASELINE C2 frame shape) in one batch."""
+    cfg = amodem.preset("standard", "QPSK", 1)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, 512, payload_len=1024)
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    assert (rec["status"] == 0).all() and (rec["crc_valid"] == 1).all()
+    assert (rec["flags"] == 0).all(), "clean frames must stay on the fast path"
+    assert (rec["preamble_idx"] == 13230).all()
+    for i in range(0, 512, 37):
+        d = amodem.to_reference(rec[i], pay[i].tobytes(), True)
+        assert d["data"] == amodem.synth_payload(0x9E3779B9 ^ i, 1024) and d["fileName"] == "f.bin"
+    # spot-check complete decoded byte streams against the CPU oracle
+    for i in (0, 255, 511):
+        ref, refpay = _oracle_ref("standard", "QPSK", 1, x[offs[i]:offs[i] + lens[i]], False)
+        assert pay[i, :len(refpay)].tobytes() == refpay.tobytes()
+
+
+def _noisy_batch(kind, n, snr, seed0):
+    """n noisy frames built by the oracle's recipes; returns (cfg, mod, rep, chunk, frames)."""
+    out = []
+    for i in range(n):
+        if kind == "qpsk":
+            case = {"config": "standard", "tx": {"kind": "legacy", "seed": 0x9E3779B9 ^ (1000 + i), "len": 1024,
+                                                 "name": "f.bin", "mod": "QPSK", "rep": 1}}
+            mod, rep, chunk = "QPSK", 1, False
+        elif kind == "qam16":
+            case = {"config": "standard", "tx": {"kind": "legacy", "seed": 0x9E3779B9 ^ (2000 + i), "len": 512,
+                                                 "name": "q", "mod": "QAM16", "rep": 1}}
+            mod, rep, chunk = "QAM16", 1, False
+        elif kind == "bpsk3":
+            case = {"config": "acoustic", "tx": {"kind": "legacy", "seed": 0x9E3779B9 ^ (3000 + i), "len": 64,
+                                                 "name": "b", "mod": "BPSK", "rep": 3}}
+            mod, rep, chunk = "BPSK", 3, False
+        else:  # chunk frames at known offsets, streaming-window length (C4 shape)
+            case = {"config": "standard", "tx": {"kind": "chunk", "seq": i, "seed": 0x9E3779B9 ^ (4000 + i),
+                                                 "len": 2048, "mod": "QPSK", "rep": 1}}
+            mod, rep, chunk = "QPSK", 1, True
+        post = [{"op": "noise", "snr": snr, "seed": seed0 + 7919 * i}]
+        if kind == "chunk":
+            post.append({"op": "slice", "start": 2205, "end": 2205 + 3 * 576 + 41 * 576})
+        case["post"] = post
+        out.append(O.build_case(case))
+    return case["config"], mod, rep, chunk, out
+
+
+@pytest.mark.parametrize("kind,n,snr", [("qpsk", 48, 10), ("qpsk", 48, 20), ("qam16", 48, 20),
+                                        ("bpsk3", 24, 10), ("chunk", 48, 10)])
+def test_noisy_batches_vs_oracle(dm, kind, n, snr):
+    cfg_name, mod, rep, chunk, fr = _noisy_batch(kind, n, snr, 0xABC0 + snr)
+    lens = np.array([len(f) for f in fr], np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    x = np.concatenate(fr).astype(np.float32)
+    cfg = amodem.preset(cfg_name, mod, rep)
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg, mode=L.MODE_CHUNK if chunk else L.MODE_RECEIVED)
+    for i, f in enumerate(fr):
+        ref, refpay = _oracle_ref(cfg_name, mod, rep, f, chunk)
+        got = as_golden(amodem.to_reference(rec[i], pay[i].tobytes(), via_legacy=not chunk))
+        assert got == ref, (kind, i, int(rec[i]["flags"]))
+        assert pay[i, :len(refpay)].tobytes() == refpay.tobytes(), (kind, i)
