@@ -96,6 +96,13 @@ def load():
     """Load libamodem.so (built by __graft_entry__.build / `make -C audio-modem_amd/csrc`)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (same
+        # SONAME as /opt/rocm's). If torch is importable, load it first so that
+        # libamodem binds to the already-loaded runtime instead of a second copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libamodem.so not built: {LIB_PATH} (run __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)

@@ -47,6 +47,7 @@ struct DevCfg {
   double te;           // sum pre1^2 in reference order (f64)
   float te_f;
   float guard;         // fast-path guard scale (1 = default)
+  int32_t stop_after;  // diagnostics only (AMOD_STOP_AFTER): fast kernel returns after this stage
   DevTables t;
 };
 

@@ -24,16 +24,18 @@ namespace {
 constexpr int WG = 1024;
 constexpr int NWAVE = WG / 64;
 constexpr int SC_BLK = 32;                 // Schmidl-Cox block / segment length
-constexpr int UNION_BYTES = 13312;         // stage-shared scratch
-constexpr int CAP = 37120;                 // max samples per LDS-resident frame
+constexpr int UNION_BYTES = 14336;         // stage-shared scratch
+constexpr int CAP = 36864;                 // max samples per LDS-resident frame
 constexpr int MAX_BITS_WORDS = 1640;       // 64 symbols x 820 bits
-constexpr int FINE_MAX = 2048;             // max fine-search positions (else exact)
+constexpr int FINE_MAX = 1008;             // max fine-search positions (else exact)
+constexpr int SC_NB = (CAP + 31) / 32 + 8; // Schmidl-Cox blocks (k-space), with slack
+constexpr int SC_MAXCAND = 256;            // blocks slid position by position (else exact)
 
 struct alignas(16) Smem {
   float x[CAP + 16];                       // raw samples: x[ph + i] is frame sample i
   union alignas(16) U {
-    struct { float bz[1184]; float be[1184]; } sc;             // stage 1
-    struct { float tmpl[768]; float m[FINE_MAX]; } fine;        // stage 2
+    struct { float bz[SC_NB]; float be[SC_NB]; float ba[SC_NB]; int16_t cand[SC_MAXCAND]; } sc; // stage 1
+    struct { float tmpl[768]; float m[FINE_MAX]; float yw[FINE_MAX + 776]; } fine; // stage 2
     struct {                                                      // stage 3
       float2 tw1[8 * 64];
       float2 tw2[8 * 8];
@@ -47,7 +49,7 @@ struct alignas(16) Smem {
   double rd[2 * NWAVE];
   uint32_t ru[16];
   // per-frame scalars (written by one thread, read after a barrier)
-  int n, ph, status, flags, coarse, clo, chi, start, nsym, data0;
+  int n, ph, status, flags, coarse, clo, chi, start, nsym, data0, ncand;
   float A, B, cbest, fbest, gmax, zce;
   double mean, mx;
 };
@@ -81,58 +83,60 @@ __device__ __forceinline__ void dft8(float2 (&v)[8]) {
   v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
 }
 
-// exchange-buffer addressing: 8 rows of 64 float2, rows 0-3 in region a, 4-7 in b
-__device__ __forceinline__ float2 *xrow(float2 *ra, float2 *rb, int row) {
-  return (row < 4 ? ra : rb) + (row & 3) * 64;
-}
+// Exchange buffer of one FFT job: 8 rows of 64 float2; rows 0-3 live at float2
+// index a of the LDS sample array, rows 4-7 at index b (each inside one symbol's
+// sample slot). Plain 32-bit LDS indices keep every access a ds_read/ds_write.
+struct XB {
+  int a, b;
+};
+__device__ __forceinline__ int xrow(const XB &x, int row) { return (row < 4 ? x.a : x.b) + (row & 3) * 64; }
 __device__ __forceinline__ int swz2(int q, int l1, int p1) { // exchange-2 column swizzle
   return 8 * ((l1 ^ q) & 7) + ((p1 ^ ((q & 3) + 4 * (l1 >> 2))) & 7);
 }
 __device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2); }
 
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); result
-// X[n] left in the exchange buffer at spec(n) = row n>>6, col spec_idx(n)&63.
-__device__ void fft512_wave(float2 (&v)[8], float2 *ra, float2 *rb, const Smem &sm) {
-  const int l = wave_lane();
+// X[n] left in the exchange buffer at row spec_idx(n)>>6, col spec_idx(n)&63.
+__device__ void fft512_wave(float2 (&v)[8], const XB xb, Smem &sm) {
+  float2 *const X2 = reinterpret_cast<float2 *>(sm.x);
+  int l = wave_lane();
+  // keep the lane-derived swizzle indices inside the job loop: hoisted out of it
+  // they occupy ~40 VGPRs for the whole stage and force spills
+  asm volatile("" : "+v"(l));
   dft8(v);
 #pragma unroll
   for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], sm.u.fq.tw1[q * 64 + l]);
   // exchange 1: row q, col l ^ (q<<3)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) xrow(ra, rb, q)[l ^ (q << 3)] = v[q];
+  for (int q = 0; q < 8; ++q) X2[xrow(xb, q) + (l ^ (q << 3))] = v[q];
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const int l1 = l & 7, q2 = l >> 3; // pass-2 lane = (l1, q)
+  const int r2 = xrow(xb, q2);
 #pragma unroll
-  for (int l2 = 0; l2 < 8; ++l2) v[l2] = xrow(ra, rb, q2)[l1 + 8 * (l2 ^ q2)];
+  for (int l2 = 0; l2 < 8; ++l2) v[l2] = X2[r2 + l1 + 8 * (l2 ^ q2)];
   dft8(v);
 #pragma unroll
   for (int p1 = 1; p1 < 8; ++p1) v[p1] = cmul(v[p1], sm.u.fq.tw2[p1 * 8 + l1]);
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // exchange 2: lane (l1, q) writes U[p1] at row q, col swz2(q, l1, p1)
 #pragma unroll
-  for (int p1 = 0; p1 < 8; ++p1) xrow(ra, rb, q2)[swz2(q2, l1, p1)] = v[p1];
+  for (int p1 = 0; p1 < 8; ++p1) X2[r2 + swz2(q2, l1, p1)] = v[p1];
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const int p1 = l & 7, q3 = l >> 3; // pass-3 lane = (p1, q)
+  const int p1 = l & 7; // pass-3 lane = (p1, q), same row as pass 2
 #pragma unroll
-  for (int a = 0; a < 8; ++a) v[a] = xrow(ra, rb, q3)[swz2(q3, a, p1)];
-  dft8(v); // v[p2] = X[q3 + 8 p1 + 64 p2]
+  for (int a = 0; a < 8; ++a) v[a] = X2[r2 + swz2(q2, a, p1)];
+  dft8(v); // v[p2] = X[q2 + 8 p1 + 64 p2]
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
   for (int p2 = 0; p2 < 8; ++p2) {
-    const int n = q3 + 8 * p1 + 64 * p2;
-    const int s = spec_idx(n);
-    xrow(ra, rb, s >> 6)[s & 63] = v[p2];
+    const int s = spec_idx(q2 + 8 * p1 + 64 * p2);
+    X2[xrow(xb, s >> 6) + (s & 63)] = v[p2];
   }
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
-__device__ __forceinline__ float2 spec_read(const float2 *ra, const float2 *rb, int n) {
+__device__ __forceinline__ float2 spec_read(const Smem &sm, const XB &xb, int n) {
   const int s = spec_idx(n & 511);
-  return (s < 256 ? ra : rb)[s & 255];
+  return reinterpret_cast<const float2 *>(sm.x)[(s < 256 ? xb.a : xb.b) + (s & 255)];
 }
 
 // ---------------------------------------------------------------------------
@@ -257,8 +261,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
   const float *X = sm.x + ph; // frame sample i at X[i]
   auto Y = [&](int i) -> float { return fmaf(X[i], A, B); };
 
-  amod_result r;
-  init_result(r);
+  if (cfg.stop_after == 0) return;
   int start = 0;
   const float eps_c = 2e-3f * cfg.guard;     // Schmidl-Cox metric guard (absolute)
   const float eps_g = 1e-3f * cfg.guard;     // energy-gate guard (relative)
@@ -271,41 +274,95 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       if (tid == 0) sm.status = AMOD_E_PREAMBLE;
       __syncthreads();
     } else {
-      const int NB = (N + SC_BLK - 1) / SC_BLK;
-      for (int b = tid; b < NB; b += WG) {
-        float zz = 0.f, ee = 0.f;
-        const int i0 = b * SC_BLK;
-#pragma unroll 8
-        for (int j = 0; j < SC_BLK; ++j) {
-          const int i = i0 + j;
-          if (i < N) {
-            const float yi = Y(i);
-            ee = fmaf(yi, yi, ee);
-            if (i < N - 256) zz = fmaf(yi, Y(i + 256), zz);
-          }
+      // Blocks of 32 in LDS-index space k = ph + i (so every block starts 16-byte aligned);
+      // window sums at block starts come from 8 block sums, and per-block bounds
+      // |p| <= |p_c| + A_c + A_{c+8}, ra >= ra_c - E_c, rb >= rb_c - E_{c+8} cap the metric
+      // of every position in the block. Only blocks whose cap can reach the best
+      // block-start metric are slid through position by position.
+      const int NB = (ph + N + SC_BLK - 1) / SC_BLK;
+      const int klo = ph, khi_e = ph + N, khi_z = ph + N - 256; // valid k ranges for e and z
+      for (int t = tid; t < NB * 4; t += WG) {
+        const int k0 = 8 * t;
+        float4 a0 = *reinterpret_cast<const float4 *>(&sm.x[k0]);
+        float4 a1 = *reinterpret_cast<const float4 *>(&sm.x[k0 + 4]);
+        float4 b0 = *reinterpret_cast<const float4 *>(&sm.x[k0 + 256]);
+        float4 b1 = *reinterpret_cast<const float4 *>(&sm.x[k0 + 260]);
+        const float ua[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float ub[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        float zz = 0.f, ee = 0.f, za = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = k0 + j;
+          const float ya = (k >= klo && k < khi_e) ? fmaf(ua[j], A, B) : 0.f;
+          const float yb = (k + 256 < khi_e) ? fmaf(ub[j], A, B) : 0.f;
+          const float z = (k >= klo && k < khi_z) ? ya * yb : 0.f;
+          ee = fmaf(ya, ya, ee);
+          zz += z;
+          za += fabsf(z);
         }
-        sm.u.sc.bz[b] = zz;
-        sm.u.sc.be[b] = ee;
+#pragma unroll
+        for (int o = 1; o < 4; o <<= 1) {
+          zz += __shfl_xor(zz, o, 64); ee += __shfl_xor(ee, o, 64); za += __shfl_xor(za, o, 64);
+        }
+        if ((t & 3) == 0) { sm.u.sc.bz[t >> 2] = zz; sm.u.sc.be[t >> 2] = ee; sm.u.sc.ba[t >> 2] = za; }
       }
+      if (tid == 0) sm.ncand = 0;
       __syncthreads();
       const float gate_lo = 0.01f * (1.f - eps_g), gate_hi = 0.01f * (1.f + eps_g);
-      const int nseg = (E + SC_BLK) / SC_BLK;
-      // pass 1: best metric (loose gate) and first index
-      float best = -1.f;
-      int bidx = 0x7fffffff;
-      for (int g = tid; g < nseg; g += WG) {
+      const int ncb = (E + ph) / SC_BLK + 1; // blocks holding at least one position d in [0, E]
+      // (a) exact window sums at block starts -> lower bound L on the best metric
+      float lmax = -1.f;
+      for (int c = tid; c < ncb; c += WG) {
         float p = 0.f, ra = 0.f, rb = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { p += sm.u.sc.bz[g + k]; ra += sm.u.sc.be[g + k]; rb += sm.u.sc.be[g + 8 + k]; }
-        const int d0 = g * SC_BLK;
-        const int dend = min(d0 + SC_BLK - 1, E);
+        for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
+        if (SC_BLK * c - ph >= 0 && ra > gate_lo && rb > gate_lo) lmax = fmaxf(lmax, (p * p) / (ra * rb));
+      }
+      lmax = wave_max(lmax);
+      if (lane == 0) sm.rf[wave] = lmax;
+      __syncthreads();
+      float Lb = -1.f;
+      for (int i = 0; i < NWAVE; ++i) Lb = fmaxf(Lb, sm.rf[i]);
+      // (b) blocks whose cap reaches Lb - eps_c become candidates
+      for (int c = tid; c < ncb; c += WG) {
+        float p = 0.f, ra = 0.f, rb = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
+        const float e0 = sm.u.sc.be[c], e8 = sm.u.sc.be[c + 8], e16 = c + 16 < NB ? sm.u.sc.be[c + 16] : 0.f;
+        const float ra_hi = ra + e8, rb_hi = rb + e16, ra_lo = ra - e0, rb_lo = rb - e8;
+        if (!(ra_hi > gate_lo && rb_hi > gate_lo)) continue; // every position gated out
+        bool cand = true;
+        if (ra_lo > 0.f && rb_lo > 0.f) {
+          const float pm = fabsf(p) + sm.u.sc.ba[c] + sm.u.sc.ba[c + 8];
+          cand = (pm * pm) * 1.0001f >= (Lb - eps_c) * (ra_lo * rb_lo);
+        }
+        if (cand) {
+          const int slot = atomicAdd(&sm.ncand, 1);
+          if (slot < SC_MAXCAND) sm.u.sc.cand[slot] = (int16_t)c;
+        }
+      }
+      __syncthreads();
+      const int ncand = sm.ncand;
+      if (ncand > SC_MAXCAND) { // too many blocks near the best: leave it to the exact path
+        if (tid == 0) sm.flags |= AMOD_FLAG_COARSE;
+        __syncthreads();
+        goto to_exact;
+      }
+      // (c) slide through candidate blocks position by position
+      float best = -1.f;
+      int bidx = 0x7fffffff;
+      for (int j = tid; j < ncand; j += WG) {
+        const int c = sm.u.sc.cand[j];
+        float p = 0.f, ra = 0.f, rb = 0.f;
+        for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
+        const int d0 = SC_BLK * c - ph, dend = min(d0 + SC_BLK - 1, E);
         for (int d = d0; d <= dend; ++d) {
-          if (ra > gate_lo && rb > gate_lo) {
+          if (d >= 0 && ra > gate_lo && rb > gate_lo) {
             const float m = (p * p) / (ra * rb);
-            if (m > best) { best = m; bidx = d; }
+            if (m > best || (m == best && d < bidx)) { best = m; bidx = d; }
           }
           if (d < dend) {
-            const float a = Y(d), mid = Y(d + 256), bb = Y(d + 512);
+            const float a = d >= 0 ? Y(d) : 0.f, mid = d + 256 >= 0 ? Y(d + 256) : 0.f, bb = Y(d + 512);
             p = fmaf(mid, bb - a, p);
             ra = fmaf(-a, a, fmaf(mid, mid, ra));
             rb = fmaf(-mid, mid, fmaf(bb, bb, rb));
@@ -327,17 +384,16 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         __syncthreads();
       }
       const float CB = sm.cbest;
-      // pass 2: candidate range {d : metric >= CB - eps_c}, and gate uncertainty there
+      // candidate range {d : metric >= CB - eps_c}, and gate uncertainty there
       int lo = 0x7fffffff, hi = -1, unc = 0;
       if (CB > 0.5f - eps_c) {
-        for (int g = tid; g < nseg; g += WG) {
+        for (int j = tid; j < ncand; j += WG) {
+          const int c = sm.u.sc.cand[j];
           float p = 0.f, ra = 0.f, rb = 0.f;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { p += sm.u.sc.bz[g + k]; ra += sm.u.sc.be[g + k]; rb += sm.u.sc.be[g + 8 + k]; }
-          const int d0 = g * SC_BLK;
-          const int dend = min(d0 + SC_BLK - 1, E);
+          for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
+          const int d0 = SC_BLK * c - ph, dend = min(d0 + SC_BLK - 1, E);
           for (int d = d0; d <= dend; ++d) {
-            if (ra > gate_lo && rb > gate_lo) {
+            if (d >= 0 && ra > gate_lo && rb > gate_lo) {
               const float m = (p * p) / (ra * rb);
               if (m >= CB - eps_c) {
                 lo = min(lo, d); hi = max(hi, d);
@@ -345,7 +401,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
               }
             }
             if (d < dend) {
-              const float a = Y(d), mid = Y(d + 256), bb = Y(d + 512);
+              const float a = d >= 0 ? Y(d) : 0.f, mid = d + 256 >= 0 ? Y(d + 256) : 0.f, bb = Y(d + 512);
               p = fmaf(mid, bb - a, p);
               ra = fmaf(-a, a, fmaf(mid, mid, ra));
               rb = fmaf(-mid, mid, fmaf(bb, bb, rb));
@@ -370,6 +426,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
     }
     if (sm.flags) goto to_exact;
     if (sm.status != AMOD_OK) goto finish_error;
+    if (cfg.stop_after == 1) return;
 
     // ---------------------------------------------- stage 2: fine timing
     {
@@ -387,48 +444,52 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         __syncthreads();
         goto finish_error;
       }
+      // template + the normalised search window, staged once in LDS
       for (int i = tid; i < SYM; i += WG) sm.u.fine.tmpl[i] = cfg.t.pre1[i];
+      const int span = P + SYM + 8;
+      for (int j = tid; j < span; j += WG) sm.u.fine.yw[j] = (w0 + j < N) ? Y(w0 + j) : 0.f;
       __syncthreads();
       const float te = cfg.te_f;
       const int nquad = (P + 3) >> 2;
-      const int split = SYM / 4; // 4 tap ranges per quad of positions
-      for (int task = tid; task < nquad * 4; task += WG) {
-        const int qd = task >> 2, sp = task & 3;
-        const int d = w0 + 4 * qd;
-        const int i0 = sp * split, i1 = (sp == 3) ? SYM : i0 + split;
+      const int L8 = (SYM / 8) | 1; // odd split length spreads the 8 splits over LDS banks
+      const float *yw = sm.u.fine.yw;
+      const float *tm = sm.u.fine.tmpl;
+      // lane = (quad of 4 positions, one of 8 tap ranges); 4 correlations + 1 energy per tap
+      for (int task = tid; task < nquad * 8; task += WG) {
+        const int qd = task >> 3, sp = task & 7;
+        const int j0 = 4 * qd; // window offset of the quad's first position
+        const int i0 = sp * L8, i1 = (sp == 7) ? SYM : i0 + L8;
         float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, e0 = 0.f;
-        // sliding window of 4 samples y[d+i .. d+i+3]
-        float y0 = (d + i0 + 0 < N) ? Y(d + i0 + 0) : 0.f;
-        float y1 = (d + i0 + 1 < N) ? Y(d + i0 + 1) : 0.f;
-        float y2 = (d + i0 + 2 < N) ? Y(d + i0 + 2) : 0.f;
+        float y0 = yw[j0 + i0], y1 = yw[j0 + i0 + 1], y2 = yw[j0 + i0 + 2];
+#pragma unroll 4
         for (int i = i0; i < i1; ++i) {
-          const float y3 = (d + i + 3 < N) ? Y(d + i + 3) : 0.f;
-          const float t = sm.u.fine.tmpl[i];
+          const float y3 = yw[j0 + i + 3];
+          const float t = tm[i];
           c0 = fmaf(y0, t, c0); c1 = fmaf(y1, t, c1); c2 = fmaf(y2, t, c2); c3 = fmaf(y3, t, c3);
           e0 = fmaf(y0, y0, e0);
           y0 = y1; y1 = y2; y2 = y3;
         }
-        // combine the 4 tap ranges (lanes 4qd .. 4qd+3 are adjacent)
+        // combine the 8 tap ranges (lanes 8qd .. 8qd+7 are adjacent)
 #pragma unroll
-        for (int o = 1; o < 4; o <<= 1) {
+        for (int o = 1; o < 8; o <<= 1) {
           c0 += __shfl_xor(c0, o, 64); c1 += __shfl_xor(c1, o, 64);
           c2 += __shfl_xor(c2, o, 64); c3 += __shfl_xor(c3, o, 64);
           e0 += __shfl_xor(e0, o, 64);
         }
-        if (sp == 0) {
-          const float cs[4] = {c0, c1, c2, c3};
+        if (sp < 4 && j0 + sp < P) {
+          // lane sp finishes position j0 + sp: slide the energy forward sp samples
+          const float cj = sp == 0 ? c0 : (sp == 1 ? c1 : (sp == 2 ? c2 : c3));
           float en = e0;
-          for (int j = 0; j < 4; ++j) {
-            const int dd = d + j;
-            if (dd > w1) break;
-            if (j > 0) { const float yo = Y(dd - 1), yn = Y(dd - 1 + SYM); en = fmaf(yn, yn, fmaf(-yo, yo, en)); }
-            const float den = sqrtf(fmaxf(en, 0.f) * te);
-            float m;
-            if (den > 0.001f * (1.f + eps_g)) m = cs[j] / den;
-            else if (den > 0.001f * (1.f - eps_g)) m = cs[j] / den + 4.f; // uncertain gate: tagged
-            else m = -8.f;                                                 // gated out
-            sm.u.fine.m[dd - w0] = m;
+          for (int j = 0; j < sp; ++j) {
+            const float yo = yw[j0 + j], yn = yw[j0 + j + SYM];
+            en = fmaf(yn, yn, fmaf(-yo, yo, en));
           }
+          const float den = sqrtf(fmaxf(en, 0.f) * te);
+          float m;
+          if (den > 0.001f * (1.f + eps_g)) m = cj / den;
+          else if (den > 0.001f * (1.f - eps_g)) m = cj / den + 4.f; // uncertain gate: tagged
+          else m = -8.f;                                              // gated out
+          sm.u.fine.m[j0 + sp] = m;
         }
       }
       __syncthreads();
@@ -485,10 +546,8 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       if (sm.flags) goto to_exact;
       if (sm.status != AMOD_OK) goto finish_error;
       start = sm.start;
-      r.fine_metric = sm.fbest;
-      r.coarse_idx = sm.coarse;
-      r.preamble_idx = start;
     }
+    if (cfg.stop_after == 2) return;
     // CE / data checks (modem.js:591-600)
     if (start + 3 * SYM > N) { if (tid == 0) sm.status = AMOD_E_SHORT_CE; __syncthreads(); goto finish_error; }
     if (start + 3 * SYM >= N) { if (tid == 0) sm.status = AMOD_E_NO_DATA; __syncthreads(); goto finish_error; }
@@ -530,10 +589,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       const int pos1 = s1 == -2 ? ce0 : data0 + s1 * SYM;
       const int pos2 = s2 >= 0 ? data0 + s2 * SYM : start + SYM; // pre2 slot when absent
       // exchange regions: 2 KB, 8-byte aligned, inside each symbol's sample slot
-      float2 *ra = reinterpret_cast<float2 *>(
-          reinterpret_cast<uintptr_t>(&sm.x[ph + pos1] + 1) & ~uintptr_t(7));
-      float2 *rb = reinterpret_cast<float2 *>(
-          reinterpret_cast<uintptr_t>(&sm.x[ph + pos2] + 1) & ~uintptr_t(7));
+      const XB xb{(ph + pos1 + 1) >> 1, (ph + pos2 + 1) >> 1}; // float2 index, first whole slot pair
       float2 v[8];
       int const1 = 0, const2 = 0;
       if (active) {
@@ -548,13 +604,13 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         }
         const1 = wave_min(mn1) == wave_max(mx1);
         const2 = wave_min(mn2) == wave_max(mx2);
-        fft512_wave(v, ra, rb, sm);
+        fft512_wave(v, xb, sm);
         if (job == 0) {
           // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
           float zmax = 0.f;
           for (int b = lane; b < nband; b += 64) {
             const int k = cfg.sub_start + b;
-            const float2 zk = spec_read(ra, rb, k), zn = spec_read(ra, rb, kFft - k);
+            const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
             zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
           }
           zmax = wave_max(zmax);
@@ -562,7 +618,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
             const int k = cfg.sub_start + b;
             float2 h = make_float2(0.f, 0.f);
             if (!const1) {
-              const float2 zk = spec_read(ra, rb, k), zn = spec_read(ra, rb, kFft - k);
+              const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
               const float2 y = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
               const float kn = cfg.t.known[b];
               h = make_float2(y.x * kn, y.y * kn);
@@ -590,6 +646,8 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       const float gmax = sm.gmax, zce = sm.zce;
       // ---- per data symbol of this job: equalise, pilot phase, demap
       for (int which = 0; which < 2; ++which) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln)); // per-iteration lane (keeps debug/bit addresses out of registers)
         const int sidx = which == 0 ? s1 : s2;
         if (sidx < 0) continue; // CE or absent
         const bool cst = which == 0 ? const1 : const2;
@@ -597,16 +655,16 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         const int sbase = sidx * cfg.ndata * cfg.bps;
         if (cst) {
           // constant window: every bin is exactly 0 in the reference -> origin decision
-          for (int b = lane; b < nband; b += 64) {
+          for (int b = ln; b < nband; b += 64) {
             const int di = cfg.t.band_di[b];
             if (di < 0) continue;
             const int pos = sbase + di * cfg.bps;
             const uint32_t val = (uint32_t)cfg.origin_idx << (32 - cfg.bps - (pos & 31));
             if (val) atomicOr(&bits[pos >> 5], val);
           }
-          if (dbg && sidx < AMOD_DBG_SYMS) if (lane == 0) D->phase[sidx] = 0.0;
+          if (dbg && sidx < AMOD_DBG_SYMS) if (ln == 0) D->phase[sidx] = 0.0;
           if (dbg && sidx == 0)
-            for (int b = lane; b < nband; b += 64) { D->x_re[b] = 0; D->x_im[b] = 0; D->eq_re[b] = 0; D->eq_im[b] = 0; }
+            for (int b = ln; b < nband; b += 64) { D->x_re[b] = 0; D->x_im[b] = 0; D->eq_re[b] = 0; D->eq_im[b] = 0; }
           continue;
         }
         float2 eq[4];
@@ -615,11 +673,11 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         int pcnt = 0, pflag = 0;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int b = lane + 64 * rr;
+          const int b = ln + 64 * rr;
           eq[rr] = make_float2(0.f, 0.f);
           if (b < nband) {
             const int k = cfg.sub_start + b;
-            const float2 zk = spec_read(ra, rb, k), zn = spec_read(ra, rb, kFft - k);
+            const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
             zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
             const float2 xs = which == 0 ? make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y))
                                          : make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
@@ -635,7 +693,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         const float delta = 2e-6f * cfg.guard * (zmax + emax * zce) * gmax + 1e-12f;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int b = lane + 64 * rr;
+          const int b = ln + 64 * rr;
           if (b < nband && cfg.t.band_di[b] < 0) {
             const float er = eq[rr].x, ei = eq[rr].y;
             const float aer = fabsf(er);
@@ -651,12 +709,12 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         const float phase = pcnt > 0 ? psum / (float)pcnt : 0.f;
         const float dphase = pcnt > 0 ? perr / (float)pcnt : 0.f;
         if (pflag) wflags |= AMOD_FLAG_PHASE;
-        if (dbg && sidx < AMOD_DBG_SYMS && lane == 0) D->phase[sidx] = phase;
+        if (dbg && sidx < AMOD_DBG_SYMS && ln == 0) D->phase[sidx] = phase;
         const float tau = 4.f * (delta * (1.f + fabsf(phase)) + emax * dphase) + 1e-9f;
         int dflag = 0;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int b = lane + 64 * rr;
+          const int b = ln + 64 * rr;
           if (b >= nband) continue;
           const int di = cfg.t.band_di[b];
           if (di < 0) continue;
@@ -677,8 +735,8 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
     __syncthreads();
     if (sm.flags) goto to_exact;
     // ------------------------------------------------ stage 4: finish
+    if (cfg.stop_after == 3) return;
     {
-      r.nbits = nbits;
       if (dbg && tid == 0) D->nsym = M;
       const uint32_t *v = sm.u.fq.bits;
       int nv = nbits;
@@ -688,7 +746,10 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         __syncthreads();
         v = voted;
       }
-      r.flags = 0;
+      amod_result r;
+      init_result(r);
+      r.nbits = nbits;
+      if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = sm.fbest; r.coarse_idx = sm.coarse; r.preamble_idx = start; }
       finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr);
       return;
     }
@@ -696,6 +757,8 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
 
 finish_error:
   if (tid == 0) {
+    amod_result r;
+    init_result(r);
     r.status = sm.status;
     if (cfg.mode == AMOD_MODE_RECEIVED) {
       r.coarse_idx = sm.status == AMOD_E_PREAMBLE ? -1 : sm.coarse;

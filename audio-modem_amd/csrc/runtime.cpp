@@ -297,6 +297,8 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.origin_idx = demap_exact(c->modulation, 0.0, 0.0);
     const char *g = getenv("AMOD_GUARD_SCALE");
     d.guard = g ? (float)atof(g) : 1.0f;
+    const char *sa = getenv("AMOD_STOP_AFTER"); // stage-cost diagnostics; results are not written
+    d.stop_after = sa ? atoi(sa) : 99;
     // host images
     std::vector<float> pre1(sym), ce(sym);
     double known_full[amod::kFft] = {0};

@@ -1,0 +1,13 @@
+# usage: bash run_gpu.sh <steps...>  (each step bounded; stop at first crash)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -4 gpurun_out/$name.log; echo "rc=$rc"; if [ $rc -ge 2 ] && [ $rc -ne 5 ]; then echo "ABORT after $name"; exit $rc; fi; }
+for s in "$@"; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
+    tests) run gpu_tests 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 3;;
+    stages) run stages 600 python tools/stage_profile.py;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 3 --cpu-frames -1;;
+  esac
+done
