@@ -71,7 +71,15 @@ struct DevWork {
 };
 
 // ---------------------------------------------------------------- helpers --
-__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+// Lane id through an opaque copy: inside persistent frame loops this keeps the
+// compiler from hoisting lane-derived addresses out of the loop (they would stay
+// live across every stage and exhaust the register file).
+__device__ __forceinline__ int ltid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ int wave_lane() { return ltid() & 63; }
 
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -170,7 +178,7 @@ __device__ inline int parse_stream(const uint32_t *v, int nbytes, int mode, amod
 // registers are moved to the end of the message with precomputed zero-byte
 // shift operators and XOR-combined (CRC linearity). `red` is >= 8 words of LDS.
 __device__ inline uint32_t block_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *red) {
-  const int tid = threadIdx.x;
+  const int tid = ltid();
   uint32_t reg = 0xFFFFFFFFu; // register carried between 4096-byte passes (uniform)
   const int npass = (L + kCrcBlock - 1) / kCrcBlock;
   for (int pass = 0; pass < npass; ++pass) {
@@ -215,7 +223,7 @@ __device__ inline int block_vote(const uint32_t *bits, int nbits, int rep, uint3
   const int nv = nbits / rep;
   const int nw = (nv + 31) >> 5;
   const int thr = (rep + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
-  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+  for (int w = ltid(); w < nw; w += blockDim.x) {
     uint32_t word = 0;
     for (int b = 0; b < 32; ++b) {
       const int j = w * 32 + b;
@@ -265,7 +273,7 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
   const int nw = (nbytes + 3) >> 2;
   uint32_t *dst = reinterpret_cast<uint32_t *>(slot);
   const int cap_w = (int)(stride >> 2);
-  for (int w = threadIdx.x; w < nw && w < cap_w; w += blockDim.x) dst[w] = __builtin_bswap32(v[w]);
+  for (int w = ltid(); w < nw && w < cap_w; w += blockDim.x) dst[w] = __builtin_bswap32(v[w]);
   __syncthreads();
   if (threadIdx.x == 0) {
     *out = r_sh;

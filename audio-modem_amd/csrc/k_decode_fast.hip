@@ -21,11 +21,13 @@
 namespace amod {
 namespace {
 
-constexpr int WG = 1024;
+constexpr int WG = 1024;                   // 16 waves (128 VGPRs each)
 constexpr int NWAVE = WG / 64;
 constexpr int SC_BLK = 32;                 // Schmidl-Cox block / segment length
-constexpr int UNION_BYTES = 14336;         // stage-shared scratch
-constexpr int CAP = 36864;                 // max samples per LDS-resident frame
+constexpr int UNION_BYTES = 14848;         // stage-shared scratch
+constexpr int CAP = 36736;                 // max samples per LDS-resident frame
+constexpr int PFV = (CAP + 8 + 4 * WG - 1) / (4 * WG); // float4 vectors per lane per frame
+constexpr int PF = PFV;                    // all issued before the first use: full memory-level parallelism
 constexpr int MAX_BITS_WORDS = 1640;       // 64 symbols x 820 bits
 constexpr int FINE_MAX = 1008;             // max fine-search positions (else exact)
 constexpr int SC_NB = (CAP + 31) / 32 + 8; // Schmidl-Cox blocks (k-space), with slack
@@ -41,6 +43,8 @@ struct alignas(16) Smem {
       float2 tw2[8 * 8];
       float2 g[kMaxBand];                  // conj(H)/|H|^2 (or 1 for passthrough)
       uint32_t bits[MAX_BITS_WORDS];
+      float known[kMaxBand];               // CE symbol signs, band order
+      int16_t band_di[kMaxBand];           // data-subcarrier index, -1 for pilots
     } fq;
     unsigned char raw[UNION_BYTES];
   } u;
@@ -162,60 +166,79 @@ __device__ __forceinline__ int decide(int mod, float cr, float ci, float &margin
 __device__ __forceinline__ void block_reduce_begin() { __syncthreads(); }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevWork w) {
-  __shared__ Smem sm;
-  const int f = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// Frame prefetch: the next frame's samples travel HBM -> VGPRs (PF float4 per
+// lane) while the current frame's FFT/demap/CRC stages run from LDS, so the
+// HBM stream overlaps compute. Routing decisions that need no samples (forced
+// exact, frame longer than LDS) are taken here.
+__device__ __forceinline__ int frame_route(const DevWork &w, int N) {
+  if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
+  if (N > CAP - 8) return AMOD_FLAG_BIG;
+  return 0;
+}
+
+// float4 vector v of a frame (aligned base a0 = off & ~3), zero outside [0, N)
+__device__ __forceinline__ float4 load_vec(const float *src, int v, int ph, int N) {
+  const int i0 = 4 * v - ph; // frame index of component 0
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i0 >= 0 && i0 + 4 <= N) {
+    t = *reinterpret_cast<const float4 *>(src + 4 * v);
+  } else {
+    if (i0 + 0 >= 0 && i0 + 0 < N) t.x = src[4 * v + 0];
+    if (i0 + 1 >= 0 && i0 + 1 < N) t.y = src[4 * v + 1];
+    if (i0 + 2 >= 0 && i0 + 2 < N) t.z = src[4 * v + 2];
+    if (i0 + 3 >= 0 && i0 + 3 < N) t.w = src[4 * v + 3];
+  }
+  return t;
+}
+
+__device__ __forceinline__ void pf_issue(const DevWork &w, int g, float4 (&q)[PF]) {
+  if (g >= w.nframes) return;
+  const int64_t off = w.off[g];
+  const int N = w.len[g];
+  if (frame_route(w, N)) return;
+  const int ph = (int)(off & 3);
+  const int nvec = (ph + N + 3) >> 2;
+  const float *src = w.samples + (off - ph);
+  const int tid = ltid();
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int v = tid + WG * j;
+    q[j] = v < nvec ? load_vec(src, v, ph, N) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// stage 0: registers -> LDS, preprocessSignal statistics (modem.js:213-232):
+// fp64 sum, min, max; sets the per-frame scalars in LDS. Whole workgroup.
+__device__ __forceinline__ void stage_in(const DevCfg &cfg, const DevWork &w, int f, const float4 (&q)[PF], Smem &sm) {
+  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int64_t off = w.off[f];
   const int N = w.len[f];
-  const int SYM = cfg.sym, CP = cfg.cp;
-  const bool dbg = w.dbg != nullptr;
-  amod_debug *D = dbg ? w.dbg + f : nullptr;
-
-  // ------------------------------------------------ routing to the exact path
-  {
-    int route = 0;
-    if (w.options & AMOD_OPT_FORCE_EXACT) route = AMOD_FLAG_FORCED;
-    else if (N > CAP - 8) route = AMOD_FLAG_BIG;
-    if (route) {
-      if (tid == 0) {
-        const int i = atomicAdd(w.fb_count, 1);
-        w.fb_list[i] = f;
-        w.fb_flags[i] = route;
-      }
-      return;
-    }
-  }
-
-  // ------------------------------------------------ stage 0: load + stats
-  const int64_t a0 = off & ~int64_t(3);
-  const int ph = (int)(off - a0);
+  const int route = frame_route(w, N);
+  const int ph = (int)(off & 3);
   const int nvec = (ph + N + 3) >> 2;
   double s = 0.0;
   float mn = INFINITY, mxv = -INFINITY;
   int nonfinite = 0;
-  const float *src = w.samples + a0;
-  for (int v = tid; v < nvec; v += WG) {
-    const int i0 = 4 * v - ph; // frame index of component 0
-    float4 q;
-    if (i0 >= 0 && i0 + 4 <= N) {
-      q = *reinterpret_cast<const float4 *>(src + 4 * v);
-    } else {
-      q.x = (i0 + 0 >= 0 && i0 + 0 < N) ? src[4 * v + 0] : 0.f;
-      q.y = (i0 + 1 >= 0 && i0 + 1 < N) ? src[4 * v + 1] : 0.f;
-      q.z = (i0 + 2 >= 0 && i0 + 2 < N) ? src[4 * v + 2] : 0.f;
-      q.w = (i0 + 3 >= 0 && i0 + 3 < N) ? src[4 * v + 3] : 0.f;
-    }
-    *reinterpret_cast<float4 *>(&sm.x[4 * v]) = q;
-    const float c[4] = {q.x, q.y, q.z, q.w};
+  if (!route) {
+    const float *src = w.samples + (off - ph);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = i0 + j;
-      if (i >= 0 && i < N) {
-        s += (double)c[j];
-        mn = fminf(mn, c[j]);
-        mxv = fmaxf(mxv, c[j]);
-        nonfinite |= !isfinite(c[j]);
+    for (int j = 0; j < PFV; ++j) {
+      const int v = tid + WG * j;
+      if (v < nvec) {
+        const float4 t = j < PF ? q[j] : load_vec(src, v, ph, N);
+        *reinterpret_cast<float4 *>(&sm.x[4 * v]) = t;
+        const int i0 = 4 * v - ph;
+        const float c[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = i0 + k;
+          if (i >= 0 && i < N) {
+            s += (double)c[k];
+            mn = fminf(mn, c[k]);
+            mxv = fmaxf(mxv, c[k]);
+            nonfinite |= !isfinite(c[k]);
+          }
+        }
       }
     }
   }
@@ -243,13 +266,29 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       if (mx > 1e-6) { A = (float)(1.0 / mx); B = (float)(-mean / mx); }
       else { A = 1.f; B = (float)(-mean); }
     }
+    if (route) flags = route;
     sm.n = N; sm.ph = ph; sm.flags = flags; sm.status = AMOD_OK;
     sm.A = A; sm.B = B; sm.mean = mean; sm.mx = mx;
-    sm.coarse = -1; sm.clo = -1; sm.chi = -1; sm.start = 0;
-    if (dbg) { D->mean = mean; D->mx = mx; }
+    sm.coarse = -1; sm.clo = -1; sm.chi = -1; sm.start = 0; sm.fbest = 0.f;
+    if (w.dbg && !route) { w.dbg[f].mean = mean; w.dbg[f].mx = mx; }
   }
   __syncthreads();
-  if (sm.flags & (AMOD_FLAG_NONFINITE | AMOD_FLAG_THRESH)) {
+}
+
+// Stages 1-4 of one frame already staged in LDS by stage_in. `issue_prefetch`
+// is called once the stage no longer issues vector-memory loads it waits on
+// (after the FFT tables are staged), so the next frame streams in behind it.
+template <typename Issue>
+__device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &w, const int f, Smem &sm,
+                                              Issue &&issue_prefetch) {
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid)); // per-frame lane id: nothing lane-derived is hoisted out of the frame loop
+  const int lane = tid & 63, wave = tid >> 6;
+  const int N = sm.n, ph = sm.ph;
+  const int SYM = cfg.sym, CP = cfg.cp;
+  const bool dbg = w.dbg != nullptr;
+  amod_debug *D = dbg ? w.dbg + f : nullptr;
+  if (sm.flags) { // forced / too long / NaN-Inf / peak at threshold
     if (tid == 0) {
       const int i = atomicAdd(w.fb_count, 1);
       w.fb_list[i] = f;
@@ -306,6 +345,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         }
         if ((t & 3) == 0) { sm.u.sc.bz[t >> 2] = zz; sm.u.sc.be[t >> 2] = ee; sm.u.sc.ba[t >> 2] = za; }
       }
+      if (cfg.stop_after == 10) return;
       if (tid == 0) sm.ncand = 0;
       __syncthreads();
       const float gate_lo = 0.01f * (1.f - eps_g), gate_hi = 0.01f * (1.f + eps_g);
@@ -342,32 +382,49 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         }
       }
       __syncthreads();
+      if (cfg.stop_after == 11) return;
       const int ncand = sm.ncand;
       if (ncand > SC_MAXCAND) { // too many blocks near the best: leave it to the exact path
         if (tid == 0) sm.flags |= AMOD_FLAG_COARSE;
         __syncthreads();
         goto to_exact;
       }
-      // (c) slide through candidate blocks position by position
+      // (c) every position of a candidate block: one 32-lane group per block; the
+      // window sums at position d0 + j are the block-start sums plus an exclusive
+      // prefix (across the group) of the per-position slide increments
+      auto cand_eval = [&](int cidx, float &m, int &d, float &ra, float &rb) -> bool {
+        const int j = lane & 31;
+        const int c = sm.u.sc.cand[cidx];
+        float p = 0.f;
+        ra = 0.f; rb = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
+        d = SC_BLK * c - ph + j;
+        const float y0 = (d >= 0 && d < N) ? Y(d) : 0.f;
+        const float y1 = (d + 256 < N) ? Y(d + 256) : 0.f;
+        const float y2 = (d + 512 < N) ? Y(d + 512) : 0.f;
+        const float z0 = (d >= 0 && d < N - 256) ? y0 * y1 : 0.f;
+        const float z1 = (d + 256 < N - 256) ? y1 * y2 : 0.f;
+        const float vp = z1 - z0, va = fmaf(y1, y1, -y0 * y0), vb = fmaf(y2, y2, -y1 * y1);
+        float sp = vp, sa = va, sb = vb; // inclusive scans over the 32-lane group
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const float tp = __shfl_up(sp, o, 32), ta = __shfl_up(sa, o, 32), tb = __shfl_up(sb, o, 32);
+          if (j >= o) { sp += tp; sa += ta; sb += tb; }
+        }
+        p += sp - vp; ra += sa - va; rb += sb - vb;
+        const bool ok = d >= 0 && d <= E && ra > gate_lo && rb > gate_lo;
+        m = ok ? (p * p) / (ra * rb) : -1.f;
+        return ok;
+      };
       float best = -1.f;
       int bidx = 0x7fffffff;
-      for (int j = tid; j < ncand; j += WG) {
-        const int c = sm.u.sc.cand[j];
-        float p = 0.f, ra = 0.f, rb = 0.f;
-        for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
-        const int d0 = SC_BLK * c - ph, dend = min(d0 + SC_BLK - 1, E);
-        for (int d = d0; d <= dend; ++d) {
-          if (d >= 0 && ra > gate_lo && rb > gate_lo) {
-            const float m = (p * p) / (ra * rb);
-            if (m > best || (m == best && d < bidx)) { best = m; bidx = d; }
-          }
-          if (d < dend) {
-            const float a = d >= 0 ? Y(d) : 0.f, mid = d + 256 >= 0 ? Y(d + 256) : 0.f, bb = Y(d + 512);
-            p = fmaf(mid, bb - a, p);
-            ra = fmaf(-a, a, fmaf(mid, mid, ra));
-            rb = fmaf(-mid, mid, fmaf(bb, bb, rb));
-          }
-        }
+      for (int g = 2 * wave + (lane >> 5); g - (lane >> 5) < ncand; g += 2 * NWAVE) {
+        if (g < ncand) {
+          float m, ra, rb;
+          int d;
+          if (cand_eval(g, m, d, ra, rb) && (m > best || (m == best && d < bidx))) { best = m; bidx = d; }
+        } // a group's 32 lanes share g, so the width-32 shuffles stay inside active lanes
       }
       // block argmax (max value, then lowest index)
       {
@@ -383,28 +440,18 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
         }
         __syncthreads();
       }
+      if (cfg.stop_after == 12) return;
       const float CB = sm.cbest;
       // candidate range {d : metric >= CB - eps_c}, and gate uncertainty there
       int lo = 0x7fffffff, hi = -1, unc = 0;
       if (CB > 0.5f - eps_c) {
-        for (int j = tid; j < ncand; j += WG) {
-          const int c = sm.u.sc.cand[j];
-          float p = 0.f, ra = 0.f, rb = 0.f;
-          for (int q = 0; q < 8; ++q) { p += sm.u.sc.bz[c + q]; ra += sm.u.sc.be[c + q]; rb += sm.u.sc.be[c + 8 + q]; }
-          const int d0 = SC_BLK * c - ph, dend = min(d0 + SC_BLK - 1, E);
-          for (int d = d0; d <= dend; ++d) {
-            if (d >= 0 && ra > gate_lo && rb > gate_lo) {
-              const float m = (p * p) / (ra * rb);
-              if (m >= CB - eps_c) {
-                lo = min(lo, d); hi = max(hi, d);
-                unc |= (ra <= gate_hi || rb <= gate_hi);
-              }
-            }
-            if (d < dend) {
-              const float a = d >= 0 ? Y(d) : 0.f, mid = d + 256 >= 0 ? Y(d + 256) : 0.f, bb = Y(d + 512);
-              p = fmaf(mid, bb - a, p);
-              ra = fmaf(-a, a, fmaf(mid, mid, ra));
-              rb = fmaf(-mid, mid, fmaf(bb, bb, rb));
+        for (int g = 2 * wave + (lane >> 5); g - (lane >> 5) < ncand; g += 2 * NWAVE) {
+          if (g < ncand) {
+            float m, ra, rb;
+            int d;
+            if (cand_eval(g, m, d, ra, rb) && m >= CB - eps_c) {
+              lo = min(lo, d); hi = max(hi, d);
+              unc |= (ra <= gate_hi || rb <= gate_hi);
             }
           }
         }
@@ -566,10 +613,12 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
     // tables + clear bit array
     for (int i = tid; i < 8 * 64; i += WG) sm.u.fq.tw1[i] = cfg.t.tw1[i];
     for (int i = tid; i < 64; i += WG) sm.u.fq.tw2[i] = cfg.t.tw2[i];
+    for (int i = tid; i < cfg.nband; i += WG) { sm.u.fq.known[i] = cfg.t.known[i]; sm.u.fq.band_di[i] = cfg.t.band_di[i]; }
     for (int i = tid; i < nwords; i += WG) sm.u.fq.bits[i] = 0u;
     if (tid == 0) { sm.nsym = M; sm.data0 = data0; sm.gmax = 0.f; sm.zce = 0.f; }
     if (nbits > MAX_BITS_WORDS * 32) { if (tid == 0) sm.flags |= AMOD_FLAG_BIG; }
     __syncthreads();
+    issue_prefetch(); // no vector-memory loads are waited on from here to the CRC
     if (sm.flags) goto to_exact;
     const bool odd = (M & 1) != 0;
     const int njobs = 1 + (M - (odd ? 1 : 0)) / 2;
@@ -593,17 +642,20 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       float2 v[8];
       int const1 = 0, const2 = 0;
       if (active) {
-        float mn1 = INFINITY, mx1 = -INFINITY, mn2 = INFINITY, mx2 = -INFINITY;
+        // a window is constant iff every raw sample equals its first one (NaN frames never get here)
+        const float f1 = X[pos1 + CP], f2 = s2 >= 0 ? X[pos2 + CP] : 0.f;
+        int ne1 = 0, ne2 = 0;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const int i = CP + lane + 64 * m;
           const float r1 = X[pos1 + i];
           const float r2 = s2 >= 0 ? X[pos2 + i] : 0.f;
-          mn1 = fminf(mn1, r1); mx1 = fmaxf(mx1, r1); mn2 = fminf(mn2, r2); mx2 = fmaxf(mx2, r2);
+          ne1 |= r1 != f1;
+          ne2 |= r2 != f2;
           v[m] = make_float2(fmaf(r1, A, B), s2 >= 0 ? fmaf(r2, A, B) : 0.f);
         }
-        const1 = wave_min(mn1) == wave_max(mx1);
-        const2 = wave_min(mn2) == wave_max(mx2);
+        const1 = __ballot(ne1) == 0;
+        const2 = __ballot(ne2) == 0;
         fft512_wave(v, xb, sm);
         if (job == 0) {
           // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
@@ -620,7 +672,7 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
             if (!const1) {
               const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
               const float2 y = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-              const float kn = cfg.t.known[b];
+              const float kn = sm.u.fq.known[b];
               h = make_float2(y.x * kn, y.y * kn);
             }
             const float m2 = h.x * h.x + h.y * h.y;
@@ -644,90 +696,105 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
       }
       if (!active) continue;
       const float gmax = sm.gmax, zce = sm.zce;
-      // ---- per data symbol of this job: equalise, pilot phase, demap
-      for (int which = 0; which < 2; ++which) {
+      // ---- both data symbols of this job in one pass: equalise, pilot phase, demap
+      {
         int ln = lane;
-        asm volatile("" : "+v"(ln)); // per-iteration lane (keeps debug/bit addresses out of registers)
-        const int sidx = which == 0 ? s1 : s2;
-        if (sidx < 0) continue; // CE or absent
-        const bool cst = which == 0 ? const1 : const2;
+        asm volatile("" : "+v"(ln)); // per-round lane (keeps debug/bit addresses out of registers)
+        const bool live1 = s1 >= 0 && !const1, live2 = s2 >= 0 && !const2;
         uint32_t *bits = sm.u.fq.bits;
-        const int sbase = sidx * cfg.ndata * cfg.bps;
-        if (cst) {
-          // constant window: every bin is exactly 0 in the reference -> origin decision
-          for (int b = ln; b < nband; b += 64) {
-            const int di = cfg.t.band_di[b];
-            if (di < 0) continue;
-            const int pos = sbase + di * cfg.bps;
-            const uint32_t val = (uint32_t)cfg.origin_idx << (32 - cfg.bps - (pos & 31));
-            if (val) atomicOr(&bits[pos >> 5], val);
-          }
-          if (dbg && sidx < AMOD_DBG_SYMS) if (ln == 0) D->phase[sidx] = 0.0;
-          if (dbg && sidx == 0)
-            for (int b = ln; b < nband; b += 64) { D->x_re[b] = 0; D->x_im[b] = 0; D->eq_re[b] = 0; D->eq_im[b] = 0; }
-          continue;
-        }
-        float2 eq[4];
-        float zmax = 0.f, emax = 0.f;
-        float psum = 0.f, perr = 0.f;
-        int pcnt = 0, pflag = 0;
+        const int per_sym = cfg.ndata * cfg.bps;
+        float2 e1[4], e2[4];
+        float zm = 0.f, em1 = 0.f, em2 = 0.f;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int b = ln + 64 * rr;
-          eq[rr] = make_float2(0.f, 0.f);
+          e1[rr] = e2[rr] = make_float2(0.f, 0.f);
           if (b < nband) {
             const int k = cfg.sub_start + b;
             const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
-            zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
-            const float2 xs = which == 0 ? make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y))
-                                         : make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
+            zm = fmaxf(zm, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
+            // Z = x1 + i x2:  X1 = (Z[k] + conj Z[-k]) / 2,  X2 = (Z[k] - conj Z[-k]) / 2i
+            const float2 x1 = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
+            const float2 x2 = make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
             const float2 g = sm.u.fq.g[b];
-            eq[rr] = cmul(xs, g);
-            emax = fmaxf(emax, fabsf(eq[rr].x) + fabsf(eq[rr].y));
-            if (dbg && sidx == 0) { D->x_re[b] = xs.x; D->x_im[b] = xs.y; D->eq_re[b] = eq[rr].x; D->eq_im[b] = eq[rr].y; }
+            e1[rr] = cmul(x1, g);
+            e2[rr] = cmul(x2, g);
+            em1 = fmaxf(em1, fabsf(e1[rr].x) + fabsf(e1[rr].y));
+            em2 = fmaxf(em2, fabsf(e2[rr].x) + fabsf(e2[rr].y));
+            if (dbg && (s1 == 0 || s2 == 0)) {
+              const bool one = s1 == 0;
+              const float2 xx = one ? x1 : x2, ee = one ? e1[rr] : e2[rr];
+              const bool c = one ? const1 : const2;
+              D->x_re[b] = c ? 0.f : xx.x; D->x_im[b] = c ? 0.f : xx.y;
+              D->eq_re[b] = c ? 0.f : ee.x; D->eq_im[b] = c ? 0.f : ee.y;
+            }
           }
         }
-        zmax = wave_max(zmax);
-        emax = wave_max(emax);
-        // error bound of eq (fp32 FFT + channel estimate), see DESIGN.md §guards
-        const float delta = 2e-6f * cfg.guard * (zmax + emax * zce) * gmax + 1e-12f;
+        // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
+        const float gsc = 2e-6f * cfg.guard * gmax;
+        float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { d1 = fmaxf(d1, __shfl_xor(d1, o, 64)); d2 = fmaxf(d2, __shfl_xor(d2, o, 64)); }
+        d1 += 1e-12f; d2 += 1e-12f;
+        // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
+        float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f;
+        int pc1 = 0, pc2 = 0, pflag = 0;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int b = ln + 64 * rr;
-          if (b < nband && cfg.t.band_di[b] < 0) {
-            const float er = eq[rr].x, ei = eq[rr].y;
-            const float aer = fabsf(er);
-            if (aer > 1e-6f) {
-              psum += ei / er;
-              pcnt += 1;
-              perr += delta * (1.f / aer + fabsf(ei) / (aer * aer));
-            }
-            if (fabsf(aer - 1e-6f) <= 2.f * delta + 1e-7f) pflag = 1;
-          }
+          const bool pil = b < nband && sm.u.fq.band_di[b] < 0;
+          const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
+          const bool ok1 = pil && a1 > 1e-6f, ok2 = pil && a2 > 1e-6f;
+          if (ok1) { ps1 += e1[rr].y / e1[rr].x; pe1 += 1.f / a1 + fabsf(e1[rr].y) / (a1 * a1); }
+          if (ok2) { ps2 += e2[rr].y / e2[rr].x; pe2 += 1.f / a2 + fabsf(e2[rr].y) / (a2 * a2); }
+          pc1 += __popcll(__ballot(ok1));
+          pc2 += __popcll(__ballot(ok2));
+          pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
         }
-        psum = wave_sum(psum); perr = wave_sum(perr); pcnt = wave_sum(pcnt); pflag = wave_or(pflag);
-        const float phase = pcnt > 0 ? psum / (float)pcnt : 0.f;
-        const float dphase = pcnt > 0 ? perr / (float)pcnt : 0.f;
-        if (pflag) wflags |= AMOD_FLAG_PHASE;
-        if (dbg && sidx < AMOD_DBG_SYMS && ln == 0) D->phase[sidx] = phase;
-        const float tau = 4.f * (delta * (1.f + fabsf(phase)) + emax * dphase) + 1e-9f;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          ps1 += __shfl_xor(ps1, o, 64); pe1 += __shfl_xor(pe1, o, 64);
+          ps2 += __shfl_xor(ps2, o, 64); pe2 += __shfl_xor(pe2, o, 64);
+        }
+        if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
+        const float ph1 = pc1 > 0 ? ps1 / (float)pc1 : 0.f, ph2 = pc2 > 0 ? ps2 / (float)pc2 : 0.f;
+        const float dp1 = pc1 > 0 ? d1 * pe1 / (float)pc1 : 0.f, dp2 = pc2 > 0 ? d2 * pe2 / (float)pc2 : 0.f;
+        const float tau1 = 4.f * (d1 * (1.f + fabsf(ph1)) + em1 * dp1) + 1e-9f;
+        const float tau2 = 4.f * (d2 * (1.f + fabsf(ph2)) + em2 * dp2) + 1e-9f;
+        if (dbg && ln == 0) {
+          if (s1 >= 0 && s1 < AMOD_DBG_SYMS) D->phase[s1] = const1 ? 0.f : ph1;
+          if (s2 >= 0 && s2 < AMOD_DBG_SYMS) D->phase[s2] = const2 ? 0.f : ph2;
+        }
+        // a constant FFT window has an all-zero spectrum in the reference: every data
+        // subcarrier takes the origin decision (ties resolve to the first point)
         int dflag = 0;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int b = ln + 64 * rr;
           if (b >= nband) continue;
-          const int di = cfg.t.band_di[b];
+          const int di = sm.u.fq.band_di[b];
           if (di < 0) continue;
-          const float cr = fmaf(eq[rr].y, phase, eq[rr].x);
-          const float ci = fmaf(-eq[rr].x, phase, eq[rr].y);
-          float margin;
-          const int idx = decide(cfg.mod, cr, ci, margin);
-          dflag |= margin <= tau;
-          const int pos = sbase + di * cfg.bps;
-          const uint32_t val = (uint32_t)idx << (32 - cfg.bps - (pos & 31));
-          if (val) atomicOr(&bits[pos >> 5], val);
+#pragma unroll
+          for (int which = 0; which < 2; ++which) {
+            const int sidx = which == 0 ? s1 : s2;
+            if (sidx < 0) continue;
+            const bool live = which == 0 ? live1 : live2;
+            int idx = cfg.origin_idx;
+            if (live) {
+              const float2 e = which == 0 ? e1[rr] : e2[rr];
+              const float ph = which == 0 ? ph1 : ph2;
+              const float cr = fmaf(e.y, ph, e.x);
+              const float ci = fmaf(-e.x, ph, e.y);
+              float margin;
+              idx = decide(cfg.mod, cr, ci, margin);
+              dflag |= margin <= (which == 0 ? tau1 : tau2);
+            }
+            const int pos = sidx * per_sym + di * cfg.bps;
+            const uint32_t val = (uint32_t)idx << (32 - cfg.bps - (pos & 31));
+            if (val) atomicOr(&bits[pos >> 5], val);
+          }
         }
-        if (wave_or(dflag)) wflags |= AMOD_FLAG_DEMAP;
+        if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
       }
     }
     wflags = wave_or(wflags);
@@ -775,6 +842,20 @@ to_exact:
     w.fb_list[i] = f;
     w.fb_flags[i] = sm.flags;
   }
+}
+
+// One workgroup per frame (LDS admits one per CU; the dispatcher refills a CU as
+// soon as its frame is done, so other CUs' compute overlaps this CU's load).
+// Every float4 of the frame is requested before the first is consumed.
+__global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevWork w) {
+  __shared__ Smem sm;
+  const int f = blockIdx.x;
+  {
+    float4 q[PF];
+    pf_issue(w, f, q);
+    stage_in(cfg, w, f, q, sm);
+  }
+  process_frame(cfg, w, f, sm, []() {});
 }
 
 } // namespace

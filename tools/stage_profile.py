@@ -28,7 +28,7 @@ def main():
     pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
     lib = L.load()
     rows = []
-    for stop in (0, 1, 2, 3, 99):
+    for stop in [int(s) for s in os.environ.get("STAGES", "0,1,2,3,99").split(",")]:
         os.environ["AMOD_STOP_AFTER"] = str(stop)
         dm = amodem.Demodulator(0)
         dm.reserve(cfg, F, 35874)
