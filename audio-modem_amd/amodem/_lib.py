@@ -78,6 +78,7 @@ SIGNATURES = {
                                     C.POINTER(C.c_int64)]),
     "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,
                                            C.c_int64, C.c_uint32, _P, _P]),
+    "amod_debug_stamps": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_crc32": (C.c_uint32, [C.c_char_p, C.c_size_t]),
     "amod_preamble1": (C.c_int, [C.POINTER(Cfg), _P]),
     "amod_tx_legacy": (C.c_int64, [C.POINTER(Cfg), C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, _P]),

@@ -68,6 +68,7 @@ struct DevWork {
   int64_t xs_stride;  // floats per slot
   int64_t bits_stride;// words per slot
   uint32_t options;
+  unsigned long long *stamps; // diagnostics (AMOD_STAMPS=1): per-frame s_memtime marks, 32 per frame
 };
 
 // ---------------------------------------------------------------- helpers --

@@ -278,6 +278,12 @@ __device__ __forceinline__ void stage_in(const DevCfg &cfg, const DevWork &w, in
 // Stages 1-4 of one frame already staged in LDS by stage_in. `issue_prefetch`
 // is called once the stage no longer issues vector-memory loads it waits on
 // (after the FFT tables are staged), so the next frame streams in behind it.
+// diagnostics only (AMOD_STAMPS): wave 0's shader-clock timeline of a frame
+#define STAMP(k)                                                                        \
+  do {                                                                                  \
+    if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 template <typename Issue>
 __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &w, const int f, Smem &sm,
                                               Issue &&issue_prefetch) {
@@ -300,6 +306,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
   const float *X = sm.x + ph; // frame sample i at X[i]
   auto Y = [&](int i) -> float { return fmaf(X[i], A, B); };
 
+  STAMP(1);
   if (cfg.stop_after == 0) return;
   int start = 0;
   const float eps_c = 2e-3f * cfg.guard;     // Schmidl-Cox metric guard (absolute)
@@ -348,6 +355,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
       if (cfg.stop_after == 10) return;
       if (tid == 0) sm.ncand = 0;
       __syncthreads();
+      STAMP(2);
       const float gate_lo = 0.01f * (1.f - eps_g), gate_hi = 0.01f * (1.f + eps_g);
       const int ncb = (E + ph) / SC_BLK + 1; // blocks holding at least one position d in [0, E]
       // (a) exact window sums at block starts -> lower bound L on the best metric
@@ -382,6 +390,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
         }
       }
       __syncthreads();
+      STAMP(3);
       if (cfg.stop_after == 11) return;
       const int ncand = sm.ncand;
       if (ncand > SC_MAXCAND) { // too many blocks near the best: leave it to the exact path
@@ -440,6 +449,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
         }
         __syncthreads();
       }
+      STAMP(4);
       if (cfg.stop_after == 12) return;
       const float CB = sm.cbest;
       // candidate range {d : metric >= CB - eps_c}, and gate uncertainty there
@@ -473,6 +483,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
     }
     if (sm.flags) goto to_exact;
     if (sm.status != AMOD_OK) goto finish_error;
+    STAMP(5);
     if (cfg.stop_after == 1) return;
 
     // ---------------------------------------------- stage 2: fine timing
@@ -594,6 +605,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
       if (sm.status != AMOD_OK) goto finish_error;
       start = sm.start;
     }
+    STAMP(6);
     if (cfg.stop_after == 2) return;
     // CE / data checks (modem.js:591-600)
     if (start + 3 * SYM > N) { if (tid == 0) sm.status = AMOD_E_SHORT_CE; __syncthreads(); goto finish_error; }
@@ -618,6 +630,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
     if (tid == 0) { sm.nsym = M; sm.data0 = data0; sm.gmax = 0.f; sm.zce = 0.f; }
     if (nbits > MAX_BITS_WORDS * 32) { if (tid == 0) sm.flags |= AMOD_FLAG_BIG; }
     __syncthreads();
+    STAMP(7);
     issue_prefetch(); // no vector-memory loads are waited on from here to the CRC
     if (sm.flags) goto to_exact;
     const bool odd = (M & 1) != 0;
@@ -657,6 +670,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
         const1 = __ballot(ne1) == 0;
         const2 = __ballot(ne2) == 0;
         fft512_wave(v, xb, sm);
+        if (round == 0) STAMP(8);
         if (job == 0) {
           // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
           float zmax = 0.f;
@@ -693,6 +707,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
         gmax_local = wave_max(gmax_local);
         if (wave == 0 && lane == 0) sm.gmax = gmax_local;
         __syncthreads();
+        STAMP(9);
       }
       if (!active) continue;
       const float gmax = sm.gmax, zce = sm.zce;
@@ -796,10 +811,12 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
         }
         if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
       }
+      STAMP(10 + round);
     }
     wflags = wave_or(wflags);
     if (lane == 0 && wflags) atomicOr(&sm.flags, wflags);
     __syncthreads();
+    STAMP(14);
     if (sm.flags) goto to_exact;
     // ------------------------------------------------ stage 4: finish
     if (cfg.stop_after == 3) return;
@@ -818,6 +835,7 @@ __device__ __forceinline__ void process_frame(const DevCfg &cfg, const DevWork &
       r.nbits = nbits;
       if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = sm.fbest; r.coarse_idx = sm.coarse; r.preamble_idx = start; }
       finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr);
+      STAMP(15);
       return;
     }
   }
@@ -851,6 +869,8 @@ __global__ __launch_bounds__(WG) void k_decode_fast(const DevCfg cfg, const DevW
   __shared__ Smem sm;
   const int f = blockIdx.x;
   {
+    const int tid = threadIdx.x;
+    STAMP(0);
     float4 q[PF];
     pf_issue(w, f, q);
     stage_in(cfg, w, f, q, sm);

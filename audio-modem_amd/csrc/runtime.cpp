@@ -237,6 +237,8 @@ struct amod_ctx {
   // host-path staging
   DevBuf h_samples, h_off, h_len, h_res, h_payload;
   std::mutex mu;
+  DevBuf stamps;
+  int64_t nstamps = 0;
   // kernel timing (amod_set_profiling)
   bool profiling = false;
   std::vector<std::array<hipEvent_t, 3>> ev_used, ev_free;
@@ -416,6 +418,12 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
+  if (getenv("AMOD_STAMPS")) { // diagnostics: per-frame s_memtime marks of the fast kernel
+    HIP_TRY(ctx->stamps.ensure(sizeof(unsigned long long) * 32 * (size_t)nframes));
+    HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, sizeof(unsigned long long) * 32 * (size_t)nframes, s));
+    w.stamps = (unsigned long long *)ctx->stamps.p;
+    ctx->nstamps = nframes;
+  }
   HIP_TRY(hipMemsetAsync(fb, 0, 256, s));
   std::array<hipEvent_t, 3> ev{};
   if (ctx->profiling) {
@@ -691,6 +699,14 @@ int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_n, double *e
   if (exact_n) *exact_n = (int64_t)ctx->ev_used.size();
   ctx->ev_used.clear();
   return AMOD_SUCCESS;
+}
+
+int64_t amod_debug_stamps(amod_ctx *ctx, uint64_t *out, int64_t cap) {
+  if (!ctx || !ctx->stamps.p) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int64_t n = std::min<int64_t>(cap, 32 * ctx->nstamps);
+  if (hipMemcpy(out, ctx->stamps.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
 }
 
 uint32_t amod_crc32(const uint8_t *d, size_t n) {

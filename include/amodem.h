@@ -174,6 +174,10 @@ int amod_decode_device_debug(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, c
                              amod_result *results, uint8_t *payload, int64_t payload_stride,
                              uint32_t options, void *stream, amod_debug *debug);
 
+/* diagnostics: with AMOD_STAMPS set in the environment, the fast kernel records
+   32 s_memtime marks per frame (wave 0); copies up to cap of them, returns count */
+int64_t amod_debug_stamps(amod_ctx *ctx, uint64_t *out, int64_t cap);
+
 /* ---- host utilities (reference-equivalent, bit-exact) ---- */
 uint32_t amod_crc32(const uint8_t *data, size_t n);
 int amod_preamble1(const amod_cfg *cfg, float *out); /* symbol_len floats */
