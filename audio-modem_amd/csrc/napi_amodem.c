@@ -1,0 +1,496 @@
+/*
+ * napi_amodem.c — N-API binding of libamodem (include/amodem.h) for Node.js.
+ *
+ * The thin C shim the JavaScript surface (audio-modem_amd/js/modem.js) calls:
+ * plain typed arrays in, typed arrays out, no state beyond one lazily opened
+ * amod_ctx per device. HIP failures throw Error(amod_last_error); per-frame
+ * outcomes come back as amod_result records for the JS side to format with the
+ * reference's exact strings (modem.js:557-654, 770-849).
+ *
+ *   decode(samples: Float32Array, offsets: Float64Array|null, lengths: Int32Array|null,
+ *          cfg: object, mode: number, options: number, device?: number)
+ *       -> { results: ArrayBuffer (96 B per frame), payload: ArrayBuffer, stride: number }
+ *   decodeAsync(...same...) -> Promise of the same object (napi_async_work)
+ *   crc32(Uint8Array) -> number                     modem.js:443-457
+ *   preamble1(cfg) -> Float32Array                  modem.js:158-170
+ *   txLegacy(cfg, data: Uint8Array, name: Uint8Array) -> Float32Array   modem.js:498-555
+ *   txMeta(cfg, totalChunks, totalSize, chunkSize, name: Uint8Array)    modem.js:758
+ *   txChunk(cfg, data: Uint8Array, seq)                                modem.js:763
+ *   txTestSignal(cfg) -> Float32Array                                   modem.js:914-973
+ *   estimateFrameSamples(cfg, payloadBytes) -> number                   modem.js:863-874
+ *   numDataSubs(cfg) -> number, payloadStride(cfg, maxLen) -> number, abiVersion() -> number
+ *
+ * cfg = { fft_size, cp_len, symbol_len, sample_rate, sub_start, sub_end,
+ *         pilots: number[], modulation: 0|1|2, repetition }
+ */
+#define NAPI_VERSION 4
+#include <node_api.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "amodem.h"
+
+#define MAX_DEVICES 16
+static amod_ctx *g_ctx[MAX_DEVICES];
+
+#define NAPI_TRY(env, call)                                                 \
+  do {                                                                      \
+    if ((call) != napi_ok) {                                                \
+      const napi_extended_error_info *ei_ = NULL;                           \
+      napi_get_last_error_info((env), &ei_);                                \
+      bool pending_ = false;                                                \
+      napi_is_exception_pending((env), &pending_);                          \
+      if (!pending_)                                                        \
+        napi_throw_error((env), NULL, ei_ && ei_->error_message ? ei_->error_message : "N-API call failed"); \
+      return NULL;                                                          \
+    }                                                                       \
+  } while (0)
+
+static napi_value throw_msg(napi_env env, const char *msg) {
+  napi_throw_error(env, NULL, msg);
+  return NULL;
+}
+
+static amod_ctx *get_ctx(napi_env env, int device) {
+  if (device < 0 || device >= MAX_DEVICES) {
+    napi_throw_range_error(env, NULL, "device index out of range");
+    return NULL;
+  }
+  if (!g_ctx[device]) {
+    amod_ctx *c = NULL;
+    if (amod_open(device, &c) != AMOD_SUCCESS) {
+      const char *e = amod_last_error(NULL);
+      napi_throw_error(env, NULL, e && *e ? e : "amod_open failed");
+      return NULL;
+    }
+    g_ctx[device] = c;
+  }
+  return g_ctx[device];
+}
+
+static int get_i32_prop(napi_env env, napi_value obj, const char *name, int32_t *out) {
+  napi_value v;
+  bool has = false;
+  if (napi_has_named_property(env, obj, name, &has) != napi_ok || !has) return 0;
+  if (napi_get_named_property(env, obj, name, &v) != napi_ok) return 0;
+  return napi_get_value_int32(env, v, out) == napi_ok;
+}
+
+/* JS cfg object -> amod_cfg; throws TypeError and returns 0 on a malformed object */
+static int to_cfg(napi_env env, napi_value obj, amod_cfg *c) {
+  memset(c, 0, sizeof *c);
+  static const char *names[] = {"fft_size", "cp_len", "symbol_len", "sample_rate", "sub_start", "sub_end",
+                                "modulation", "repetition"};
+  int32_t *dst[] = {&c->fft_size, &c->cp_len, &c->symbol_len, &c->sample_rate, &c->sub_start, &c->sub_end,
+                    &c->modulation, &c->repetition};
+  for (int i = 0; i < 8; ++i)
+    if (!get_i32_prop(env, obj, names[i], dst[i])) {
+      char msg[96];
+      snprintf(msg, sizeof msg, "cfg.%s missing or not a number", names[i]);
+      napi_throw_type_error(env, NULL, msg);
+      return 0;
+    }
+  napi_value pil;
+  bool is_arr = false;
+  uint32_t n = 0;
+  if (napi_get_named_property(env, obj, "pilots", &pil) != napi_ok || napi_is_array(env, pil, &is_arr) != napi_ok ||
+      !is_arr || napi_get_array_length(env, pil, &n) != napi_ok || n > AMOD_MAX_PILOTS) {
+    napi_throw_type_error(env, NULL, "cfg.pilots must be an array of at most 32 numbers");
+    return 0;
+  }
+  c->npilots = (int32_t)n;
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value e;
+    if (napi_get_element(env, pil, i, &e) != napi_ok || napi_get_value_int32(env, e, &c->pilots[i]) != napi_ok) {
+      napi_throw_type_error(env, NULL, "cfg.pilots must be an array of numbers");
+      return 0;
+    }
+  }
+  return 1;
+}
+
+/* typed array view: data pointer + element count, checks the element type */
+static int typed(napi_env env, napi_value v, napi_typedarray_type want, void **data, size_t *len) {
+  bool is = false;
+  if (napi_is_typedarray(env, v, &is) != napi_ok || !is) return 0;
+  napi_typedarray_type t;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok) return 0;
+  return t == want;
+}
+
+static int is_nullish(napi_env env, napi_value v) {
+  napi_valuetype t;
+  return napi_typeof(env, v, &t) == napi_ok && (t == napi_null || t == napi_undefined);
+}
+
+/* ------------------------------------------------------------------ decode */
+typedef struct {
+  amod_ctx *ctx;
+  amod_cfg cfg;
+  int32_t mode, nframes;
+  uint32_t options;
+  const float *samples;
+  int64_t nsamples;
+  int64_t *offsets;
+  int32_t *lengths;
+  int64_t stride;
+  void *results, *payload; /* ArrayBuffer backing stores (owned by JS objects) */
+  int rc;
+  char err[256];
+  /* async only */
+  napi_ref refs[3];
+  napi_value res_ab, pay_ab;
+  napi_ref res_ref, pay_ref;
+  napi_deferred deferred;
+  napi_async_work work;
+} decode_job;
+
+/* parse args into a job; allocates offsets/lengths and the output ArrayBuffers */
+static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_value argv_out[3]) {
+  size_t argc = 7;
+  napi_value argv[7];
+  memset(j, 0, sizeof *j);
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 6) {
+    napi_throw_type_error(env, NULL, "decode(samples, offsets, lengths, cfg, mode, options[, device])");
+    return 0;
+  }
+  void *sp;
+  size_t ns;
+  if (!typed(env, argv[0], napi_float32_array, &sp, &ns)) {
+    napi_throw_type_error(env, NULL, "samples must be a Float32Array");
+    return 0;
+  }
+  j->samples = (const float *)sp;
+  j->nsamples = (int64_t)ns;
+  if (!to_cfg(env, argv[3], &j->cfg)) return 0;
+  if (napi_get_value_int32(env, argv[4], &j->mode) != napi_ok) {
+    napi_throw_type_error(env, NULL, "mode must be a number");
+    return 0;
+  }
+  if (napi_get_value_uint32(env, argv[5], &j->options) != napi_ok) j->options = 0;
+  int32_t device = 0;
+  if (argc >= 7 && !is_nullish(env, argv[6]) && napi_get_value_int32(env, argv[6], &device) != napi_ok) device = 0;
+  j->ctx = get_ctx(env, device);
+  if (!j->ctx) return 0;
+
+  if (is_nullish(env, argv[1])) { /* one frame: the whole buffer */
+    j->nframes = 1;
+    j->offsets = (int64_t *)calloc(1, sizeof(int64_t));
+    j->lengths = (int32_t *)calloc(1, sizeof(int32_t));
+    if (!j->offsets || !j->lengths) return throw_msg(env, "out of memory"), 0;
+    if (ns > INT32_MAX) return napi_throw_range_error(env, NULL, "frame longer than 2^31-1 samples"), 0;
+    j->lengths[0] = (int32_t)ns;
+  } else {
+    void *op, *lp;
+    size_t no, nl;
+    if (!typed(env, argv[1], napi_float64_array, &op, &no) || !typed(env, argv[2], napi_int32_array, &lp, &nl) ||
+        no != nl || no > INT32_MAX) {
+      napi_throw_type_error(env, NULL, "offsets must be a Float64Array and lengths an Int32Array of equal length");
+      return 0;
+    }
+    j->nframes = (int32_t)no;
+    j->offsets = (int64_t *)malloc(sizeof(int64_t) * (no ? no : 1));
+    j->lengths = (int32_t *)malloc(sizeof(int32_t) * (no ? no : 1));
+    if (!j->offsets || !j->lengths) return throw_msg(env, "out of memory"), 0;
+    const double *od = (const double *)op;
+    const int32_t *ld = (const int32_t *)lp;
+    for (size_t i = 0; i < no; ++i) {
+      const double o = od[i];
+      if (!(o >= 0) || o != (double)(int64_t)o || ld[i] < 0 || (int64_t)o + ld[i] > (int64_t)ns) {
+        napi_throw_range_error(env, NULL, "frame slice outside the sample buffer");
+        return 0;
+      }
+      j->offsets[i] = (int64_t)o;
+      j->lengths[i] = ld[i];
+    }
+  }
+  int32_t maxlen = 0;
+  for (int32_t i = 0; i < j->nframes; ++i) maxlen = j->lengths[i] > maxlen ? j->lengths[i] : maxlen;
+  j->stride = amod_payload_stride(&j->cfg, maxlen);
+  if (j->stride <= 0) {
+    napi_throw_type_error(env, NULL, "invalid OFDM configuration");
+    return 0;
+  }
+  if (napi_create_arraybuffer(env, (size_t)j->nframes * sizeof(amod_result), &j->results, &j->res_ab) != napi_ok ||
+      napi_create_arraybuffer(env, (size_t)j->nframes * (size_t)j->stride, &j->payload, &j->pay_ab) != napi_ok) {
+    napi_throw_error(env, NULL, "cannot allocate decode outputs");
+    return 0;
+  }
+  if (j->nframes) {
+    memset(j->results, 0, (size_t)j->nframes * sizeof(amod_result));
+    memset(j->payload, 0, (size_t)j->nframes * (size_t)j->stride);
+  }
+  argv_out[0] = argv[0];
+  argv_out[1] = argv[1];
+  argv_out[2] = argv[2];
+  return 1;
+}
+
+static void run_decode(decode_job *j) {
+  j->rc = amod_decode_host(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths, j->nframes,
+                           (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options);
+  if (j->rc != AMOD_SUCCESS) {
+    const char *e = amod_last_error(j->ctx);
+    snprintf(j->err, sizeof j->err, "libamodem error %d: %s", j->rc, e ? e : "");
+  }
+}
+
+static napi_value result_object(napi_env env, decode_job *j, napi_value res_ab, napi_value pay_ab) {
+  napi_value out, st;
+  NAPI_TRY(env, napi_create_object(env, &out));
+  NAPI_TRY(env, napi_set_named_property(env, out, "results", res_ab));
+  NAPI_TRY(env, napi_set_named_property(env, out, "payload", pay_ab));
+  NAPI_TRY(env, napi_create_double(env, (double)j->stride, &st));
+  NAPI_TRY(env, napi_set_named_property(env, out, "stride", st));
+  return out;
+}
+
+static void free_job(decode_job *j) {
+  free(j->offsets);
+  free(j->lengths);
+  j->offsets = NULL;
+  j->lengths = NULL;
+}
+
+static napi_value js_decode(napi_env env, napi_callback_info info) {
+  decode_job j;
+  napi_value keep[3];
+  if (!prepare(env, info, &j, keep)) {
+    free_job(&j);
+    return NULL;
+  }
+  run_decode(&j);
+  free_job(&j);
+  if (j.rc != AMOD_SUCCESS) return throw_msg(env, j.err);
+  return result_object(env, &j, j.res_ab, j.pay_ab);
+}
+
+static void async_execute(napi_env env, void *data) {
+  (void)env;
+  run_decode((decode_job *)data);
+}
+
+static void async_complete(napi_env env, napi_status status, void *data) {
+  decode_job *j = (decode_job *)data;
+  napi_value res_ab, pay_ab, val;
+  napi_get_reference_value(env, j->res_ref, &res_ab);
+  napi_get_reference_value(env, j->pay_ref, &pay_ab);
+  if (status != napi_ok || j->rc != AMOD_SUCCESS) {
+    napi_value msg, err;
+    napi_create_string_utf8(env, j->rc != AMOD_SUCCESS ? j->err : "decode cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+  } else {
+    val = result_object(env, j, res_ab, pay_ab);
+    napi_resolve_deferred(env, j->deferred, val);
+  }
+  for (int i = 0; i < 3; ++i)
+    if (j->refs[i]) napi_delete_reference(env, j->refs[i]);
+  napi_delete_reference(env, j->res_ref);
+  napi_delete_reference(env, j->pay_ref);
+  napi_delete_async_work(env, j->work);
+  free_job(j);
+  free(j);
+}
+
+static napi_value js_decode_async(napi_env env, napi_callback_info info) {
+  decode_job *j = (decode_job *)malloc(sizeof *j);
+  if (!j) return throw_msg(env, "out of memory");
+  napi_value keep[3];
+  if (!prepare(env, info, j, keep)) {
+    free_job(j);
+    free(j);
+    return NULL;
+  }
+  /* keep the caller's typed arrays (samples + offsets/lengths) and the outputs alive */
+  for (int i = 0; i < 3; ++i) {
+    napi_valuetype t;
+    napi_typeof(env, keep[i], &t);
+    if (t == napi_object) napi_create_reference(env, keep[i], 1, &j->refs[i]);
+  }
+  napi_create_reference(env, j->res_ab, 1, &j->res_ref);
+  napi_create_reference(env, j->pay_ab, 1, &j->pay_ref);
+  napi_value promise, name;
+  NAPI_TRY(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_TRY(env, napi_create_string_utf8(env, "amodem.decode", NAPI_AUTO_LENGTH, &name));
+  NAPI_TRY(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
+  NAPI_TRY(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+/* ------------------------------------------------------------ host utilities */
+static napi_value make_f32(napi_env env, int64_t n, float **data) {
+  napi_value ab, ta;
+  void *p;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)(n > 0 ? n : 0) * sizeof(float), &p, &ab));
+  NAPI_TRY(env, napi_create_typedarray(env, napi_float32_array, (size_t)(n > 0 ? n : 0), ab, 0, &ta));
+  *data = (float *)p;
+  return ta;
+}
+
+static int get_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
+  size_t argc = want;
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < want) {
+    napi_throw_type_error(env, NULL, "wrong number of arguments");
+    return 0;
+  }
+  return 1;
+}
+
+static int get_u8(napi_env env, napi_value v, const uint8_t **p, int32_t *n) {
+  void *d;
+  size_t len;
+  if (!typed(env, v, napi_uint8_array, &d, &len) || len > INT32_MAX) {
+    napi_throw_type_error(env, NULL, "expected a Uint8Array");
+    return 0;
+  }
+  *p = (const uint8_t *)d;
+  *n = (int32_t)len;
+  return 1;
+}
+
+static napi_value js_crc32(napi_env env, napi_callback_info info) {
+  napi_value argv[1], out;
+  if (!get_args(env, info, 1, argv)) return NULL;
+  const uint8_t *p;
+  int32_t n;
+  if (!get_u8(env, argv[0], &p, &n)) return NULL;
+  NAPI_TRY(env, napi_create_uint32(env, amod_crc32(p, (size_t)n), &out));
+  return out;
+}
+
+static napi_value js_preamble1(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  amod_cfg c;
+  if (!get_args(env, info, 1, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  float *d;
+  napi_value ta = make_f32(env, c.symbol_len, &d);
+  if (!ta) return NULL;
+  if (amod_preamble1(&c, d) != AMOD_SUCCESS) return throw_msg(env, "invalid OFDM configuration");
+  return ta;
+}
+
+static napi_value js_tx_legacy(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  amod_cfg c;
+  const uint8_t *data, *name;
+  int32_t nd, nn;
+  if (!get_args(env, info, 3, argv) || !to_cfg(env, argv[0], &c) || !get_u8(env, argv[1], &data, &nd) ||
+      !get_u8(env, argv[2], &name, &nn))
+    return NULL;
+  const int64_t n = amod_tx_legacy(&c, data, nd, name, nn, NULL);
+  if (n < 0) return throw_msg(env, "invalid transmit arguments");
+  float *d;
+  napi_value ta = make_f32(env, n, &d);
+  if (ta && n) amod_tx_legacy(&c, data, nd, name, nn, d);
+  return ta;
+}
+
+static napi_value js_tx_meta(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  amod_cfg c;
+  int32_t tc, ts, cs, nn;
+  const uint8_t *name;
+  if (!get_args(env, info, 5, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  if (napi_get_value_int32(env, argv[1], &tc) != napi_ok || napi_get_value_int32(env, argv[2], &ts) != napi_ok ||
+      napi_get_value_int32(env, argv[3], &cs) != napi_ok)
+    return napi_throw_type_error(env, NULL, "totalChunks/totalFileSize/chunkSize must be numbers"), NULL;
+  if (!get_u8(env, argv[4], &name, &nn)) return NULL;
+  const int64_t n = amod_tx_meta(&c, tc, ts, cs, name, nn, NULL);
+  if (n < 0) return throw_msg(env, "invalid transmit arguments");
+  float *d;
+  napi_value ta = make_f32(env, n, &d);
+  if (ta && n) amod_tx_meta(&c, tc, ts, cs, name, nn, d);
+  return ta;
+}
+
+static napi_value js_tx_chunk(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  amod_cfg c;
+  const uint8_t *data;
+  int32_t nd, seq;
+  if (!get_args(env, info, 3, argv) || !to_cfg(env, argv[0], &c) || !get_u8(env, argv[1], &data, &nd)) return NULL;
+  if (napi_get_value_int32(env, argv[2], &seq) != napi_ok)
+    return napi_throw_type_error(env, NULL, "seqNum must be a number"), NULL;
+  const int64_t n = amod_tx_chunk(&c, data, nd, seq, NULL);
+  if (n < 0) return throw_msg(env, "invalid transmit arguments");
+  float *d;
+  napi_value ta = make_f32(env, n, &d);
+  if (ta && n) amod_tx_chunk(&c, data, nd, seq, d);
+  return ta;
+}
+
+static napi_value js_tx_test(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  amod_cfg c;
+  if (!get_args(env, info, 1, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  const int64_t n = amod_tx_test_signal(&c, NULL);
+  if (n < 0) return throw_msg(env, "invalid transmit arguments");
+  float *d;
+  napi_value ta = make_f32(env, n, &d);
+  if (ta && n) amod_tx_test_signal(&c, d);
+  return ta;
+}
+
+static napi_value js_estimate(napi_env env, napi_callback_info info) {
+  napi_value argv[2], out;
+  amod_cfg c;
+  int32_t nb;
+  if (!get_args(env, info, 2, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  if (napi_get_value_int32(env, argv[1], &nb) != napi_ok)
+    return napi_throw_type_error(env, NULL, "payloadBytes must be a number"), NULL;
+  NAPI_TRY(env, napi_create_int32(env, amod_estimate_frame_samples(&c, nb), &out));
+  return out;
+}
+
+static napi_value js_num_data_subs(napi_env env, napi_callback_info info) {
+  napi_value argv[1], out;
+  amod_cfg c;
+  if (!get_args(env, info, 1, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  NAPI_TRY(env, napi_create_int32(env, amod_num_data_subs(&c), &out));
+  return out;
+}
+
+static napi_value js_payload_stride(napi_env env, napi_callback_info info) {
+  napi_value argv[2], out;
+  amod_cfg c;
+  int64_t ml;
+  if (!get_args(env, info, 2, argv) || !to_cfg(env, argv[0], &c)) return NULL;
+  if (napi_get_value_int64(env, argv[1], &ml) != napi_ok)
+    return napi_throw_type_error(env, NULL, "maxLen must be a number"), NULL;
+  NAPI_TRY(env, napi_create_double(env, (double)amod_payload_stride(&c, ml), &out));
+  return out;
+}
+
+static napi_value js_abi(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value out;
+  NAPI_TRY(env, napi_create_int32(env, amod_abi_version(), &out));
+  return out;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  const napi_property_descriptor props[] = {
+      {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"decodeAsync", NULL, js_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"crc32", NULL, js_crc32, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"preamble1", NULL, js_preamble1, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"txLegacy", NULL, js_tx_legacy, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"txMeta", NULL, js_tx_meta, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"txChunk", NULL, js_tx_chunk, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"txTestSignal", NULL, js_tx_test, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"estimateFrameSamples", NULL, js_estimate, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"numDataSubs", NULL, js_num_data_subs, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"payloadStride", NULL, js_payload_stride, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"abiVersion", NULL, js_abi, NULL, NULL, NULL, napi_enumerable, NULL},
+  };
+  if (napi_define_properties(env, exports, sizeof props / sizeof props[0], props) != napi_ok) return NULL;
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

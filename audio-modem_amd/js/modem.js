@@ -1,0 +1,359 @@
+'use strict';
+// modem.js — the playok/audio-modem `modem.js` function surface, backed by the
+// MI355X engine (libamodem.so through the N-API addon amodem.node).
+//
+// Exports the 17 globals app.js uses (SURVEY.md §8b) with the reference's
+// names, argument meaning, return shapes and error strings, as CommonJS exports
+// and, when loaded in a page-like global scope, as globals:
+//   fft, OFDM_CONFIGS, OFDM, setOFDMConfig, Constellations,
+//   generatePreambleSymbol1, buildTransmitSignal, decodeReceivedSignal,
+//   FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame,
+//   decodeChunkFrame, estimateFrameSamples, generateSweepTone,
+//   generateTestSignal, analyzeLoopback
+// plus the additive batch entry decodeBatch (Promise, napi_async_work).
+//
+// decodeReceivedSignal (modem.js:557-654) and decodeChunkFrame (modem.js:770-803)
+// run on the GPU; the transmit builders run in the native host library. There is
+// no JavaScript fallback: if the addon cannot load, requiring this module throws.
+
+const path = require('path');
+const util = require('util');
+
+const native = require(process.env.AMODEM_NODE || path.join(__dirname, '..', 'lib', 'amodem.node'));
+
+const TD = typeof TextDecoder !== 'undefined' ? TextDecoder : util.TextDecoder;
+const TE = typeof TextEncoder !== 'undefined' ? TextEncoder : util.TextEncoder;
+
+// ------------------------------------------------------------------ config --
+// Presets (modem.js:69-85)
+const OFDM_CONFIGS = {
+  standard: {
+    FFT_SIZE: 512, CP_LEN: 64, SYMBOL_LEN: 576, SAMPLE_RATE: 44100, SUB_START: 12, SUB_END: 232,
+    PILOTS: [15, 29, 43, 57, 71, 85, 99, 113, 127, 141, 155, 169, 183, 197, 211, 225],
+  },
+  acoustic: {
+    FFT_SIZE: 512, CP_LEN: 128, SYMBOL_LEN: 640, SAMPLE_RATE: 44100, SUB_START: 23, SUB_END: 93,
+    PILOTS: [25, 35, 45, 55, 65, 75, 85],
+  },
+  narrowband: {
+    FFT_SIZE: 512, CP_LEN: 256, SYMBOL_LEN: 768, SAMPLE_RATE: 44100, SUB_START: 35, SUB_END: 58,
+    PILOTS: [37, 45, 53],
+  },
+};
+
+// The mutable current configuration (modem.js:87-93): a copy of a preset plus helpers.
+const OFDM = Object.assign({}, OFDM_CONFIGS.standard);
+OFDM.isPilot = (k) => OFDM.PILOTS.includes(k);
+OFDM.numDataSubs = () => {
+  let n = 0;
+  for (let k = OFDM.SUB_START; k <= OFDM.SUB_END; k++) if (!OFDM.isPilot(k)) n++;
+  return n;
+};
+
+// setOFDMConfig: unknown names select 'standard' (modem.js:95-98)
+function setOFDMConfig(name) {
+  const preset = Object.prototype.hasOwnProperty.call(OFDM_CONFIGS, name) ? OFDM_CONFIGS[name] : OFDM_CONFIGS.standard;
+  for (const key of Object.keys(preset)) OFDM[key] = preset[key];
+}
+
+const FRAME_META = 0xFE;
+const FRAME_DATA = 0xFF;
+
+// ----------------------------------------------------------- constellation --
+// Constellations + lazily filled points (modem.js:101-131). 16-QAM: Gray per
+// axis, unit average energy.
+const Constellations = {
+  BPSK: { bps: 1, points: null },
+  QPSK: { bps: 2, points: null },
+  QAM16: { bps: 4, points: null },
+};
+const MOD_ID = { BPSK: 0, QPSK: 1, QAM16: 2 };
+
+function fillPoints(name) {
+  const c = Constellations[name];
+  if (c.points) return c;
+  if (name === 'BPSK') {
+    c.points = [[1, 0], [-1, 0]];
+  } else if (name === 'QPSK') {
+    const a = 1 / Math.SQRT2;
+    c.points = [[a, a], [-a, a], [-a, -a], [a, -a]];
+  } else {
+    const gray = (v) => v ^ (v >> 1);
+    const pts = [];
+    let energy = 0;
+    for (let idx = 0; idx < 16; idx++) {
+      const x = 2 * gray(idx & 3) - 3, y = 2 * gray(idx >> 2) - 3;
+      pts.push([x, y]);
+      energy += x * x + y * y;
+    }
+    const scale = 1 / Math.sqrt(energy / 16);
+    c.points = pts.map(([x, y]) => [x * scale, y * scale]);
+  }
+  return c;
+}
+
+function modulationId(modName) {
+  if (!Object.prototype.hasOwnProperty.call(MOD_ID, modName)) {
+    // the reference dereferences Constellations[modName].points (modem.js:108-109)
+    throw new TypeError("Cannot read property 'points' of undefined");
+  }
+  fillPoints(modName);
+  return MOD_ID[modName];
+}
+
+// amod_cfg for the native side, from the current OFDM state
+function nativeCfg(modName, repetition, checkMod) {
+  return {
+    fft_size: OFDM.FFT_SIZE, cp_len: OFDM.CP_LEN, symbol_len: OFDM.SYMBOL_LEN, sample_rate: OFDM.SAMPLE_RATE,
+    sub_start: OFDM.SUB_START, sub_end: OFDM.SUB_END, pilots: OFDM.PILOTS.slice(),
+    modulation: checkMod === false ? 1 : modulationId(modName),
+    repetition: Math.max(1, (repetition || 1) | 0),
+  };
+}
+
+// --------------------------------------------------------------------- FFT --
+// fft(re, im) -> [Float64Array re, Float64Array im] (modem.js:6-13): radix-2
+// decimation in time after a bit-reversal permutation; each stage's twiddles
+// come from the same complex recurrence w <- w * wn, tabulated once per size, so
+// the rounding equals the reference's.
+const twiddleCache = new Map();
+function stageTwiddles(n) {
+  let t = twiddleCache.get(n);
+  if (t) return t;
+  t = [];
+  for (let size = 2; size <= n; size <<= 1) {
+    const half = size >> 1;
+    const ang = -2 * Math.PI / size;
+    const cr = Math.cos(ang), ci = Math.sin(ang);
+    const tr = new Float64Array(half), ti = new Float64Array(half);
+    let wr = 1, wi = 0;
+    for (let j = 0; j < half; j++) {
+      tr[j] = wr; ti[j] = wi;
+      const nr = wr * cr - wi * ci;
+      wi = wr * ci + wi * cr;
+      wr = nr;
+    }
+    t.push([tr, ti]);
+  }
+  twiddleCache.set(n, t);
+  return t;
+}
+
+function fft(re, im) {
+  const n = re.length;
+  const xr = Float64Array.from(re), xi = Float64Array.from(im);
+  let lg = 0;
+  while ((1 << lg) < n) lg++;
+  for (let i = 0; i < n; i++) {
+    let r = 0;
+    for (let b = 0, v = i; b < lg; b++, v >>= 1) r = (r << 1) | (v & 1);
+    if (i < r) {
+      let s = xr[i]; xr[i] = xr[r]; xr[r] = s;
+      s = xi[i]; xi[i] = xi[r]; xi[r] = s;
+    }
+  }
+  const tw = n > 1 ? stageTwiddles(n) : [];
+  for (let st = 0, half = 1; half < n; st++, half <<= 1) {
+    const [tr, ti] = tw[st];
+    for (let base = 0; base < n; base += 2 * half) {
+      for (let j = 0; j < half; j++) {
+        const a = base + j, b = a + half;
+        const pr = tr[j] * xr[b] - ti[j] * xi[b];
+        const pi = tr[j] * xi[b] + ti[j] * xr[b];
+        xr[b] = xr[a] - pr; xi[b] = xi[a] - pi;
+        xr[a] += pr; xi[a] += pi;
+      }
+    }
+  }
+  return [xr, xi];
+}
+
+// ---------------------------------------------------------- transmit side --
+function generatePreambleSymbol1() { // modem.js:158-170
+  return native.preamble1(nativeCfg('QPSK', 1, false));
+}
+
+function estimateFrameSamples(payloadBytes, modName, repetition) { // modem.js:863-874
+  return native.estimateFrameSamples(nativeCfg(modName, repetition), payloadBytes | 0);
+}
+
+function toBytes(x) {
+  if (x instanceof Uint8Array) return x;
+  if (ArrayBuffer.isView(x)) return new Uint8Array(x.buffer, x.byteOffset, x.byteLength);
+  return Uint8Array.from(x || []);
+}
+
+// buildTransmitSignal(fileData, modName, fileName, repetition) (modem.js:498-555)
+function buildTransmitSignal(fileData, modName, fileName, repetition) {
+  const cfg = nativeCfg(modName, repetition);
+  const data = toBytes(fileData);
+  const name = new TE().encode(fileName || 'file');
+  const signal = native.txLegacy(cfg, data, name.subarray(0, Math.min(name.length, 255)));
+  const bitsPerSymbol = OFDM.numDataSubs() * Constellations[modName].bps;
+  const rawBits = (1 + Math.min(name.length, 255) + 4 + data.length + 4) * 8 * cfg.repetition;
+  const numSymbols = Math.ceil(rawBits / bitsPerSymbol);
+  return { signal, numSymbols, bitsPerSymbol, totalBits: numSymbols * bitsPerSymbol, dataLen: data.length };
+}
+
+// buildMetadataFrame / buildDataChunkFrame (modem.js:758-766) -> Float32Array
+function buildMetadataFrame(totalChunks, totalFileSize, chunkSize, fileName, modName, rep) {
+  const name = new TE().encode(fileName || 'file');
+  return native.txMeta(nativeCfg(modName, rep), totalChunks | 0, totalFileSize | 0, chunkSize | 0,
+    name.subarray(0, Math.min(name.length, 255)));
+}
+
+function buildDataChunkFrame(chunkData, seqNum, modName, rep) {
+  return native.txChunk(nativeCfg(modName, rep), toBytes(chunkData), seqNum | 0);
+}
+
+// generateTestSignal(modName, repetition) -> {signal, testData} (modem.js:914-973)
+function generateTestSignal(modName, repetition) {
+  const testData = new Uint8Array(16);
+  for (let i = 0; i < 16; i++) testData[i] = i;
+  return { signal: native.txTestSignal(nativeCfg(modName, repetition)), testData };
+}
+
+// generateSweepTone(startFreq, endFreq, duration, sampleRate) (modem.js:890-911):
+// linear chirp at 0.8 peak with 50 ms linear fades at both ends.
+function generateSweepTone(startFreq, endFreq, duration, sampleRate) {
+  const n = Math.round(duration * sampleRate);
+  const out = new Float32Array(n);
+  const fade = Math.round(0.05 * sampleRate);
+  const span = endFreq - startFreq, twoD = 2 * duration;
+  for (let i = 0; i < n; i++) {
+    const t = i / sampleRate;
+    // phase = 2*pi*(f0*t + (f1-f0)*t^2/(2d)), evaluated in the reference's operation order
+    let v = 0.8 * Math.sin(2 * Math.PI * (startFreq * t + span * t * t / twoD));
+    if (i < fade) v *= i / fade;
+    else if (i > n - fade) v *= (n - i) / fade;
+    out[i] = v;
+  }
+  return out;
+}
+
+// ----------------------------------------------------------- receive side --
+const MODE_RECEIVED = 0, MODE_CHUNK = 1;
+const ERR = {
+  1: 'Preamble not detected',
+  2: 'Preamble not detected (low correlation)',
+  3: 'Signal too short for CE',
+  4: 'No data after CE',
+  5: 'Decoded data too short',
+  6: 'Decoded data too short for header',
+  8: 'Metadata frame too short',
+  9: 'Metadata frame truncated',
+  10: 'Data chunk frame too short',
+  11: 'Data chunk truncated',
+  12: 'Frame too short for CE',
+};
+const PRE_DEMOD = new Set([1, 2, 3, 4, 12]); // outcomes decided before demodulateOFDM runs
+const E_INVALID_LEN = 7, E_UNKNOWN_TYPE = 13, E_CAPACITY = 100;
+const REC = 96; // sizeof(amod_result)
+
+function utf8(bytes) {
+  return new TD().decode(bytes);
+}
+
+// one amod_result record (+ its payload slot) -> the reference's return object
+function formatResult(view, i, payload, stride, viaLegacy) {
+  const o = i * REC;
+  const g = (k) => view.getInt32(o + 4 * k, true);
+  const status = g(0), preambleIdx = g(1), frameType = g(3), aux = g(4);
+  const slot = new Uint8Array(payload, i * stride, stride);
+  if (status === E_CAPACITY) throw new Error('frame exceeds the reserved decode workspace');
+  if (status === 0) {
+    const nameOff = g(6), nameLen = g(7), dataOff = g(8), dataLen = g(9);
+    const crc = {
+      crcValid: g(16) !== 0,
+      expectedCRC: view.getUint32(o + 56, true),
+      actualCRC: view.getUint32(o + 60, true),
+    };
+    if (frameType === FRAME_META) {
+      const r = Object.assign({
+        frameType: FRAME_META, totalChunks: g(11), totalFileSize: g(12), chunkSize: g(13),
+        fileName: utf8(slot.slice(nameOff, nameOff + nameLen)),
+      }, crc);
+      if (viaLegacy) r.preambleIdx = preambleIdx;
+      return r;
+    }
+    if (frameType === FRAME_DATA) {
+      const r = Object.assign({
+        frameType: FRAME_DATA, seqNum: g(10), data: slot.slice(dataOff, dataOff + dataLen), dataLen,
+      }, crc);
+      if (viaLegacy) r.preambleIdx = preambleIdx;
+      return r;
+    }
+    return Object.assign({
+      data: slot.slice(dataOff, dataOff + dataLen), dataLen, fileName: utf8(slot.slice(nameOff, nameOff + nameLen)),
+    }, crc, { preambleIdx, frameType: 'legacy' });
+  }
+  if (status === E_INVALID_LEN) return { error: `Invalid data length: ${aux}` };
+  if (status === E_UNKNOWN_TYPE) return { error: `Unknown frame type: 0x${aux.toString(16)}`, frameType: aux };
+  const r = { error: ERR[status] };
+  if (viaLegacy && (frameType === FRAME_META || frameType === FRAME_DATA) && status >= 8 && status <= 11) {
+    r.preambleIdx = preambleIdx;
+  }
+  return r;
+}
+
+function asFloat32(sig) {
+  return sig instanceof Float32Array ? sig : Float32Array.from(sig);
+}
+
+function decodeOne(signal, modName, repetition, mode) {
+  // an unknown modulation only throws once demodulation is reached (modem.js:365-367)
+  const known = Object.prototype.hasOwnProperty.call(MOD_ID, modName);
+  const cfg = nativeCfg(modName, repetition, known ? undefined : false);
+  const out = native.decode(asFloat32(signal), null, null, cfg, mode, 0);
+  const view = new DataView(out.results);
+  if (!known && !PRE_DEMOD.has(view.getInt32(0, true))) modulationId(modName);
+  return formatResult(view, 0, out.payload, out.stride, mode === MODE_RECEIVED);
+}
+
+// decodeReceivedSignal(signal, modName, repetition) (modem.js:557-654)
+function decodeReceivedSignal(signal, modName, repetition) {
+  return decodeOne(signal, modName, repetition, MODE_RECEIVED);
+}
+
+// decodeChunkFrame(frameSamples, modName, repetition) (modem.js:770-803)
+function decodeChunkFrame(frameSamples, modName, repetition) {
+  return decodeOne(frameSamples, modName, repetition, MODE_CHUNK);
+}
+
+// decodeBatch(samples, frameOffsets, frameLens, modName, rep, {device, mode})
+// -> Promise<result[]>: many frames of one buffer in one GPU launch (additive API).
+function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
+  const o = opts || {};
+  const mode = o.mode === 'chunk' || o.mode === MODE_CHUNK ? MODE_CHUNK : MODE_RECEIVED;
+  const cfg = nativeCfg(modName, rep);
+  const offs = frameOffsets instanceof Float64Array ? frameOffsets : Float64Array.from(frameOffsets);
+  const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
+  return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0)
+    .then((out) => {
+      const view = new DataView(out.results);
+      const res = new Array(lens.length);
+      for (let i = 0; i < lens.length; i++) res[i] = formatResult(view, i, out.payload, out.stride, mode === MODE_RECEIVED);
+      return res;
+    });
+}
+
+// analyzeLoopback(recorded, modName, repetition, testData) (modem.js:975-1082):
+// the loopback self-test's RX core (cross-correlation fallback detection, no
+// low-correlation cut-off, channel magnitude and pilot SNR) is SURVEY.md §8f row 4
+// and not yet on the GPU; calling it fails loudly rather than running a CPU copy.
+function analyzeLoopback(recorded, modName, repetition, testData) {
+  throw new Error('analyzeLoopback: GPU loopback analysis is not implemented yet (SURVEY.md §8f-4)');
+}
+
+const api = {
+  fft, OFDM_CONFIGS, OFDM, setOFDMConfig, Constellations, generatePreambleSymbol1, buildTransmitSignal,
+  decodeReceivedSignal, FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame, decodeChunkFrame,
+  estimateFrameSamples, generateSweepTone, generateTestSignal, analyzeLoopback,
+  decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native,
+};
+
+module.exports = api;
+// browser-style globals for code written against the reference's script-tag globals
+if (typeof globalThis !== 'undefined' && process.env.AMODEM_NO_GLOBALS !== '1') {
+  for (const k of Object.keys(api)) if (k !== 'native' && !(k in globalThis)) globalThis[k] = api[k];
+}

@@ -400,6 +400,17 @@ kat.detectPreamble = [];
   const x = preprocessSignal(applyPost(buildTx({ kind: 'legacy', seed: frameSeed(0), len: 1024, name: 'f.bin', mod: 'QPSK', rep: 1 }), []));
   kat.detectPreamble.push({ label: 'std_qpsk_1k', config: 'standard', coarseIdx: detectPreamble(x) });
 }
+kat.sweepTone = [[500, 8000, 0.2, 44100], [1000, 1000, 0.05, 48000], [200, 12000, 0.5, 44100]].map(([a, b, d, sr]) => {
+  const x = generateSweepTone(a, b, d, sr);
+  return { args: [a, b, d, sr], n: x.length, sha: sha(x), head: arr(x.subarray(0, 64)), tail: arr(x.subarray(Math.max(0, x.length - 64))) };
+});
+kat.txInfo = [];
+for (const [cfg, mod, rep, len, name] of [['standard', 'QPSK', 1, 1024, 'f.bin'], ['acoustic', 'BPSK', 3, 256, 'x'], ['standard', 'QAM16', 1, 100, ''], ['narrowband', 'BPSK', 1, 40, 'nb']]) {
+  setOFDMConfig(cfg);
+  const r = buildTransmitSignal(payloadBytes(frameSeed(7), len), mod, name, rep);
+  kat.txInfo.push({ config: cfg, mod, rep, len, name, n: r.signal.length, sha: sha(r.signal), numSymbols: r.numSymbols, bitsPerSymbol: r.bitsPerSymbol, totalBits: r.totalBits, dataLen: r.dataLen });
+}
+setOFDMConfig('standard');
 kat.payloadXs32 = { seed: frameSeed(0), hex16: hex(payloadBytes(frameSeed(0), 16)) };
 
 const meta = {

@@ -1,0 +1,60 @@
+'use strict';
+// Test driver for the JS surface (audio-modem_amd/js/modem.js). Reads a job file
+// (JSON list of operations; float32 inputs as raw little-endian files) and
+// prints one JSON object of results. Uint8Array values are emitted as {hex}.
+const fs = require('fs');
+const path = require('path');
+process.env.AMODEM_NO_GLOBALS = '1';
+const M = require(path.join(__dirname, '..', '..', 'audio-modem_amd', 'js', 'modem.js'));
+
+const sha = (ta) => require('crypto').createHash('sha256').update(Buffer.from(ta.buffer, ta.byteOffset, ta.byteLength)).digest('hex');
+const enc = (v) => {
+  if (v instanceof Uint8Array) return { hex: Buffer.from(v.buffer, v.byteOffset, v.byteLength).toString('hex') };
+  if (ArrayBuffer.isView(v)) return { sha: sha(v), n: v.length };
+  if (Array.isArray(v)) return v.map(enc);
+  if (v && typeof v === 'object') {
+    const o = {};
+    for (const k of Object.keys(v)) o[k] = enc(v[k]);
+    return o;
+  }
+  if (typeof v === 'number' && !Number.isFinite(v)) return { num: String(v) };
+  return v;
+};
+const f32 = (file) => {
+  const b = fs.readFileSync(file);
+  return new Float32Array(b.buffer.slice(b.byteOffset, b.byteOffset + b.byteLength));
+};
+
+async function main() {
+  const jobs = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+  const out = {};
+  for (const j of jobs) {
+    try {
+      if (j.config) M.setOFDMConfig(j.config);
+      let r;
+      switch (j.op) {
+        case 'exports': r = Object.keys(M).sort(); break;
+        case 'fft': r = M.fft(j.re, j.im).map((a) => Array.from(a)); break;
+        case 'crc32': r = M.crc32(Buffer.from(j.hex, 'hex')); break;
+        case 'estimate': r = M.estimateFrameSamples(j.payload, j.mod, j.rep); break;
+        case 'preamble1': r = M.generatePreambleSymbol1(); break;
+        case 'sweep': r = M.generateSweepTone(...j.args); break;
+        case 'tx_legacy': r = M.buildTransmitSignal(Buffer.from(j.hex, 'hex'), j.mod, j.name, j.rep); break;
+        case 'tx_meta': r = M.buildMetadataFrame(j.chunks, j.size, j.chunkSize, j.name, j.mod, j.rep); break;
+        case 'tx_chunk': r = M.buildDataChunkFrame(Buffer.from(j.hex, 'hex'), j.seq, j.mod, j.rep); break;
+        case 'tx_test': r = M.generateTestSignal(j.mod, j.rep); break;
+        case 'constellations': M.estimateFrameSamples(1, j.mod, 1); r = M.Constellations[j.mod]; break;
+        case 'ofdm': r = { cfg: Object.assign({}, M.OFDM, { isPilot: undefined, numDataSubs: undefined }), nds: M.OFDM.numDataSubs() }; break;
+        case 'decode': r = M.decodeReceivedSignal(f32(j.file), j.mod, j.rep); break;
+        case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
+        case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { mode: j.mode }); break;
+        default: throw new Error('unknown op ' + j.op);
+      }
+      out[j.id] = { ok: enc(r) };
+    } catch (e) {
+      out[j.id] = { throw: e.constructor.name, message: e.message };
+    }
+  }
+  process.stdout.write(JSON.stringify(out));
+}
+main().catch((e) => { console.error(e); process.exit(1); });

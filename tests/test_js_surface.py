@@ -1,0 +1,181 @@
+"""The JavaScript surface (audio-modem_amd/js/modem.js over the N-API addon) against
+the reference's golden vectors: same names, return shapes, values and error strings
+as modem.js. CPU tests cover the host-side functions (no GPU call); the `gpu`
+tests decode the golden frames through decodeReceivedSignal / decodeChunkFrame /
+decodeBatch and compare with the reference's result objects."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import ROOT, frames, kat, sha
+
+NODE = shutil.which("node")
+DRIVER = os.path.join(ROOT, "tests", "js", "surface_driver.js")
+ADDON = os.path.join(ROOT, "audio-modem_amd", "lib", "amodem.node")
+pytestmark = pytest.mark.skipif(NODE is None or not os.path.exists(ADDON), reason="node or amodem.node missing")
+
+GLOBALS = ["fft", "OFDM_CONFIGS", "OFDM", "setOFDMConfig", "Constellations", "generatePreambleSymbol1",
+           "buildTransmitSignal", "decodeReceivedSignal", "FRAME_META", "FRAME_DATA", "buildMetadataFrame",
+           "buildDataChunkFrame", "decodeChunkFrame", "estimateFrameSamples", "generateSweepTone",
+           "generateTestSignal", "analyzeLoopback"]
+
+
+def run(jobs, tmp_path, timeout=600):
+    for i, j in enumerate(jobs):
+        j.setdefault("id", str(i))
+    p = tmp_path / "jobs.json"
+    p.write_text(json.dumps(jobs))
+    out = subprocess.run([NODE, DRIVER, str(p)], capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout)
+
+
+def ok(res, key):
+    r = res[key]
+    assert "ok" in r, r
+    return r["ok"]
+
+
+def test_exports(tmp_path):
+    names = ok(run([{"op": "exports", "id": "e"}], tmp_path), "e")
+    for g in GLOBALS + ["decodeBatch"]:
+        assert g in names, g
+
+
+def test_fft_bit_exact(tmp_path):
+    vecs = kat()["fft"]
+    res = run([{"op": "fft", "re": v["inRe"], "im": v["inIm"], "id": v["label"]} for v in vecs], tmp_path)
+    for v in vecs:
+        re, im = ok(res, v["label"])
+        assert re == v["fftRe"] and im == v["fftIm"], v["label"]
+
+
+def test_crc32(tmp_path):
+    vecs = kat()["crc32"]
+    res = run([{"op": "crc32", "hex": v["hex"], "id": v["label"]} for v in vecs], tmp_path)
+    for v in vecs:
+        assert ok(res, v["label"]) == v["crc"]
+
+
+def test_estimate_frame_samples_and_config(tmp_path):
+    jobs = []
+    for cfg, c in kat()["configs"].items():
+        jobs.append({"op": "ofdm", "config": cfg, "id": f"ofdm_{cfg}"})
+        jobs.append({"op": "preamble1", "config": cfg, "id": f"pre1_{cfg}"})
+        for i, e in enumerate(c["estimateFrameSamples"]):
+            jobs.append({"op": "estimate", "config": cfg, "payload": e["payload"], "mod": e["mod"], "rep": e["rep"],
+                         "id": f"{cfg}_{i}"})
+    jobs.append({"op": "ofdm", "config": "no-such-config", "id": "fallback"})
+    res = run(jobs, tmp_path)
+    for cfg, c in kat()["configs"].items():
+        o = ok(res, f"ofdm_{cfg}")
+        for k in ("FFT_SIZE", "CP_LEN", "SYMBOL_LEN", "SAMPLE_RATE", "SUB_START", "SUB_END", "PILOTS"):
+            assert o["cfg"][k] == c[k], (cfg, k)
+        assert o["nds"] == c["numDataSubs"]
+        assert ok(res, f"pre1_{cfg}")["sha"] == sha(np.asarray(c["pre1"], np.float32))
+        for i, e in enumerate(c["estimateFrameSamples"]):
+            assert ok(res, f"{cfg}_{i}") == e["samples"], (cfg, e)
+    assert ok(res, "fallback")["cfg"]["CP_LEN"] == 64  # unknown name -> standard (modem.js:96)
+
+
+def test_constellations(tmp_path):
+    jobs = [{"op": "constellations", "mod": m, "id": m} for m in ("BPSK", "QPSK", "QAM16")]
+    jobs.append({"op": "estimate", "payload": 1, "mod": "PSK8", "rep": 1, "id": "bad"})
+    res = run(jobs, tmp_path)
+    for m in ("BPSK", "QPSK", "QAM16"):
+        c = ok(res, m)
+        assert c["bps"] == kat()["constellations"][m]["bps"]
+        assert c["points"] == kat()["constellations"][m]["points"]
+    assert res["bad"]["throw"] == "TypeError"
+
+
+def test_sweep_tone(tmp_path):
+    vecs = kat()["sweepTone"]
+    res = run([{"op": "sweep", "args": v["args"], "id": str(i)} for i, v in enumerate(vecs)], tmp_path)
+    for i, v in enumerate(vecs):
+        r = ok(res, str(i))
+        assert r["n"] == v["n"] and r["sha"] == v["sha"], v["args"]
+
+
+def test_transmit_builders(tmp_path):
+    from oracle import oracle as O
+    jobs = []
+    for i, t in enumerate(kat()["txInfo"]):
+        data = O.payload(0x9E3779B9 ^ 7, t["len"]).tobytes()
+        jobs.append({"op": "tx_legacy", "config": t["config"], "hex": data.hex(), "mod": t["mod"], "rep": t["rep"],
+                     "name": t["name"], "id": f"info{i}"})
+    cases = [f for f in frames() if f["tx"]["kind"] in ("legacy", "meta", "chunk", "test")]
+    for f in cases:
+        tx = f["tx"]
+        j = {"config": f["config"], "mod": tx["mod"], "rep": tx["rep"], "id": f["name"]}
+        if tx["kind"] == "legacy":
+            j.update(op="tx_legacy", hex=O.payload(tx["seed"], tx["len"]).tobytes().hex(), name=tx["name"])
+        elif tx["kind"] == "meta":
+            j.update(op="tx_meta", chunks=tx["totalChunks"], size=tx["totalFileSize"], chunkSize=tx["chunkSize"],
+                     name=tx["name"])
+        elif tx["kind"] == "chunk":
+            j.update(op="tx_chunk", hex=O.payload(tx["seed"], tx["len"]).tobytes().hex(), seq=tx["seq"])
+        else:
+            j.update(op="tx_test")
+        jobs.append(j)
+    res = run(jobs, tmp_path)
+    for i, t in enumerate(kat()["txInfo"]):
+        r = ok(res, f"info{i}")
+        assert r["signal"]["sha"] == t["sha"] and r["signal"]["n"] == t["n"]
+        for k in ("numSymbols", "bitsPerSymbol", "totalBits", "dataLen"):
+            assert r[k] == t[k], (t, k)
+    for f in cases:
+        r = ok(res, f["name"])
+        sig = r["signal"] if f["tx"]["kind"] in ("legacy", "test") else r
+        assert sig["n"] == f["txLen"] and sig["sha"] == f["txSha"], f["name"]
+        if f["tx"]["kind"] == "test":
+            assert r["testData"] == {"hex": bytes(range(16)).hex()}
+
+
+def test_analyze_loopback_fails_loudly(tmp_path):
+    # not yet GPU-backed: it must throw, never run a CPU copy
+    p = tmp_path / "lb.js"
+    p.write_text("process.env.AMODEM_NO_GLOBALS='1';const M=require(%r);"
+                 "try{M.analyzeLoopback(new Float32Array(10),'QPSK',1,new Uint8Array(16));process.exit(3)}"
+                 "catch(e){process.exit(e instanceof Error?0:4)}" % os.path.join(ROOT, "audio-modem_amd", "js", "modem.js"))
+    assert subprocess.run([NODE, str(p)], timeout=120).returncode == 0
+
+
+# --------------------------------------------------------------- GPU decode --
+def _norm(v):
+    """golden JSON and driver output share the {hex} convention; strip nothing else"""
+    return v
+
+
+@pytest.mark.gpu
+def test_decode_golden_frames_through_js(tmp_path):
+    from oracle import oracle as O
+    jobs = []
+    for f in frames():
+        x = np.ascontiguousarray(O.build_case(f), np.float32)
+        fn = tmp_path / f"{f['name']}.f32"
+        x.tofile(fn)
+        jobs.append({"op": "decode" if f["rx"] == "legacy" else "decode_chunk", "config": f["config"],
+                     "file": str(fn), "mod": f["mod"], "rep": f["rep"], "id": f["name"]})
+    res = run(jobs, tmp_path)
+    for f in frames():
+        assert ok(res, f["name"]) == f["result"], f["name"]
+
+
+@pytest.mark.gpu
+def test_decode_batch_through_js(tmp_path):
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["mod"] == "QPSK"
+           and f["rep"] == 1]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    res = run([{"op": "decode_batch", "config": "standard", "file": str(fn), "offsets": offs,
+                "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1, "id": "b"}], tmp_path)
+    got = ok(res, "b")
+    assert got == [f["result"] for f in sel]
