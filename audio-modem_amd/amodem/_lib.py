@@ -37,7 +37,7 @@ class Result(C.Structure):
                                           "total_chunks", "total_size", "chunk_size")] + \
                [("expected_crc", C.c_uint32), ("actual_crc", C.c_uint32), ("crc_valid", C.c_int32),
                 ("nbits", C.c_int32), ("flags", C.c_int32), ("fine_metric", C.c_float),
-                ("reserved", C.c_int32 * 4)]
+                ("payload_valid", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 DBG_BAND = 256

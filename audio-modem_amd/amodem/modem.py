@@ -51,7 +51,7 @@ RESULT_DTYPE = np.dtype([(n, "<i4") for n in ("status", "preamble_idx", "coarse_
                                               "name_off", "name_len", "data_off", "data_len", "seq_num",
                                               "total_chunks", "total_size", "chunk_size")] +
                         [("expected_crc", "<u4"), ("actual_crc", "<u4"), ("crc_valid", "<i4"), ("nbits", "<i4"),
-                         ("flags", "<i4"), ("fine_metric", "<f4"), ("reserved", "<i4", (4,))])
+                         ("flags", "<i4"), ("fine_metric", "<f4"), ("payload_valid", "<i4"), ("reserved", "<i4", (3,))])
 assert RESULT_DTYPE.itemsize == 96
 
 

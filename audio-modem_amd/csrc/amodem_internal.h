@@ -174,6 +174,55 @@ __device__ inline int parse_stream(const uint32_t *v, int nbytes, int mode, amod
   return off;
 }
 
+// Byte i of the majority-voted stream (modem.js:487-495 then 468-476), read from
+// the raw MSB-first bit array; rep == 1 reads the raw stream directly.
+__device__ inline uint32_t voted_byte(const uint32_t *raw, int i, int rep) {
+  if (rep == 1) return stream_byte(raw, i);
+  const int thr = (rep + 1) >> 1;
+  uint32_t out = 0;
+  for (int b = 0; b < 8; ++b) {
+    const int j = 8 * i + b;
+    int sum = 0;
+    for (int u = 0; u < rep; ++u) {
+      const int pos = j * rep + u;
+      sum += (raw[pos >> 5] >> (31 - (pos & 31))) & 1;
+    }
+    out = (out << 1) | (uint32_t)(sum >= thr);
+  }
+  return out;
+}
+
+// How many leading bytes of the voted stream parse_stream() reads for a stream of
+// nbytes bytes, given that the first `avail` are known. The answer only ever
+// grows as more bytes become known; the parse is final once it is <= avail.
+// Reads exactly the bytes parse_stream branches on (modem.js:607-640, 793-849).
+__device__ inline int parse_need(const uint32_t *raw, int rep, int avail, int nbytes, int mode) {
+  const int min_bytes = mode == AMOD_MODE_CHUNK ? 6 : 10;
+  if (nbytes < min_bytes) return 0;
+  if (avail < 1) return 1;
+  const int t = (int)voted_byte(raw, 0, rep);
+  if (t == 0xFE) {
+    if (nbytes < 16) return 1;
+    if (avail < 12) return 12;
+    const int nl = (int)voted_byte(raw, 11, rep);
+    return 12 + nl + 4 > nbytes ? 12 : 12 + nl + 4;
+  }
+  if (t == 0xFF) {
+    if (nbytes < 11) return 1;
+    if (avail < 7) return 7;
+    const int dl = (int)((voted_byte(raw, 5, rep) << 8) | voted_byte(raw, 6, rep));
+    return 7 + dl + 4 > nbytes ? 7 : 7 + dl + 4;
+  }
+  if (mode == AMOD_MODE_CHUNK) return 1;
+  const int nl = t;
+  if (1 + nl + 8 > nbytes) return 1;
+  if (avail < 1 + nl + 4) return 1 + nl + 4;
+  int32_t dl = 0;
+  for (int q = 0; q < 4; ++q) dl = (int32_t)(((uint32_t)dl << 8) | voted_byte(raw, 1 + nl + q, rep));
+  if (dl <= 0 || (int64_t)1 + nl + 4 + dl + 4 > nbytes) return 1 + nl + 4;
+  return 1 + nl + 4 + dl + 4;
+}
+
 // Workgroup CRC-32 (modem.js:443-457) of bytes [0, L) of stream v.
 // 256 threads each hash one 16-byte chunk with slice-by-4 tables; the chunk
 // registers are moved to the end of the message with precomputed zero-byte
@@ -243,10 +292,13 @@ __device__ inline int block_vote(const uint32_t *bits, int nbits, int rep, uint3
 
 // Parse + CRC + store of one frame whose (voted) bit stream is in `v`.
 // r must already hold status = AMOD_OK and the detection fields. Whole workgroup.
+// store_bytes: how many leading payload bytes are decoded and stored (the fast
+// kernel demodulates only the symbols holding header, data and CRC bytes).
 __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg &cfg, amod_result &r_in,
                                     amod_result *out, uint8_t *slot, int64_t stride, uint32_t *red,
-                                    int *shared_status) {
+                                    int *shared_status, int store_bytes) {
   const int nbytes = nvoted >> 3;
+  store_bytes = min(store_bytes, nbytes);
   __shared__ amod_result r_sh;
   __shared__ int crc_len;
   if (threadIdx.x == 0) {
@@ -271,12 +323,18 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
     }
   }
   // payload bytes, big-endian words -> memory order
-  const int nw = (nbytes + 3) >> 2;
+  const int nw = (store_bytes + 3) >> 2;
   uint32_t *dst = reinterpret_cast<uint32_t *>(slot);
   const int cap_w = (int)(stride >> 2);
-  for (int w = ltid(); w < nw && w < cap_w; w += blockDim.x) dst[w] = __builtin_bswap32(v[w]);
+  for (int w = ltid(); w < nw && w < cap_w; w += blockDim.x) {
+    uint32_t word = v[w];
+    const int keep = store_bytes - 4 * w; // bytes of this word that were decoded
+    if (keep < 4) word &= ~(0xFFFFFFFFu >> (8 * keep));
+    dst[w] = __builtin_bswap32(word);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
+    r_sh.payload_valid = store_bytes;
     *out = r_sh;
     if (shared_status) *shared_status = r_sh.status;
   }
@@ -287,7 +345,7 @@ __device__ inline void init_result(amod_result &r) {
   r.nbytes = 0; r.name_off = 0; r.name_len = 0; r.data_off = 0; r.data_len = 0;
   r.seq_num = 0; r.total_chunks = 0; r.total_size = 0; r.chunk_size = 0;
   r.expected_crc = 0; r.actual_crc = 0; r.crc_valid = 0; r.nbits = 0; r.flags = 0;
-  r.fine_metric = 0.f; r.reserved[0] = r.reserved[1] = r.reserved[2] = r.reserved[3] = 0;
+  r.fine_metric = 0.f; r.payload_valid = 0; r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
 }
 
 } // namespace amod

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       wg_global_sync();
       v = voted;
     }
-    finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr);
+    finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr, nv >> 3);
     __syncthreads();
   }
 }

@@ -402,6 +402,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (nframes < 0) return fail(ctx, "nframes < 0", AMOD_ERR_ARG);
   if (nframes == 0) return AMOD_SUCCESS;
   if (payload_stride < 16 || payload_stride % 16) return fail(ctx, "payload_stride must be a positive multiple of 16", AMOD_ERR_ARG);
+  if (reinterpret_cast<uintptr_t>(samples) & 15) return fail(ctx, "samples must be 16-byte aligned", AMOD_ERR_ARG);
   HIP_TRY(hipSetDevice(ctx->device));
   amod::DevCfg d;
   int rc = get_tables(ctx, cfg, d);
@@ -654,6 +655,8 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   if (nsamples) HIP_TRY(hipMemcpyAsync(ctx->h_samples.p, samples, sizeof(float) * nsamples, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(ctx->h_off.p, offsets, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(ctx->h_len.p, lengths, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
+  // the fast kernel writes only the decoded prefix of each slot: hand back zeros past it
+  HIP_TRY(hipMemsetAsync(ctx->h_payload.p, 0, (size_t)payload_stride * (size_t)nframes, s));
   int64_t max_len = 0;
   for (int32_t i = 0; i < nframes; ++i) max_len = std::max<int64_t>(max_len, lengths[i]);
   int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p,

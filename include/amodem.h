@@ -110,7 +110,11 @@ typedef struct amod_result {
   int32_t nbits;       /* demodulated bits before vote                                  */
   int32_t flags;       /* AMOD_FLAG_*                                                   */
   float fine_metric;   /* best normalised cross-correlation                             */
-  int32_t reserved[4];
+  int32_t payload_valid; /* leading payload-slot bytes that hold decoded bytes: all nbytes
+                            (exact kernel), or the header..CRC prefix the parse reads (fast
+                            kernel: symbols past the CRC are not demodulated). Bytes past it
+                            are not written by the device path (zero from amod_decode_host) */
+  int32_t reserved[3];
 } amod_result;
 
 typedef struct amod_ctx amod_ctx;
@@ -134,7 +138,7 @@ int amod_reserve(amod_ctx *ctx, const amod_cfg *cfg, int32_t nframes, int64_t ma
 
 /* ---- decode ----
  * Frames are slices [offsets[i], offsets[i]+lengths[i]) of one float32 sample
- * buffer. Results go to results[i]; decoded bytes to payload + i*payload_stride.
+ * buffer (device path: the buffer must be 16-byte aligned). Results go to results[i]; decoded bytes to payload + i*payload_stride.
  * amod_decode_device: every pointer is device memory; enqueued on `stream`
  * (hipStream_t, NULL = the context's stream); returns without synchronising.
  * amod_decode_host: host pointers; copies over PCIe and synchronises.
