@@ -49,7 +49,7 @@ struct alignas(16) Smem {
       float sx[MAXNB];                       // sum u u'     -> Z_b = sum y[k] y[k+256]
       int16_t cand[SC_MAXCAND];
     } mom;
-    struct { float tmpl[768]; float m[FINE_MAX]; float yw[FINE_MAX + 776]; } fine; // stage 2
+    struct { float tmpl[768]; float m[FINE_MAX + 8]; float yw[FINE_MAX + 800]; } fine; // stage 2
     struct {                                 // stages 3-4
       float2 xch[NWAVE][512];                // per-wave FFT exchange buffer; voted bits at finish
       float2 tw1[8 * 64];
@@ -162,6 +162,15 @@ __device__ __forceinline__ int decide(int mod, float cr, float ci, float &margin
   return 4 * row + col;
 }
 
+// sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
+__device__ __forceinline__ float dpp_sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
 __device__ __forceinline__ int frame_route(const DevWork &w, int N) {
   if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
   if (N > CAP) return AMOD_FLAG_BIG;
@@ -215,7 +224,8 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
   __shared__ Smem sm;
   FRESH_ARGS;
   const int f = blockIdx.x;
-  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
+  const int tid = ltid(), lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform (SGPR)
   const int64_t off = w.off[f];
   const int N = w.len[f];
   const int ph = (int)(off & 3);
@@ -257,23 +267,22 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
     const int bz_edge = max(0, (K - 256) >> 5); // blocks >= this have pairs past the frame end
     {
       FRESH_ARGS;
-      const float *const base = X - ph;       // 16-byte aligned
-      const int nvec = (K + 3) >> 2;
-      const float c0 = N > 0 ? X[0] : 0.f;
+      // Vector pass over the float4s wholly inside the frame's k-range (k < kfull);
+      // the <= 3 samples of a trailing partial float4 are added by thread 0 below.
+      // A lane past the last full float4 reloads it (masked below), so no load sits
+      // under a branch.
+      const float4 *const b4 = reinterpret_cast<const float4 *>(X - ph); // 16-byte aligned
+      const int nfull = K >> 2, kfull = 4 * nfull;
+      const float c0 = X[0];
       const int q0 = (wave * nch) / NWAVE, q1 = ((wave + 1) * nch) / NWAVE;
       double sacc = 0.0;
       float mn = INFINITY, mxv = -INFINITY;
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      auto ld = [&](int q) -> float4 { return (q <= q1 && q < nch) ? ld_chunk(base, q, lane, nvec, K) : z4; };
-      float4 b0 = ld(q0), b1 = ld(q0 + 1), b2 = ld(q0 + 2), b3 = ld(q0 + 3);
-      for (int q = q0; q < q1; ++q) {
-        const float4 a = b0, nb = b1;
-        b0 = b1; b1 = b2; b2 = b3;
-        b3 = ld(q + 4);
+      auto LD = [&](int q) -> float4 { return b4[min(64 * q + lane, nfull - 1)]; };
+      auto step = [&](int q, const float4 a, const float4 nb) {
         const int kq = 256 * q;
         float ua[4] = {a.x - c0, a.y - c0, a.z - c0, a.w - c0};
         const float ub[4] = {nb.x - c0, nb.y - c0, nb.z - c0, nb.w - c0};
-        if (kq >= ph && kq + 256 <= K) { // whole chunk inside the frame (wave-uniform)
+        if (kq >= ph && kq + 256 <= kfull) { // whole chunk inside the frame (wave-uniform)
           mn = fminf(mn, fminf(fminf(a.x, a.y), fminf(a.z, a.w)));
           mxv = fmaxf(mxv, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
         } else {
@@ -281,22 +290,28 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           const float av[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (k0 + j >= ph && k0 + j < K) { mn = fminf(mn, av[j]); mxv = fmaxf(mxv, av[j]); }
+            if (k0 + j >= ph && k0 + j < kfull) { mn = fminf(mn, av[j]); mxv = fmaxf(mxv, av[j]); }
             else ua[j] = 0.f;
           }
         }
-        float s1 = (ua[0] + ua[1]) + (ua[2] + ua[3]);
-        float s2 = fmaf(ua[3], ua[3], fmaf(ua[2], ua[2], fmaf(ua[1], ua[1], ua[0] * ua[0])));
-        float sx = fmaf(ua[3], ub[3], fmaf(ua[2], ub[2], fmaf(ua[1], ub[1], ua[0] * ub[0])));
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); sx += __shfl_xor(sx, o, 64);
-        }
+        const float s1 = dpp_sum8((ua[0] + ua[1]) + (ua[2] + ua[3]));
+        const float s2 = dpp_sum8(fmaf(ua[3], ua[3], fmaf(ua[2], ua[2], fmaf(ua[1], ua[1], ua[0] * ua[0]))));
+        const float sx = dpp_sum8(fmaf(ua[3], ub[3], fmaf(ua[2], ub[2], fmaf(ua[1], ub[1], ua[0] * ub[0]))));
         if ((lane & 7) == 0) {
           const int b = 8 * q + (lane >> 3);
           sm.u.mom.s1[b] = s1; sm.u.mom.s2[b] = s2; sm.u.mom.sx[b] = sx;
           sacc += (double)s1;
         }
+      };
+      // batches of 8 chunks (+ the partner chunk): 9 loads in flight, then 8 steps
+      // in straight-line code so each step waits only for its own two chunks
+      for (int qb = q0; qb < q1; qb += 8) {
+        float4 c[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) c[j] = LD(qb + j);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (qb + j < q1) step(qb + j, c[j], c[j + 1]); // partner of chunk q is chunk q + 1 (k + 256)
       }
       sacc = wave_sum(sacc);
       mn = wave_min(mn);
@@ -307,6 +322,12 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         double S = 0.0;
         float MN = INFINITY, MX = -INFINITY;
         for (int i = 0; i < NWAVE; ++i) { S += sm.rd[i]; MN = fminf(MN, sm.rf[i]); MX = fmaxf(MX, sm.rf[NWAVE + i]); }
+        for (int k = max(kfull, ph); k < K; ++k) { // trailing partial float4
+          const float x = X[k - ph], u = x - c0;
+          S += (double)u; MN = fminf(MN, x); MX = fmaxf(MX, x);
+          sm.u.mom.s1[k >> 5] += u;
+          sm.u.mom.s2[k >> 5] = fmaf(u, u, sm.u.mom.s2[k >> 5]);
+        }
         int flags = 0;
         float A = 1.f, B = 0.f, Bu = 0.f;
         double mean = 0.0, mx = 0.0;
@@ -558,38 +579,45 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       }
       // template + the normalised search window, staged once in LDS
       for (int i = tid; i < SYM; i += WG) sm.u.fine.tmpl[i] = cfg.t.pre1[i];
-      const int span = P + SYM + 8;
+      const int span = P + SYM + 16;
       for (int j = tid; j < span; j += WG) sm.u.fine.yw[j] = (w0 + j < N) ? fmaf(X[w0 + j], A, B) : 0.f;
       __syncthreads();
       const float te = cfg.te_f;
-      const int nquad = (P + 3) >> 2;
+      const int noct = (P + 7) >> 3;
       const int L8 = (SYM / 8) | 1; // odd split length spreads the 8 splits over LDS banks
       const float *yw = sm.u.fine.yw;
       const float *tm = sm.u.fine.tmpl;
-      // lane = (quad of 4 positions, one of 8 tap ranges); 4 correlations + 1 energy per tap
-      for (int task = tid; task < nquad * 8; task += WG) {
-        const int qd = task >> 3, sp = task & 7;
-        const int j0 = 4 * qd; // window offset of the quad's first position
+      // lane = (octet of 8 positions, one of 8 tap ranges): per tap one window read,
+      // one template read, 8 correlations + 1 energy; the 8 ranges of an octet are 8
+      // aligned lanes, combined by DPP
+      for (int task = tid; task < noct * 8; task += WG) {
+        const int oc = task >> 3, sp = task & 7;
+        const int j0 = 8 * oc; // window offset of the octet's first position
         const int i0 = sp * L8, i1 = (sp == 7) ? SYM : i0 + L8;
-        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, e0 = 0.f;
-        float y0 = yw[j0 + i0], y1 = yw[j0 + i0 + 1], y2 = yw[j0 + i0 + 2];
-#pragma unroll 4
+        float c[8], yv[8];
+        float e0 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c[r] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 7; ++r) yv[r] = yw[j0 + i0 + r];
+#pragma unroll 8
         for (int i = i0; i < i1; ++i) {
-          const float y3 = yw[j0 + i + 3];
+          yv[7] = yw[j0 + i + 7];
           const float t = tm[i];
-          c0 = fmaf(y0, t, c0); c1 = fmaf(y1, t, c1); c2 = fmaf(y2, t, c2); c3 = fmaf(y3, t, c3);
-          e0 = fmaf(y0, y0, e0);
-          y0 = y1; y1 = y2; y2 = y3;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) c[r] = fmaf(yv[r], t, c[r]);
+          e0 = fmaf(yv[0], yv[0], e0);
+#pragma unroll
+          for (int r = 0; r < 7; ++r) yv[r] = yv[r + 1];
         }
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          c0 += __shfl_xor(c0, o, 64); c1 += __shfl_xor(c1, o, 64);
-          c2 += __shfl_xor(c2, o, 64); c3 += __shfl_xor(c3, o, 64);
-          e0 += __shfl_xor(e0, o, 64);
-        }
-        if (sp < 4 && j0 + sp < P) {
+        for (int r = 0; r < 8; ++r) c[r] = dpp_sum8(c[r]);
+        e0 = dpp_sum8(e0);
+        if (j0 + sp < P) {
           // lane sp finishes position j0 + sp: slide the energy forward sp samples
-          const float cj = sp == 0 ? c0 : (sp == 1 ? c1 : (sp == 2 ? c2 : c3));
+          float cj = c[0];
+#pragma unroll
+          for (int r = 1; r < 8; ++r) cj = sp == r ? c[r] : cj;
           float en = e0;
           for (int j = 0; j < sp; ++j) {
             const float yo = yw[j0 + j], yn = yw[j0 + j + SYM];

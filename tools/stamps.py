@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Diagnostics: wave 0's s_memtime timeline inside k_decode_fast (AMOD_STAMPS=1).
 
-Marks: 0 entry, 1 staged+stats, 2 SC block sums, 3 SC candidates, 4 SC argmax,
-5 SC done, 6 fine done, 7 FFT tables, 8 round-0 FFT, 9 G published, 10.. end of
-FFT round r, 14 all rounds, 15 finish. Prints the median/p90 cycles between
-consecutive marks and the spread of frame start times (dispatch pattern)."""
+Marks: 0 entry, 1 stream pass + block sums, 2 SC block-start metrics, 3 SC
+candidates, 4 SC argmax, 5 SC plateau/decision, 6 fine timing, 7 FFT tables,
+14 FFT rounds done, 15 finish. Prints the median/p10/p90 cycles between
+consecutive marks (per workgroup, so it includes time shared with the other
+workgroups on the CU)."""
 import ctypes as C
 import os
 import sys
@@ -13,9 +14,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "audio-modem_amd"))
-NAMES = {0: "entry", 1: "stage_in", 2: "sc_sums", 3: "sc_cand", 4: "sc_argmax", 5: "sc_done", 6: "fine",
-         7: "fft_tables", 8: "r0_fft", 9: "r0_G", 10: "round0", 11: "round1", 12: "round2", 13: "round3",
-         14: "rounds_done", 15: "finish"}
+NAMES = {0: "entry", 1: "stream", 2: "sc_blocks", 3: "sc_cand", 4: "sc_argmax", 5: "sc_done", 6: "fine",
+         7: "fft_tables", 14: "fft_rounds", 15: "finish"}
 
 
 def main():
