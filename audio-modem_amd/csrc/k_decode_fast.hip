@@ -162,12 +162,25 @@ __device__ __forceinline__ int decide(int mod, float cr, float ci, float &margin
   return 4 * row + col;
 }
 
+// min/max of three without the NaN canonicalisation fminf/fmaxf add (a NaN sample
+// is caught through the sum instead)
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
 __device__ __forceinline__ float dpp_sum8(float v) {
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, true));
   return v;
 }
 
@@ -226,8 +239,11 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
   const int f = blockIdx.x;
   const int tid = ltid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform (SGPR)
-  const int64_t off = w.off[f];
-  const int N = w.len[f];
+  // frame geometry in SGPRs: every branch and loop bound below is wave-uniform
+  const int64_t off_l = w.off[f];
+  const int64_t off = ((int64_t)__builtin_amdgcn_readfirstlane((int)(off_l >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off_l);
+  const int N = __builtin_amdgcn_readfirstlane(w.len[f]);
   const int ph = (int)(off & 3);
   const int K = ph + N;                      // k-space end (exclusive)
   const float *const X = w.samples + off;    // frame sample i at X[i]
@@ -271,20 +287,25 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       // the <= 3 samples of a trailing partial float4 are added by thread 0 below.
       // A lane past the last full float4 reloads it (masked below), so no load sits
       // under a branch.
-      const float4 *const b4 = reinterpret_cast<const float4 *>(X - ph); // 16-byte aligned
+      // frame as a raw buffer over its whole float4s: lanes past the end read zeros
       const int nfull = K >> 2, kfull = 4 * nfull;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void *)(X - ph), (short)0, 16 * nfull, 0x00020000);
       const float c0 = X[0];
       const int q0 = (wave * nch) / NWAVE, q1 = ((wave + 1) * nch) / NWAVE;
-      double sacc = 0.0;
+      float sacc = 0.f;
       float mn = INFINITY, mxv = -INFINITY;
-      auto LD = [&](int q) -> float4 { return b4[min(64 * q + lane, nfull - 1)]; };
+      auto LD = [&](int q) -> float4 {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * q, 0);
+        return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      };
       auto step = [&](int q, const float4 a, const float4 nb) {
         const int kq = 256 * q;
         float ua[4] = {a.x - c0, a.y - c0, a.z - c0, a.w - c0};
         const float ub[4] = {nb.x - c0, nb.y - c0, nb.z - c0, nb.w - c0};
         if (kq >= ph && kq + 256 <= kfull) { // whole chunk inside the frame (wave-uniform)
-          mn = fminf(mn, fminf(fminf(a.x, a.y), fminf(a.z, a.w)));
-          mxv = fmaxf(mxv, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+          mn = min3_raw(mn, min3_raw(a.x, a.y, a.z), a.w);
+          mxv = max3_raw(mxv, max3_raw(a.x, a.y, a.z), a.w);
         } else {
           const int k0 = kq + 4 * lane;
           const float av[4] = {a.x, a.y, a.z, a.w};
@@ -297,10 +318,10 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         const float s1 = dpp_sum8((ua[0] + ua[1]) + (ua[2] + ua[3]));
         const float s2 = dpp_sum8(fmaf(ua[3], ua[3], fmaf(ua[2], ua[2], fmaf(ua[1], ua[1], ua[0] * ua[0]))));
         const float sx = dpp_sum8(fmaf(ua[3], ub[3], fmaf(ua[2], ub[2], fmaf(ua[1], ub[1], ua[0] * ub[0]))));
+        sacc += s1; // every lane of a group holds its block's sum: lane 0 of the group counts it
         if ((lane & 7) == 0) {
           const int b = 8 * q + (lane >> 3);
           sm.u.mom.s1[b] = s1; sm.u.mom.s2[b] = s2; sm.u.mom.sx[b] = sx;
-          sacc += (double)s1;
         }
       };
       // batches of 8 chunks (+ the partner chunk): 9 loads in flight, then 8 steps
@@ -308,15 +329,19 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       for (int qb = q0; qb < q1; qb += 8) {
         float4 c[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) c[j] = LD(qb + j);
+        for (int j = 0; j < 9; ++j) {
+          c[j] = LD(qb + j);
+          __builtin_amdgcn_sched_barrier(0); // keep the loads in chunk order (vmcnt is in-order)
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (qb + j < q1) step(qb + j, c[j], c[j + 1]); // partner of chunk q is chunk q + 1 (k + 256)
       }
-      sacc = wave_sum(sacc);
+      double sacc_d = (lane & 7) == 0 ? (double)sacc : 0.0;
+      sacc_d = wave_sum(sacc_d);
       mn = wave_min(mn);
       mxv = wave_max(mxv);
-      if (lane == 0) { sm.rd[wave] = sacc; sm.rf[wave] = mn; sm.rf[NWAVE + wave] = mxv; }
+      if (lane == 0) { sm.rd[wave] = sacc_d; sm.rf[wave] = mn; sm.rf[NWAVE + wave] = mxv; }
       __syncthreads();
       if (tid == 0) {
         double S = 0.0;
@@ -762,7 +787,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
             const float r2 = s2 >= 0 ? X[pos2 + i] : 0.f;
             ne1 |= r1 != f1;
             ne2 |= r2 != f2;
-            nf |= !isfinite(r1) || !isfinite(r2);
+            if (cfg.mode == AMOD_MODE_CHUNK) nf |= !isfinite(r1) || !isfinite(r2); // received: stage 0 saw them
             v[m] = make_float2(fmaf(r1, A, B), s2 >= 0 ? fmaf(r2, A, B) : 0.f);
           }
           const1 = __ballot(ne1) == 0;
@@ -844,28 +869,39 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           for (int o = 32; o > 0; o >>= 1) { d1 = fmaxf(d1, __shfl_xor(d1, o, 64)); d2 = fmaxf(d2, __shfl_xor(d2, o, 64)); }
           d1 += 1e-12f; d2 += 1e-12f;
           // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
-          float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f;
-          int pc1 = 0, pc2 = 0, pflag = 0;
+          float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
+          int pflag = 0;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
             const bool pil = b < nband && sm.u.fq.band_di[b] < 0;
             const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
-            const bool ok1 = pil && a1 > 1e-6f, ok2 = pil && a2 > 1e-6f;
-            if (ok1) { ps1 += e1[rr].y / e1[rr].x; pe1 += 1.f / a1 + fabsf(e1[rr].y) / (a1 * a1); }
-            if (ok2) { ps2 += e2[rr].y / e2[rr].x; pe2 += 1.f / a2 + fabsf(e2[rr].y) / (a2 * a2); }
-            pc1 += __popcll(__ballot(ok1));
-            pc2 += __popcll(__ballot(ok2));
+            // 0/1 weights in VGPRs (no lane masks kept live across the loop)
+            const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
+            // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below
+            // signed 1/eqRe, finite for every lane (weight 0 where the reference skips)
+            const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), e1[rr].x));
+            const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), e2[rr].x));
+            const float r1 = fabsf(q1), r2 = fabsf(q2);
+            ps1 = fmaf(w1 * q1, e1[rr].y, ps1);
+            ps2 = fmaf(w2 * q2, e2[rr].y, ps2);
+            pe1 = fmaf(w1 * r1, fmaf(fabsf(e1[rr].y), r1, 1.f), pe1);
+            pe2 = fmaf(w2 * r2, fmaf(fabsf(e2[rr].y), r2, 1.f), pe2);
+            pc1 += w1;
+            pc2 += w2;
             pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
           }
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) {
             ps1 += __shfl_xor(ps1, o, 64); pe1 += __shfl_xor(pe1, o, 64);
             ps2 += __shfl_xor(ps2, o, 64); pe2 += __shfl_xor(pe2, o, 64);
+            pc1 += __shfl_xor(pc1, o, 64); pc2 += __shfl_xor(pc2, o, 64);
           }
           if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
-          const float ph1 = pc1 > 0 ? ps1 / (float)pc1 : 0.f, ph2 = pc2 > 0 ? ps2 / (float)pc2 : 0.f;
-          const float dp1 = pc1 > 0 ? d1 * pe1 / (float)pc1 : 0.f, dp2 = pc2 > 0 ? d2 * pe2 / (float)pc2 : 0.f;
+          const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
+          const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
+          const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
+          const float dp1 = d1 * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d2 * pe2 * ip2 + 1e-6f * fabsf(ph2);
           const float tau1 = 4.f * (d1 * (1.f + fabsf(ph1)) + em1 * dp1) + 1e-9f;
           const float tau2 = 4.f * (d2 * (1.f + fabsf(ph2)) + em2 * dp2) + 1e-9f;
           if (dbg && ln == 0) {
