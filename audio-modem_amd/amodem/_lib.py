@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(HERE), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libamodem.so")
+LIB_PATH = os.environ.get("AMODEM_LIB") or os.path.join(LIB_DIR, "libamodem.so")  # override: experiments only
 
 MAX_PILOTS = 32
 BPSK, QPSK, QAM16 = 0, 1, 2

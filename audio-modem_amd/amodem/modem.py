@@ -152,7 +152,7 @@ class Demodulator:
 
     # ---------------------------------------------------------------- host path
     def decode_batch(self, samples: np.ndarray, offsets, lengths, mod="QPSK", rep=1, mode=L.MODE_RECEIVED,
-                     cfg: L.Cfg | None = None, options: int = 0):
+                     cfg: L.Cfg | None = None, options: int = 0, stride: int | None = None):
         """Decode frames samples[off:off+len] (host memory, PCIe round trip).
         Returns (records: RESULT_DTYPE array, payload: uint8 [nframes, stride])."""
         samples = np.ascontiguousarray(samples, np.float32)
@@ -160,7 +160,11 @@ class Demodulator:
         lengths = np.ascontiguousarray(lengths, np.int32)
         cfg = cfg or make_cfg(mod, rep)
         n = len(offsets)
-        stride = int(self._L.amod_payload_stride(C.byref(cfg), int(lengths.max()) if n else 0))
+        need = int(self._L.amod_payload_stride(C.byref(cfg), int(lengths.max()) if n else 0))
+        if stride is None:
+            stride = need
+        elif stride < need or stride % 16:
+            raise ValueError(f"payload stride {stride} < {need} or not a multiple of 16")
         rec = np.zeros(n, RESULT_DTYPE)
         pay = np.zeros((n, stride), np.uint8)
         with self._lock:
