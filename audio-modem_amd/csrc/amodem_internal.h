@@ -46,6 +46,7 @@ struct DevCfg {
   int32_t pilots[AMOD_MAX_PILOTS];
   double te;           // sum pre1^2 in reference order (f64)
   float te_f;
+  int32_t fold;        // +-1: pre1[i + 256] = fold * pre1[i] (fast fine stage folds on it), 0: no fold
   float guard;         // fast-path guard scale (1 = default)
   int32_t stop_after;  // diagnostics only (AMOD_STOP_AFTER): fast kernel returns after this stage
   DevTables t;
@@ -69,6 +70,8 @@ struct DevWork {
   int64_t bits_stride;// words per slot
   uint32_t options;
   unsigned long long *stamps; // diagnostics (AMOD_STAMPS=1): per-frame s_memtime marks, 32 per frame
+  int32_t nb_cap;     // fast kernel: Schmidl-Cox moment blocks per frame (dynamic LDS)
+  int32_t bits_cap;   // fast kernel: raw bit words per frame (dynamic LDS)
 };
 
 // ---------------------------------------------------------------- helpers --
@@ -354,5 +357,5 @@ __device__ inline void init_result(amod_result &r) {
 extern "C" {
 hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
-int amod_fast_capacity(void); // max samples per frame of the LDS-resident kernel
+int amod_fast_lds_bytes(int nb_cap, int bits_cap); // dynamic LDS of one fast-kernel workgroup
 }

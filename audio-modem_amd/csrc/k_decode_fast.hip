@@ -28,38 +28,41 @@
 // for k_decode_exact (IEEE double, reference operation order).
 #include "amodem_internal.h"
 
+#include <algorithm>
+
 namespace amod {
 namespace {
 
 constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
-constexpr int MAXNB = 2304;                  // blocks of the moment arrays (k-space)
-constexpr int CAP = MAXNB * BLK - 64;        // max samples per frame on this path
 constexpr int FINE_MAX = 1024;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
-constexpr int BITS_WORDS = 1024;             // raw demodulated bits kept per frame (32 Ki)
 constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT round (+ CE)
+#ifndef AMOD_SB
+#define AMOD_SB 8
+#endif
+constexpr int SB = AMOD_SB;                  // stream pass: chunks per load batch
+#ifndef AMOD_WPE
+#define AMOD_WPE 5                           // waves per SIMD the register budget is sized for
+#endif
 
-struct alignas(16) Smem {
-  union alignas(16) U {
-    struct {                                 // stages 0-1
-      float s1[MAXNB];                       // sum u        -> later: block caps
-      float s2[MAXNB];                       // sum u^2      -> E_b = sum y^2
-      float sx[MAXNB];                       // sum u u'     -> Z_b = sum y[k] y[k+256]
-      int16_t cand[SC_MAXCAND];
-    } mom;
-    struct { float tmpl[768]; float m[FINE_MAX + 8]; float yw[FINE_MAX + 800]; } fine; // stage 2
-    struct {                                 // stages 3-4
-      float2 xch[NWAVE][512];                // per-wave FFT exchange buffer; voted bits at finish
-      float2 tw1[8 * 64];
-      float2 tw2[8 * 8];
-      float2 g[kMaxBand];                    // conj(H)/|H|^2 (or 1 for passthrough)
-      float known[kMaxBand];                 // CE symbol signs, band order
-      int16_t band_di[kMaxBand];             // data-subcarrier index, -1 for pilots
-      uint32_t bits[BITS_WORDS];             // raw demodulated bits, MSB first
-    } fq;
-  } u;
+// Dynamic LDS, sized per launch from the reserved frame length (amod_fast_lds_bytes):
+// one region reused by the stages, addressed by float / float2 / word index.
+//   stages 0-1: s1[nbc] s2[nbc] sx[nbc] (block moments -> caps / E_b / Z_b), cand[256]
+//   stage 2   : tmpl[768] m[FINE_MAX + 8] yw[FINE_MAX + 800] q[FINE_MAX + 280] (folded window)
+//   stage 3-4 : xch[4][512] float2 (FFT exchange; voted bits at finish), g[256] float2,
+//               bits[bitc] (raw demodulated bits)
+extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
+#define LDS_F (reinterpret_cast<float *>(amod_dyn))
+#define LDS_F2 (reinterpret_cast<float2 *>(amod_dyn))
+#define LDS_U (reinterpret_cast<uint32_t *>(amod_dyn))
+#define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
+constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
+constexpr int FQ_G = NWAVE * 512;             // float2 index of g
+constexpr int FQ_BITS = 2 * (FQ_G + kMaxBand); // word index of bits
+
+struct Smem {  // fixed part (static LDS)
   float rf[4 * NWAVE];
   int ri[4 * NWAVE];
   double rd[2 * NWAVE];
@@ -69,7 +72,6 @@ struct alignas(16) Smem {
   float A, B, Bu, errw, cbest, cblo, cbhi, fbest, gmax, zce;
   double mean, mx;
 };
-static_assert(sizeof(Smem) <= 163840 / 5 - 512, "five workgroups per CU");
 
 __device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 operator-(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -107,13 +109,14 @@ __device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2
 
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); X[n] is
 // left in the wave's exchange buffer (float2 index xb) at spec_idx(n).
-__device__ void fft512_wave(float2 (&v)[8], const int xb, Smem &sm) {
-  float2 *const X2 = &sm.u.fq.xch[0][0];
+__device__ void fft512_wave(float2 (&v)[8], const int xb, const float2 *__restrict__ tw1,
+                            const float2 *__restrict__ tw2) {
+  float2 *const X2 = LDS_F2;
   int l = wave_lane();
   asm volatile("" : "+v"(l)); // keep lane-derived swizzles inside the job loop
   dft8(v);
 #pragma unroll
-  for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], sm.u.fq.tw1[q * 64 + l]);
+  for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], tw1[q * 64 + l]);
   // exchange 1: row q, col l ^ (q<<3)
 #pragma unroll
   for (int q = 0; q < 8; ++q) X2[xb + q * 64 + (l ^ (q << 3))] = v[q];
@@ -124,7 +127,7 @@ __device__ void fft512_wave(float2 (&v)[8], const int xb, Smem &sm) {
   for (int l2 = 0; l2 < 8; ++l2) v[l2] = X2[r2 + l1 + 8 * (l2 ^ q2)];
   dft8(v);
 #pragma unroll
-  for (int p1 = 1; p1 < 8; ++p1) v[p1] = cmul(v[p1], sm.u.fq.tw2[p1 * 8 + l1]);
+  for (int p1 = 1; p1 < 8; ++p1) v[p1] = cmul(v[p1], tw2[p1 * 8 + l1]);
   __builtin_amdgcn_wave_barrier();
   // exchange 2: lane (l1, q) writes U[p1] at row q, col swz2(q, l1, p1)
 #pragma unroll
@@ -139,9 +142,7 @@ __device__ void fft512_wave(float2 (&v)[8], const int xb, Smem &sm) {
   for (int p2 = 0; p2 < 8; ++p2) X2[xb + spec_idx(q2 + 8 * p1 + 64 * p2)] = v[p2];
   __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ float2 spec_read(const Smem &sm, const int xb, int n) {
-  return (&sm.u.fq.xch[0][0])[xb + spec_idx(n & 511)];
-}
+__device__ __forceinline__ float2 spec_read(const int xb, int n) { return LDS_F2[xb + spec_idx(n & 511)]; }
 
 // Constellation decision (modem.js:140-150) and its distance to the nearest
 // decision boundary. Ties resolve to the lowest index like the reference loop.
@@ -186,7 +187,7 @@ __device__ __forceinline__ float dpp_sum8(float v) {
 
 __device__ __forceinline__ int frame_route(const DevWork &w, int N) {
   if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
-  if (N > CAP) return AMOD_FLAG_BIG;
+  if (8 * ((N + 3 + 255) >> 8) > w.nb_cap) return AMOD_FLAG_BIG; // moment arrays of this launch
   return 0;
 }
 
@@ -231,11 +232,12 @@ __device__ __forceinline__ const KArgs &kargs() {
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-__global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
   __shared__ Smem sm;
   FRESH_ARGS;
+  const int nbc = w.nb_cap, bitc = w.bits_cap; // dynamic LDS capacities of this launch
   const int f = blockIdx.x;
   const int tid = ltid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform (SGPR)
@@ -321,20 +323,20 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         sacc += s1; // every lane of a group holds its block's sum: lane 0 of the group counts it
         if ((lane & 7) == 0) {
           const int b = 8 * q + (lane >> 3);
-          sm.u.mom.s1[b] = s1; sm.u.mom.s2[b] = s2; sm.u.mom.sx[b] = sx;
+          LDS_F[b] = s1; LDS_F[nbc + b] = s2; LDS_F[2 * nbc + b] = sx;
         }
       };
-      // batches of 8 chunks (+ the partner chunk): 9 loads in flight, then 8 steps
+      // batches of SB chunks (+ the partner chunk): SB + 1 loads in flight, then SB steps
       // in straight-line code so each step waits only for its own two chunks
-      for (int qb = q0; qb < q1; qb += 8) {
-        float4 c[9];
+      for (int qb = q0; qb < q1; qb += SB) {
+        float4 c[SB + 1];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) {
+        for (int j = 0; j < SB + 1; ++j) {
           c[j] = LD(qb + j);
           __builtin_amdgcn_sched_barrier(0); // keep the loads in chunk order (vmcnt is in-order)
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < SB; ++j)
           if (qb + j < q1) step(qb + j, c[j], c[j + 1]); // partner of chunk q is chunk q + 1 (k + 256)
       }
       double sacc_d = (lane & 7) == 0 ? (double)sacc : 0.0;
@@ -350,8 +352,8 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         for (int k = max(kfull, ph); k < K; ++k) { // trailing partial float4
           const float x = X[k - ph], u = x - c0;
           S += (double)u; MN = fminf(MN, x); MX = fmaxf(MX, x);
-          sm.u.mom.s1[k >> 5] += u;
-          sm.u.mom.s2[k >> 5] = fmaf(u, u, sm.u.mom.s2[k >> 5]);
+          LDS_F[k >> 5] += u;
+          LDS_F[nbc + (k >> 5)] = fmaf(u, u, LDS_F[nbc + (k >> 5)]);
         }
         int flags = 0;
         float A = 1.f, B = 0.f, Bu = 0.f;
@@ -379,18 +381,18 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       const float A = sm.A, Bu = sm.Bu, AA = A * A, AB = A * Bu, BB = Bu * Bu, aAB = fabsf(AB);
       float tmax = 0.f;
       for (int b = tid; b < NB; b += WG) { // Z first: it reads s1/s2 of block b + 8
-        const float s2b = fmaxf(sm.u.mom.s2[b], 0.f);
+        const float s2b = fmaxf(LDS_F[nbc + b], 0.f);
         if (b < bz_edge && (b > 0 || ph == 0)) {
-          const float s1b = sm.u.mom.s1[b], s1p = sm.u.mom.s1[b + 8], s2p = fmaxf(sm.u.mom.s2[b + 8], 0.f);
-          sm.u.mom.sx[b] = fmaf(AA, sm.u.mom.sx[b], fmaf(AB, s1b + s1p, 32.f * BB));
+          const float s1b = LDS_F[b], s1p = LDS_F[b + 8], s2p = fmaxf(LDS_F[nbc + b + 8], 0.f);
+          LDS_F[2 * nbc + b] = fmaf(AA, LDS_F[2 * nbc + b], fmaf(AB, s1b + s1p, 32.f * BB));
           tmax = fmaxf(tmax, AA * sqrtf(s2b * s2p) + aAB * (sqrtf(32.f * s2b) + sqrtf(32.f * s2p)) + 32.f * BB);
         }
       }
       __syncthreads();
       for (int b = tid; b < NB; b += WG) {
-        const float s1b = sm.u.mom.s1[b], s2b = fmaxf(sm.u.mom.s2[b], 0.f);
+        const float s1b = LDS_F[b], s2b = fmaxf(LDS_F[nbc + b], 0.f);
         const int nv = min(BLK * b + BLK, K) - max(BLK * b, ph);
-        sm.u.mom.s2[b] = fmaf(AA, s2b, fmaf(2.f * AB, s1b, (float)nv * BB));
+        LDS_F[nbc + b] = fmaf(AA, s2b, fmaf(2.f * AB, s1b, (float)nv * BB));
         tmax = fmaxf(tmax, AA * s2b + 2.f * aAB * sqrtf(32.f * s2b) + 32.f * BB);
       }
       // blocks whose pairs leave the frame (and block 0 when the frame starts mid-float4):
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         if (i >= 0 && i + 256 < N) z = fmaf(X[i], Af, Bf) * fmaf(X[i + 256], Af, Bf);
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) z += __shfl_xor(z, o, 32);
-        if ((lane & 31) == 0) sm.u.mom.sx[b] = z;
+        if ((lane & 31) == 0) LDS_F[2 * nbc + b] = z;
       }
       tmax = wave_max(tmax);
       if (lane == 0) sm.rf[wave] = tmax;
@@ -433,8 +435,8 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       const float errw = sm.errw;
       const float A = sm.A, B = sm.B;
       const float gate_lo = 0.01f * (1.f - eps_g) - errw, gate_hi = 0.01f * (1.f + eps_g) + errw;
-      const float *const Eb = sm.u.mom.s2, *const Zb = sm.u.mom.sx;
-      float *const cap = sm.u.mom.s1;
+      const float *const Eb = LDS_F + nbc, *const Zb = LDS_F + 2 * nbc;
+      float *const cap = LDS_F;
       const int ncb = (E + ph) / BLK + 1; // blocks holding at least one position d in [0, E]
       // (a) window sums at block starts: a rigorous lower bound Lb on the best metric,
       //     and every block's cap (upper bound of the metric over its 32 positions)
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       for (int c = tid; c < ncb; c += WG) {
         if (cap[c] >= Lb - eps_c) {
           const int slot = atomicAdd(&sm.ncand, 1);
-          if (slot < SC_MAXCAND) sm.u.mom.cand[slot] = (int16_t)c;
+          if (slot < SC_MAXCAND) LDS_I16[6 * nbc + slot] = (int16_t)c;
         }
       }
       __syncthreads();
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       // given the block-sum error errw.
       auto cand_eval = [&](int cidx, float &m, float &mlo, float &mhi, int &d, float &ra, float &rb) -> bool {
         const int j = lane & 31;
-        const int c = sm.u.mom.cand[cidx];
+        const int c = LDS_I16[6 * nbc + cidx];
         float p = 0.f;
         ra = 0.f; rb = 0.f;
 #pragma unroll
@@ -603,38 +605,66 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
         goto finish_error;
       }
       // template + the normalised search window, staged once in LDS
-      for (int i = tid; i < SYM; i += WG) sm.u.fine.tmpl[i] = cfg.t.pre1[i];
+      for (int i = tid; i < SYM; i += WG) LDS_F[FINE_TM + i] = cfg.t.pre1[i];
       const int span = P + SYM + 16;
-      for (int j = tid; j < span; j += WG) sm.u.fine.yw[j] = (w0 + j < N) ? fmaf(X[w0 + j], A, B) : 0.f;
+      for (int j = tid; j < span; j += WG) LDS_F[FINE_YW + j] = (w0 + j < N) ? fmaf(X[w0 + j], A, B) : 0.f;
       __syncthreads();
       const float te = cfg.te_f;
       const int noct = (P + 7) >> 3;
-      const int L8 = (SYM / 8) | 1; // odd split length spreads the 8 splits over LDS banks
-      const float *yw = sm.u.fine.yw;
-      const float *tm = sm.u.fine.tmpl;
+      const float *yw = LDS_F + FINE_YW;
+      const float *tm = LDS_F + FINE_TM;
+      const int fold = cfg.fold;
+      if (fold) {
+        // corr(d) = sum_{i<256} t[i] (y[d+i] + fold y[d+i+256]) + sum_{i<CP} t[i] y[d+i+512]
+        // (t[i+256] = fold t[i]): 256 + CP taps instead of SYM
+        for (int j = tid; j < 8 * noct + 264; j += WG) LDS_F[FINE_Q + j] = fmaf((float)fold, yw[j + 256], yw[j]);
+        __syncthreads();
+      }
+      const float *qw = LDS_F + FINE_Q;
       // lane = (octet of 8 positions, one of 8 tap ranges): per tap one window read,
-      // one template read, 8 correlations + 1 energy; the 8 ranges of an octet are 8
-      // aligned lanes, combined by DPP
+      // one template read, 8 correlations; the energy of the octet's first position
+      // runs over its own SYM/8 range. The 8 ranges of an octet are 8 aligned lanes,
+      // combined by DPP.
       for (int task = tid; task < noct * 8; task += WG) {
         const int oc = task >> 3, sp = task & 7;
         const int j0 = 8 * oc; // window offset of the octet's first position
-        const int i0 = sp * L8, i1 = (sp == 7) ? SYM : i0 + L8;
         float c[8], yv[8];
-        float e0 = 0.f;
 #pragma unroll
         for (int r = 0; r < 8; ++r) c[r] = 0.f;
+        // correlation segments: (array, window offset, first tap, taps)
+        auto corr = [&](const float *arr, int base, int i0, int n) {
 #pragma unroll
-        for (int r = 0; r < 7; ++r) yv[r] = yw[j0 + i0 + r];
+          for (int r = 0; r < 7; ++r) yv[r] = arr[base + i0 + r];
 #pragma unroll 8
-        for (int i = i0; i < i1; ++i) {
-          yv[7] = yw[j0 + i + 7];
-          const float t = tm[i];
+          for (int i = i0; i < i0 + n; ++i) {
+            yv[7] = arr[base + i + 7];
+            const float t = tm[i];
 #pragma unroll
-          for (int r = 0; r < 8; ++r) c[r] = fmaf(yv[r], t, c[r]);
-          e0 = fmaf(yv[0], yv[0], e0);
+            for (int r = 0; r < 8; ++r) c[r] = fmaf(yv[r], t, c[r]);
 #pragma unroll
-          for (int r = 0; r < 7; ++r) yv[r] = yv[r + 1];
+            for (int r = 0; r < 7; ++r) yv[r] = yv[r + 1];
+          }
+        };
+        // tap range n split 8 ways with an odd length L (banks of the 8 splits differ)
+        auto split = [&](int n, int &i0, int &cnt) {
+          const int L = (n >> 3) | 1;
+          i0 = sp * L;
+          cnt = sp < 7 ? L : n - 7 * L;
+        };
+        int i0, cnt;
+        if (fold) {
+          split(256, i0, cnt);
+          corr(qw, j0, i0, cnt);                    // folded body
+          split(CP, i0, cnt);
+          corr(yw, j0 + 512, i0, cnt);              // tail taps at offset 512
+        } else {
+          split(SYM, i0, cnt);
+          corr(yw, j0, i0, cnt);
         }
+        float e0 = 0.f; // energy of position j0 over this lane's share of the SYM taps
+        split(SYM, i0, cnt);
+#pragma unroll 8
+        for (int i = i0; i < i0 + cnt; ++i) e0 = fmaf(yw[j0 + i], yw[j0 + i], e0);
 #pragma unroll
         for (int r = 0; r < 8; ++r) c[r] = dpp_sum8(c[r]);
         e0 = dpp_sum8(e0);
@@ -653,7 +683,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           if (den > 0.001f * (1.f + eps_g)) m = cj / den;
           else if (den > 0.001f * (1.f - eps_g)) m = cj / den + 4.f; // uncertain gate: tagged
           else m = -8.f;                                              // gated out
-          sm.u.fine.m[j0 + sp] = m;
+          LDS_F[FINE_M + j0 + sp] = m;
         }
       }
       __syncthreads();
@@ -661,7 +691,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       float b1 = -8.f;
       int i1x = 0x7fffffff;
       for (int k = tid; k < P; k += WG) {
-        float m = sm.u.fine.m[k];
+        float m = LDS_F[FINE_M + k];
         if (m > 2.f) m -= 4.f;
         if (m > b1) { b1 = m; i1x = k; }
       }
@@ -684,7 +714,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       float b2 = -8.f;
       int unc = 0;
       for (int k = tid; k < P; k += WG) {
-        float m = sm.u.fine.m[k];
+        float m = LDS_F[FINE_M + k];
         const bool tagged = m > 2.f;
         if (tagged) m -= 4.f;
         if (k != kst) b2 = fmaxf(b2, m);
@@ -737,14 +767,11 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
     const int nbytes_total = (nbits / cfg.rep) >> 3;
     const int nband = cfg.nband;
     // tables
-    for (int i = tid; i < 8 * 64; i += WG) sm.u.fq.tw1[i] = cfg.t.tw1[i];
-    for (int i = tid; i < 64; i += WG) sm.u.fq.tw2[i] = cfg.t.tw2[i];
-    for (int i = tid; i < nband; i += WG) { sm.u.fq.known[i] = cfg.t.known[i]; sm.u.fq.band_di[i] = cfg.t.band_di[i]; }
-    for (int i = tid; i < BITS_WORDS; i += WG) sm.u.fq.bits[i] = 0u;
+    for (int i = tid; i < bitc; i += WG) LDS_U[FQ_BITS + i] = 0u;
     if (tid == 0) {
       sm.gmax = 0.f; sm.zce = 0.f;
       sm.target = dbg ? M : min(M, FIRST_SYMS);
-      if (sm.target * per_sym > BITS_WORDS * 32) sm.flags |= AMOD_FLAG_BIG;
+      if (sm.target * per_sym > bitc * 32) sm.flags |= AMOD_FLAG_BIG;
     }
     __syncthreads();
     if (sm.flags) goto to_exact;
@@ -793,13 +820,13 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           const1 = __ballot(ne1) == 0;
           const2 = __ballot(ne2) == 0;
           if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
-          fft512_wave(v, xb, sm);
+          fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
           if (job == 0 && first) {
             // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
             float zmax = 0.f, gmax_local = 0.f;
             for (int b = lane; b < nband; b += 64) {
               const int k = cfg.sub_start + b;
-              const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
+              const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
               zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
             }
             zmax = wave_max(zmax);
@@ -807,9 +834,9 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
               const int k = cfg.sub_start + b;
               float2 h = make_float2(0.f, 0.f);
               if (!const1) {
-                const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
+                const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
                 const float2 y = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-                const float kn = sm.u.fq.known[b];
+                const float kn = cfg.t.known[b];
                 h = make_float2(y.x * kn, y.y * kn);
               }
               const float m2 = h.x * h.x + h.y * h.y;
@@ -818,7 +845,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
               else g = make_float2(1.f, 0.f);
               // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
               if (!const1 && m2 < 1e-6f) wflags |= AMOD_FLAG_CHANNEL;
-              sm.u.fq.g[b] = g;
+              LDS_F2[FQ_G + b] = g;
               gmax_local = fmaxf(gmax_local, fabsf(g.x) + fabsf(g.y));
               if (dbg) { D->h_re[b] = h.x; D->h_im[b] = h.y; }
             }
@@ -834,7 +861,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           int ln = lane;
           asm volatile("" : "+v"(ln)); // per-round lane (keeps debug/bit addresses out of registers)
           const bool live1 = s1 >= 0 && !const1, live2 = s2 >= 0 && !const2;
-          uint32_t *bits = sm.u.fq.bits;
+          uint32_t *bits = (LDS_U + FQ_BITS);
           float2 e1[4], e2[4];
           float zm = 0.f, em1 = 0.f, em2 = 0.f;
 #pragma unroll
@@ -843,12 +870,12 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
             e1[rr] = e2[rr] = make_float2(0.f, 0.f);
             if (b < nband) {
               const int k = cfg.sub_start + b;
-              const float2 zk = spec_read(sm, xb, k), zn = spec_read(sm, xb, kFft - k);
+              const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
               zm = fmaxf(zm, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
               // Z = x1 + i x2:  X1 = (Z[k] + conj Z[-k]) / 2,  X2 = (Z[k] - conj Z[-k]) / 2i
               const float2 x1 = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
               const float2 x2 = make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
-              const float2 g = sm.u.fq.g[b];
+              const float2 g = LDS_F2[FQ_G + b];
               e1[rr] = cmul(x1, g);
               e2[rr] = cmul(x2, g);
               em1 = fmaxf(em1, fabsf(e1[rr].x) + fabsf(e1[rr].y));
@@ -874,7 +901,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
-            const bool pil = b < nband && sm.u.fq.band_di[b] < 0;
+            const bool pil = b < nband && cfg.t.band_di[b] < 0;
             const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
             // 0/1 weights in VGPRs (no lane masks kept live across the loop)
             const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
@@ -915,7 +942,7 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
             if (b >= nband) continue;
-            const int di = sm.u.fq.band_di[b];
+            const int di = cfg.t.band_di[b];
             if (di < 0) continue;
 #pragma unroll
             for (int which = 0; which < 2; ++which) {
@@ -945,12 +972,12 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
       // how much of the voted stream the parse reads; decode more symbols if needed
       if (tid == 0) {
         const int avail = ((min(done * per_sym, nbits) / cfg.rep) >> 3);
-        need_bytes = parse_need(sm.u.fq.bits, cfg.rep, avail, nbytes_total, cfg.mode);
+        need_bytes = parse_need((LDS_U + FQ_BITS), cfg.rep, avail, nbytes_total, cfg.mode);
         int t = done;
         if (need_bytes > avail) {
           const int64_t raw = (int64_t)need_bytes * 8 * cfg.rep;
           t = (int)min<int64_t>((int64_t)M, (raw + per_sym - 1) / per_sym);
-          if ((int64_t)t * per_sym > BITS_WORDS * 32) sm.flags |= AMOD_FLAG_BIG;
+          if ((int64_t)t * per_sym > bitc * 32) sm.flags |= AMOD_FLAG_BIG;
         }
         sm.target = t;
         sm.ru[0] = (uint32_t)need_bytes;
@@ -969,13 +996,13 @@ __global__ __launch_bounds__(WG, 5) void k_decode_fast(const DevCfg cfg_arg, con
     {
       FRESH_ARGS;
       if (dbg && tid == 0) D->nsym = M;
-      const uint32_t *v = sm.u.fq.bits;
+      const uint32_t *v = (LDS_U + FQ_BITS);
       const int nv = nbits / cfg.rep;
       if (cfg.rep > 1) {
         // vote only the decoded prefix (the parse reads need_bytes bytes)
-        uint32_t *voted = reinterpret_cast<uint32_t *>(&sm.u.fq.xch[0][0]);
+        uint32_t *voted = reinterpret_cast<uint32_t *>(LDS_F2);
         const int decoded = min(done * per_sym, nbits);
-        block_vote(sm.u.fq.bits, min(decoded, need_bytes * 8 * cfg.rep), cfg.rep, voted);
+        block_vote((LDS_U + FQ_BITS), min(decoded, need_bytes * 8 * cfg.rep), cfg.rep, voted);
         __syncthreads();
         v = voted;
       }
@@ -1017,7 +1044,15 @@ to_exact:
 
 extern "C" hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s) {
   if (w.nframes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_decode_fast, dim3(w.nframes), dim3(amod::WG), 0, s, cfg, w);
+  hipLaunchKernelGGL(amod::k_decode_fast, dim3(w.nframes), dim3(amod::WG),
+                     (unsigned)amod_fast_lds_bytes(w.nb_cap, w.bits_cap), s, cfg, w);
   return hipGetLastError();
 }
-extern "C" int amod_fast_capacity(void) { return amod::CAP; }
+// dynamic LDS bytes of a launch with nb_cap moment blocks and bits_cap bit words
+extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap) {
+  using namespace amod;
+  const int mom = 12 * nb_cap + 2 * SC_MAXCAND;
+  const int fine = 4 * (FINE_Q + FINE_MAX + 280);
+  const int fq = 4 * (FQ_BITS + bits_cap);
+  return (std::max(mom, std::max(fine, fq)) + 15) & ~15;
+}

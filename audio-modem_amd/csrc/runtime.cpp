@@ -234,6 +234,7 @@ struct amod_ctx {
   DevBuf xs, bits;     // exact-kernel scratch
   int64_t xs_stride = 0, bits_stride = 0;
   int nslots = 0;
+  int64_t max_len = 0; // longest frame any reservation was sized for
   // host-path staging
   DevBuf h_samples, h_off, h_len, h_res, h_payload;
   std::mutex mu;
@@ -309,6 +310,16 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     double te = 0.0;
     for (int i = 0; i < sym; ++i) te += (double)pre1[i] * (double)pre1[i];
     d.te = te; d.te_f = (float)te;
+    // pre1 uses subcarriers of one parity, so its body repeats every 256 samples up
+    // to a sign (even: +, odd: -): pre1[i + 256] = sign * pre1[i]. The fast fine stage
+    // folds the correlation on it when the float32 template honours it to 1e-6.
+    {
+      const float sgn = (c->sub_start & 1) ? -1.f : 1.f;
+      float tmax = 0.f, dmax = 0.f;
+      for (int i = 0; i < sym; ++i) tmax = std::max(tmax, std::fabs(pre1[i]));
+      for (int i = 0; i + 256 < sym; ++i) dmax = std::max(dmax, std::fabs(pre1[i + 256] - sgn * pre1[i]));
+      d.fold = (sym - 512 <= 256 && dmax <= 1e-6f * tmax) ? (int)sgn : 0;
+    }
     std::vector<float> known(nband);
     std::vector<int16_t> band_di(nband);
     int di = 0;
@@ -389,6 +400,7 @@ int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) 
     ctx->bits_stride = bits_stride;
   }
   ctx->nslots = std::max<int>(ctx->nslots, (int)nslots);
+  ctx->max_len = std::max<int64_t>(ctx->max_len, max_len);
   return AMOD_SUCCESS;
 }
 
@@ -419,6 +431,12 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
+  { // fast-kernel LDS sized for the longest frame of this launch (host path) or reservation
+    const int64_t flen = max_len >= 0 ? max_len : ctx->max_len;
+    w.nb_cap = 8 * (int)((flen + 3 + 255) / 256) + 8;
+    const int64_t words = (flen / cfg->symbol_len) * amod_num_data_subs(cfg) * bps_of(cfg->modulation) / 32 + 2;
+    w.bits_cap = (int)std::min<int64_t>(2048, words);
+  }
   if (getenv("AMOD_STAMPS")) { // diagnostics: per-frame s_memtime marks of the fast kernel
     HIP_TRY(ctx->stamps.ensure(sizeof(unsigned long long) * 32 * (size_t)nframes));
     HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, sizeof(unsigned long long) * 32 * (size_t)nframes, s));
