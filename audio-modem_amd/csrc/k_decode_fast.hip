@@ -176,6 +176,39 @@ __device__ __forceinline__ float max3_raw(float a, float b, float c) {
   return r;
 }
 
+// Whole-wave reductions to a wave-uniform value: DPP butterflies inside each row of
+// 16 lanes (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror),
+// then the four rows combined through readlane. No LDS round trips. Whole wave active.
+#define AMOD_DPP_I(v, ctrl) __builtin_amdgcn_update_dpp(0, (v), (ctrl), 0xF, 0xF, true)
+#define AMOD_DPP_F(v, ctrl) __int_as_float(AMOD_DPP_I(__float_as_int(v), (ctrl)))
+__device__ __forceinline__ float rlane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ float wsum(float v) {
+  v += AMOD_DPP_F(v, 0xB1); v += AMOD_DPP_F(v, 0x4E); v += AMOD_DPP_F(v, 0x141); v += AMOD_DPP_F(v, 0x140);
+  return (rlane(v, 0) + rlane(v, 16)) + (rlane(v, 32) + rlane(v, 48));
+}
+__device__ __forceinline__ float wmax(float v) {
+  v = fmaxf(v, AMOD_DPP_F(v, 0xB1)); v = fmaxf(v, AMOD_DPP_F(v, 0x4E));
+  v = fmaxf(v, AMOD_DPP_F(v, 0x141)); v = fmaxf(v, AMOD_DPP_F(v, 0x140));
+  return fmaxf(fmaxf(rlane(v, 0), rlane(v, 16)), fmaxf(rlane(v, 32), rlane(v, 48)));
+}
+__device__ __forceinline__ int wmin_i(int v) {
+  v = min(v, AMOD_DPP_I(v, 0xB1)); v = min(v, AMOD_DPP_I(v, 0x4E));
+  v = min(v, AMOD_DPP_I(v, 0x141)); v = min(v, AMOD_DPP_I(v, 0x140));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ int wmax_i(int v) {
+  v = max(v, AMOD_DPP_I(v, 0xB1)); v = max(v, AMOD_DPP_I(v, 0x4E));
+  v = max(v, AMOD_DPP_I(v, 0x141)); v = max(v, AMOD_DPP_I(v, 0x140));
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ int wor_i(int v) {
+  v |= AMOD_DPP_I(v, 0xB1); v |= AMOD_DPP_I(v, 0x4E); v |= AMOD_DPP_I(v, 0x141); v |= AMOD_DPP_I(v, 0x140);
+  return (__builtin_amdgcn_readlane(v, 0) | __builtin_amdgcn_readlane(v, 16)) |
+         (__builtin_amdgcn_readlane(v, 32) | __builtin_amdgcn_readlane(v, 48));
+}
+
 // sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
 __device__ __forceinline__ float dpp_sum8(float v) {
@@ -341,8 +374,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       }
       double sacc_d = (lane & 7) == 0 ? (double)sacc : 0.0;
       sacc_d = wave_sum(sacc_d);
-      mn = wave_min(mn);
-      mxv = wave_max(mxv);
+      mn = -wmax(-mn);
+      mxv = wmax(mxv);
       if (lane == 0) { sm.rd[wave] = sacc_d; sm.rf[wave] = mn; sm.rf[NWAVE + wave] = mxv; }
       __syncthreads();
       if (tid == 0) {
@@ -409,7 +442,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         for (int o = 1; o < 32; o <<= 1) z += __shfl_xor(z, o, 32);
         if ((lane & 31) == 0) LDS_F[2 * nbc + b] = z;
       }
-      tmax = wave_max(tmax);
+      tmax = wmax(tmax);
       if (lane == 0) sm.rf[wave] = tmax;
       __syncthreads();
       if (tid == 0) {
@@ -461,7 +494,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         } else cv = INFINITY;
         cap[c] = cv;
       }
-      lmax = wave_max(lmax);
+      lmax = wmax(lmax);
       if (tid == 0) sm.ncand = 0;
       if (lane == 0) sm.rf[wave] = lmax;
       __syncthreads();
@@ -531,9 +564,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         } // a group's 32 lanes share g, so the width-32 shuffles stay inside active lanes
       }
       {
-        const float bw = wave_max(best);
-        const int iw = wave_min(best == bw ? bidx : 0x7fffffff);
-        const float lw = wave_max(blo), hw = wave_max(bhi);
+        const float bw = wmax(best);
+        const int iw = wmin_i(best == bw ? bidx : 0x7fffffff);
+        const float lw = wmax(blo), hw = wmax(bhi);
         if (lane == 0) { sm.rf[wave] = bw; sm.ri[wave] = iw; sm.rf[NWAVE + wave] = lw; sm.rf[2 * NWAVE + wave] = hw; }
         __syncthreads();
         if (tid == 0) {
@@ -566,7 +599,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           }
         }
       }
-      lo = wave_min(lo); hi = wave_max(hi); unc = wave_or(unc);
+      lo = wmin_i(lo); hi = wmax_i(hi); unc = wor_i(unc);
       if (lane == 0) { sm.ri[wave] = lo; sm.ri[NWAVE + wave] = hi; sm.ri[2 * NWAVE + wave] = unc; }
       __syncthreads();
       if (tid == 0) {
@@ -696,8 +729,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         if (m > b1) { b1 = m; i1x = k; }
       }
       {
-        const float bw = wave_max(b1);
-        const int iw = wave_min(b1 == bw ? i1x : 0x7fffffff);
+        const float bw = wmax(b1);
+        const int iw = wmin_i(b1 == bw ? i1x : 0x7fffffff);
         if (lane == 0) { sm.rf[wave] = bw; sm.ri[wave] = iw; }
         __syncthreads();
         if (tid == 0) {
@@ -720,7 +753,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         if (k != kst) b2 = fmaxf(b2, m);
         if (tagged && m >= FB - eps_f) unc = 1;
       }
-      b2 = wave_max(b2); unc = wave_or(unc);
+      b2 = wmax(b2); unc = wor_i(unc);
       if (lane == 0) { sm.rf[wave] = b2; sm.ri[wave] = unc; }
       __syncthreads();
       if (tid == 0) {
@@ -776,52 +809,73 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
     __syncthreads();
     if (sm.flags) goto to_exact;
     STAMP(7);
-    int done = 0;
+    int done = 0;                  // data symbols decoded so far (a prefix)
     int need_bytes = 0;
     int wflags = 0;
+    // Jobs are numbered over the whole frame: job 0 = (CE, symbol 0), job j = (2j-1, 2j);
+    // wave w owns jobs w, w+4, ... and prefetches its next job's samples while it
+    // transforms and demaps the current one (across the round boundary too: the
+    // first-round prefetch is speculative and simply dropped if unused).
+    auto jobs_for = [](int T) { return T == 0 ? 1 : 1 + T / 2; };
+    auto job_syms = [&](int j, int T, int &s1, int &s2) {
+      if (j == 0) { s1 = -2; s2 = T > 0 ? 0 : -1; }
+      else { s1 = 2 * j - 1; s2 = 2 * j < T ? 2 * j : -1; }
+    };
+    float pf1[8], pf2[8];
+    int pf_job = -1;
+    auto load_job = [&](int j, int T, float (&r1)[8], float (&r2)[8]) {
+      int a, b;
+      job_syms(j, T, a, b);
+      const int p1 = a == -2 ? ce0 : data0 + a * SYM, p2 = b >= 0 ? data0 + b * SYM : p1;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        r1[m] = X[p1 + CP + lane + 64 * m];
+        r2[m] = X[p2 + CP + lane + 64 * m];
+      }
+    };
+    int jdone = 0;                 // jobs completed in earlier rounds
     for (;;) {
       FRESH_ARGS;
       const int target = sm.target;
       const bool first = done == 0;
-      // jobs of this round: first round job 0 = (CE, symbol 0); then pairs of symbols
-      const int nsyms = target - done;
-      const int njobs = first ? 1 + nsyms / 2 : (nsyms + 1) / 2;
-      for (int r = 0; r * NWAVE < njobs; ++r) {
-        const int job = r * NWAVE + wave;
-        const bool active = job < njobs;
-        int s1 = -1, s2 = -1; // data-symbol indices; s1 = -2 marks the CE symbol
-        if (active) {
-          if (first) {
-            if (job == 0) { s1 = -2; s2 = nsyms > 0 ? 0 : -1; }
-            else { s1 = 2 * job - 1; s2 = 2 * job < nsyms ? 2 * job : -1; }
-          } else {
-            s1 = done + 2 * job; s2 = done + 2 * job + 1 < target ? done + 2 * job + 1 : -1;
-          }
-        }
-        const int pos1 = s1 == -2 ? ce0 : data0 + s1 * SYM;
-        const int pos2 = s2 >= 0 ? data0 + s2 * SYM : pos1;
+      const int jend = jobs_for(target);
+      // round: jobs [jdone, jend); the first round is exactly one job per wave
+      for (int j = jdone + ((wave - jdone) & (NWAVE - 1)), r = 0; (first && r == 0) || j < jend; j += NWAVE, ++r) {
+        const bool active = j < jend;
+        int s1 = -1, s2 = -1;      // data-symbol indices; s1 = -2 marks the CE symbol
+        if (active) job_syms(j, target, s1, s2);
         const int xb = wave * 512;
         float2 v[8];
         int const1 = 0, const2 = 0;
         if (active) {
+          float r1[8], r2[8];
+          if (pf_job == j) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) { r1[m] = pf1[m]; r2[m] = pf2[m]; }
+          } else {
+            load_job(j, target, r1, r2);
+          }
+          // next job of this wave: inside this round, or speculatively the next round's
+          const int jn = j + NWAVE;
+          if (jn < jend || (first && 2 * jn - 1 < M)) { load_job(jn, M, pf1, pf2); pf_job = jn; }
+          else pf_job = -1;
           // a window is constant iff every raw sample equals its first one
-          const float f1 = X[pos1 + CP], f2 = s2 >= 0 ? X[pos2 + CP] : 0.f;
+          const float f1 = rlane(r1[0], 0), f2 = rlane(r2[0], 0);
           int ne1 = 0, ne2 = 0, nf = 0;
 #pragma unroll
           for (int m = 0; m < 8; ++m) {
-            const int i = CP + lane + 64 * m;
-            const float r1 = X[pos1 + i];
-            const float r2 = s2 >= 0 ? X[pos2 + i] : 0.f;
-            ne1 |= r1 != f1;
-            ne2 |= r2 != f2;
-            if (cfg.mode == AMOD_MODE_CHUNK) nf |= !isfinite(r1) || !isfinite(r2); // received: stage 0 saw them
-            v[m] = make_float2(fmaf(r1, A, B), s2 >= 0 ? fmaf(r2, A, B) : 0.f);
+            ne1 |= r1[m] != f1;
+            ne2 |= r2[m] != f2;
+            if (cfg.mode == AMOD_MODE_CHUNK) nf |= !isfinite(r1[m]) || !isfinite(r2[m]); // received: stage 0 saw them
+            v[m] = make_float2(fmaf(r1[m], A, B), s2 >= 0 ? fmaf(r2[m], A, B) : 0.f);
           }
           const1 = __ballot(ne1) == 0;
           const2 = __ballot(ne2) == 0;
           if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
+          if (r == 0) STAMP(first ? 8 : 16);
           fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
-          if (job == 0 && first) {
+          if (r == 0) STAMP(first ? 9 : 17);
+          if (j == 0) {
             // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
             float zmax = 0.f, gmax_local = 0.f;
             for (int b = lane; b < nband; b += 64) {
@@ -829,7 +883,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
               const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
               zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
             }
-            zmax = wave_max(zmax);
+            zmax = wmax(zmax);
             for (int b = lane; b < nband; b += 64) {
               const int k = cfg.sub_start + b;
               float2 h = make_float2(0.f, 0.f);
@@ -841,7 +895,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
               }
               const float m2 = h.x * h.x + h.y * h.y;
               float2 g;
-              if (m2 > 1e-10f) g = make_float2(h.x / m2, -h.y / m2);
+              if (m2 > 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the 2e-6 eq bound
               else g = make_float2(1.f, 0.f);
               // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
               if (!const1 && m2 < 1e-6f) wflags |= AMOD_FLAG_CHANNEL;
@@ -849,11 +903,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
               gmax_local = fmaxf(gmax_local, fabsf(g.x) + fabsf(g.y));
               if (dbg) { D->h_re[b] = h.x; D->h_im[b] = h.y; }
             }
-            gmax_local = wave_max(gmax_local);
+            gmax_local = wmax(gmax_local);
             if (lane == 0) { sm.zce = zmax; sm.gmax = gmax_local; }
           }
         }
-        if (first && r == 0) __syncthreads(); // publish G, |G|max and the CE spectrum scale
+        if (first && r == 0) __syncthreads(); // publish G, |G|max and the CE spectrum scale (every wave passes r = 0)
+        if (first && r == 0) STAMP(10);
         if (!active) continue;
         const float gmax = sm.gmax, zce = sm.zce;
         // ---- both data symbols of this job in one pass: equalise, pilot phase, demap
@@ -892,8 +947,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
           const float gsc = 2e-6f * cfg.guard * gmax;
           float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) { d1 = fmaxf(d1, __shfl_xor(d1, o, 64)); d2 = fmaxf(d2, __shfl_xor(d2, o, 64)); }
+          d1 = wmax(d1); d2 = wmax(d2);
           d1 += 1e-12f; d2 += 1e-12f;
           // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
           float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
@@ -918,12 +972,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
             pc2 += w2;
             pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
           }
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            ps1 += __shfl_xor(ps1, o, 64); pe1 += __shfl_xor(pe1, o, 64);
-            ps2 += __shfl_xor(ps2, o, 64); pe2 += __shfl_xor(pe2, o, 64);
-            pc1 += __shfl_xor(pc1, o, 64); pc2 += __shfl_xor(pc2, o, 64);
-          }
+          ps1 = wsum(ps1); pe1 = wsum(pe1); ps2 = wsum(ps2); pe2 = wsum(pe2); pc1 = wsum(pc1); pc2 = wsum(pc2);
           if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
           const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
           const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
@@ -965,10 +1014,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
             }
           }
           if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
+          if (r == 0) STAMP(first ? 11 : 18);
         }
       }
       __syncthreads(); // the round's bits are complete
+      STAMP(first ? 12 : 19);
       done = target;
+      jdone = jend;
       // how much of the voted stream the parse reads; decode more symbols if needed
       if (tid == 0) {
         const int avail = ((min(done * per_sym, nbits) / cfg.rep) >> 3);
@@ -976,7 +1028,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         int t = done;
         if (need_bytes > avail) {
           const int64_t raw = (int64_t)need_bytes * 8 * cfg.rep;
-          t = (int)min<int64_t>((int64_t)M, (raw + per_sym - 1) / per_sym);
+          t = (int)min<int64_t>((int64_t)M, ((raw + per_sym - 1) / per_sym) | 1); // whole jobs
           if ((int64_t)t * per_sym > bitc * 32) sm.flags |= AMOD_FLAG_BIG;
         }
         sm.target = t;
@@ -986,7 +1038,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       if (sm.flags || sm.target <= done) break;
     }
     need_bytes = (int)sm.ru[0];
-    wflags = wave_or(wflags);
+    wflags = wor_i(wflags);
     if (lane == 0 && wflags) atomicOr(&sm.flags, wflags);
     __syncthreads();
     if (sm.flags) goto to_exact;

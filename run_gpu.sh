@@ -14,5 +14,6 @@ for s in "$@"; do
          run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE --kernel-trace --stats -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-frames -1;;
     pmcstages) run pmc_stages 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --kernel-trace -d gpurun_out/pmc_stages -o run --output-format csv -- python tools/stage_profile.py;;
     variants) for v in ${VARIANTS:-w5s8}; do run bench_$v 300 env AMODEM_LIB=audio-modem_amd/lib/variants/$v/libamodem.so python bench.py --steps 20 --warmup 3 --cpu-frames -1; done;;
+    pmcic) run pmc_ic 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/pmc_ic -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-frames -1;;
   esac
 done

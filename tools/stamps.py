@@ -15,7 +15,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "audio-modem_amd"))
 NAMES = {0: "entry", 1: "stream", 2: "sc_blocks", 3: "sc_cand", 4: "sc_argmax", 5: "sc_done", 6: "fine",
-         7: "fft_tables", 14: "fft_rounds", 15: "finish"}
+         7: "fft_tables", 8: "r1_loaded", 9: "r1_fft", 10: "r1_G", 11: "r1_band", 12: "r1_barrier",
+         16: "r2_loaded", 17: "r2_fft", 18: "r2_band", 19: "r2_barrier", 14: "fft_rounds", 15: "finish"}
 
 
 def main():
@@ -43,7 +44,8 @@ def main():
     st = np.zeros(F * 32, dtype=np.uint64)
     n = lib.amod_debug_stamps(dm.ctx, st.ctypes.data, st.size)
     st = st[:n].reshape(F, 32).astype(np.int64)
-    have = [k for k in range(32) if (st[:, k] != 0).any()]
+    order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 18, 19, 14, 15]
+    have = [k for k in order if (st[:, k] != 0).any()]
     print(f"frames {F}  marks {have}")
     prev = None
     for k in have:
