@@ -110,6 +110,8 @@ def main():
     lib.amod_kernel_times(dm.ctx, C.byref(fast_ms), C.byref(nfast), C.byref(exact_ms), C.byref(nexact))
     lib.amod_set_profiling(dm.ctx, 0)
 
+    scan = scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream)
+
     t = torch.tensor([elapsed, float(ok), float(fallback)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t[:1].clone()
@@ -161,11 +163,39 @@ def main():
                          "kernel": "k_decode_fast", "kernel_ms_avg": fast_avg_s * 1e3,
                          "exact_kernel_ms_avg": exact_ms.value / max(1, nexact.value)},
             "cpu_baseline": cpu,
+            "scan_roofline": {"phase": "stream pass + Schmidl-Cox coarse search (k_decode_fast stopped after "
+                                       "the coarse decision; diagnostic launch, results not written)",
+                              "kernel_ms_avg": scan, "achieved": algo_bytes / (scan / 1e3) / 1e9,
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": algo_bytes / (scan / 1e3) / 1e9 / HBM_PEAK_GBS},
         }
         print(json.dumps(out), flush=True)
     dm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, reps=10):
+    """Average duration of the correlation-scan phase alone: the same kernel on the same
+    resident batch, told (AMOD_STOP_AFTER=1, read when a context builds its tables) to
+    stop after the Schmidl-Cox decision."""
+    os.environ["AMOD_STOP_AFTER"] = "1"
+    try:
+        dm = amodem.Demodulator(local)
+        dm.reserve(cfg, F, SAMPLES_PER_FRAME)
+        run = lambda: dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
+                                       d_res.data_ptr(), d_pay.data_ptr(), stride, stream=stream)
+        run()
+        dm.synchronize()
+        lib.amod_set_profiling(dm.ctx, 1)
+        for _ in range(reps):
+            run()
+        fm, fn, em, en = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
+        lib.amod_kernel_times(dm.ctx, C.byref(fm), C.byref(fn), C.byref(em), C.byref(en))
+        dm.close()
+        return fm.value / max(1, fn.value)
+    finally:
+        del os.environ["AMOD_STOP_AFTER"]
 
 
 def cpu_baseline(x, offs, lens, nframes):
