@@ -209,6 +209,14 @@ __device__ __forceinline__ int wor_i(int v) {
          (__builtin_amdgcn_readlane(v, 32) | __builtin_amdgcn_readlane(v, 48));
 }
 
+// inclusive prefix sum inside each aligned 32-lane group: row_shr 1/2/4/8 inside rows of
+// 16, then row_bcast:15 carries row 0 (2) into row 1 (3). The group's lanes all active.
+__device__ __forceinline__ float scan32(float v) {
+  v += AMOD_DPP_F(v, 0x111); v += AMOD_DPP_F(v, 0x112); v += AMOD_DPP_F(v, 0x114); v += AMOD_DPP_F(v, 0x118);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  return v;
+}
+
 // sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
 __device__ __forceinline__ float dpp_sum8(float v) {
@@ -469,6 +477,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       const float A = sm.A, B = sm.B;
       const float gate_lo = 0.01f * (1.f - eps_g) - errw, gate_hi = 0.01f * (1.f + eps_g) + errw;
       const float *const Eb = LDS_F + nbc, *const Zb = LDS_F + 2 * nbc;
+      const int CMAX = 3 * nbc + SC_MAXCAND / 2;   // per-candidate max metric (after cand[])
       float *const cap = LDS_F;
       const int ncb = (E + ph) / BLK + 1; // blocks holding at least one position d in [0, E]
       // (a) window sums at block starts: a rigorous lower bound Lb on the best metric,
@@ -536,13 +545,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         const float z0 = (d >= 0 && d < N - 256) ? y0 * y1 : 0.f;
         const float z1 = (d + 256 >= 0 && d + 256 < N - 256) ? y1 * y2 : 0.f;
         const float vp = z1 - z0, va = fmaf(y1, y1, -y0 * y0), vb = fmaf(y2, y2, -y1 * y1);
-        float sp = vp, sa = va, sb = vb; // inclusive scans over the 32-lane group
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          const float tp = __shfl_up(sp, o, 32), ta = __shfl_up(sa, o, 32), tb = __shfl_up(sb, o, 32);
-          if (j >= o) { sp += tp; sa += ta; sb += tb; }
-        }
-        p += sp - vp; ra += sa - va; rb += sb - vb;
+        // exclusive prefix (inclusive scan minus own term) over the 32-lane group
+        p += scan32(vp) - vp; ra += scan32(va) - va; rb += scan32(vb) - vb;
         const bool ok = d >= 0 && d <= E && ra > gate_lo && rb > gate_lo;
         m = ok ? (p * p) / (ra * rb) : -1.f;
         const float pl = fmaxf(fabsf(p) - errw, 0.f), ph2 = fabsf(p) + errw;
@@ -556,12 +560,19 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         if (g < ncand) {
           float m, mlo, mhi, ra, rb;
           int d;
-          if (cand_eval(g, m, mlo, mhi, d, ra, rb)) {
+          const bool ok = cand_eval(g, m, mlo, mhi, d, ra, rb);
+          if (ok) {
             if (m > best || (m == best && d < bidx)) { best = m; bidx = d; }
             blo = fmaxf(blo, mlo);
             bhi = fmaxf(bhi, mhi);
           }
-        } // a group's 32 lanes share g, so the width-32 shuffles stay inside active lanes
+          // the block's highest possible metric, for pass 2's filter
+          float top = ok ? fmaxf(m, mhi) : -2.f;
+          top = fmaxf(top, AMOD_DPP_F(top, 0xB1)); top = fmaxf(top, AMOD_DPP_F(top, 0x4E));
+          top = fmaxf(top, AMOD_DPP_F(top, 0x141)); top = fmaxf(top, AMOD_DPP_F(top, 0x140));
+          top = fmaxf(top, __shfl_xor(top, 16, 32));
+          if ((lane & 31) == 0) LDS_F[CMAX + g] = top;
+        } // a group's 32 lanes share g, so its DPP/shuffles stay inside active lanes
       }
       {
         const float bw = wmax(best);
@@ -588,7 +599,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       int lo = 0x7fffffff, hi = -1, unc = 0;
       if (CBH >= 0.5f - eps_c) {
         for (int g = 2 * wave + (lane >> 5); g - (lane >> 5) < ncand; g += 2 * NWAVE) {
-          if (g < ncand) {
+          if (g < ncand && LDS_F[CMAX + g] >= CBL - eps_c) { // blocks that can reach the band
             float m, mlo, mhi, ra, rb;
             int d;
             if (cand_eval(g, m, mlo, mhi, d, ra, rb) && fmaxf(m, mhi) >= CBL - eps_c) {
@@ -1103,7 +1114,7 @@ extern "C" hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevW
 // dynamic LDS bytes of a launch with nb_cap moment blocks and bits_cap bit words
 extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap) {
   using namespace amod;
-  const int mom = 12 * nb_cap + 2 * SC_MAXCAND;
+  const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND;
   const int fine = 4 * (FINE_Q + FINE_MAX + 280);
   const int fq = 4 * (FQ_BITS + bits_cap);
   return (std::max(mom, std::max(fine, fq)) + 15) & ~15;
