@@ -60,7 +60,12 @@ extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
 constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
 constexpr int FQ_G = NWAVE * 512;             // float2 index of g
-constexpr int FQ_BITS = 2 * (FQ_G + kMaxBand); // word index of bits
+#ifndef AMOD_TW_LDS
+#define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
+#endif
+constexpr int FQ_TW = FQ_G + kMaxBand;        // float2 index of the twiddles (tw1[512], tw2[64])
+constexpr int TW_WORDS = AMOD_TW_LDS ? 2 * (8 * 64 + 8 * 8) : 0;
+constexpr int FQ_BITS = 2 * (FQ_G + kMaxBand) + TW_WORDS; // word index of bits
 
 struct Smem {  // fixed part (static LDS)
   float rf[4 * NWAVE];
@@ -812,6 +817,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
     const int nband = cfg.nband;
     // tables
     for (int i = tid; i < bitc; i += WG) LDS_U[FQ_BITS + i] = 0u;
+    if (AMOD_TW_LDS) {
+      for (int i = tid; i < 8 * 64; i += WG) LDS_F2[FQ_TW + i] = cfg.t.tw1[i];
+      for (int i = tid; i < 8 * 8; i += WG) LDS_F2[FQ_TW + 8 * 64 + i] = cfg.t.tw2[i];
+    }
+    // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
+    int di_l[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) di_l[rr] = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
     if (tid == 0) {
       sm.gmax = 0.f; sm.zce = 0.f;
       sm.target = dbg ? M : min(M, FIRST_SYMS);
@@ -884,7 +897,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           const2 = __ballot(ne2) == 0;
           if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
           if (r == 0) STAMP(first ? 8 : 16);
-          fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
+          if (AMOD_TW_LDS) fft512_wave(v, xb, LDS_F2 + FQ_TW, LDS_F2 + FQ_TW + 8 * 64);
+          else fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
           if (r == 0) STAMP(first ? 9 : 17);
           if (j == 0) {
             // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
@@ -966,7 +980,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
-            const bool pil = b < nband && cfg.t.band_di[b] < 0;
+            const bool pil = di_l[rr] == -1;
             const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
             // 0/1 weights in VGPRs (no lane masks kept live across the loop)
             const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
@@ -1002,7 +1016,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
             if (b >= nband) continue;
-            const int di = cfg.t.band_di[b];
+            const int di = di_l[rr];
             if (di < 0) continue;
 #pragma unroll
             for (int which = 0; which < 2; ++which) {
