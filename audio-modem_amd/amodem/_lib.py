@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("AMODEM_LIB") or os.path.join(LIB_DIR, "libamodem.so")
 MAX_PILOTS = 32
 BPSK, QPSK, QAM16 = 0, 1, 2
 MODS = {"BPSK": BPSK, "QPSK": QPSK, "QAM16": QAM16}
-MODE_RECEIVED, MODE_CHUNK = 0, 1
+MODE_RECEIVED, MODE_CHUNK, MODE_LOOPBACK = 0, 1, 2
 OPT_FORCE_EXACT = 1
 
 OK = 0
@@ -79,6 +79,7 @@ SIGNATURES = {
     "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,
                                            C.c_int64, C.c_uint32, _P, _P]),
     "amod_debug_stamps": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_analyze_loopback": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, _P, C.c_int64]),
     "amod_crc32": (C.c_uint32, [C.c_char_p, C.c_size_t]),
     "amod_preamble1": (C.c_int, [C.POINTER(Cfg), _P]),
     "amod_tx_legacy": (C.c_int64, [C.POINTER(Cfg), C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, _P]),

@@ -70,6 +70,56 @@ __device__ __forceinline__ double js_max(double a, double b) { // Math.max, NaN-
   return b > a ? b : a;
 }
 
+// detectPreambleCrossCorr (modem.js:235-284) on the preprocessed samples xs: a strided
+// coarse search then a +-step fine search, each offset's sums sequential in fp64 on one
+// lane; first strict maximum like the reference loops. Whole workgroup; returns the index
+// or -1.
+__device__ int crosscorr_detect(const float *xs, int N, const DevCfg &cfg, XSmem &sm) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pLen = cfg.sym;
+  if (N < pLen || cfg.te < 1e-10) return -1;
+  const int end = N - pLen;
+  const int step = max(1, pLen / 10);
+  int best_idx = -1;
+  double best = 0.0;
+  auto scan = [&](int d0, int d1, int dstep, double &b, int &bi) {
+    double bm = b;
+    int bx = 0x7fffffff;
+    for (int d = d0 + tid * dstep; d <= d1; d += XT * dstep) {
+      double corr = 0.0, se = 0.0;
+      for (int i = 0; i < pLen; ++i) {
+        const double sv = xs[d + i];
+        corr += sv * (double)cfg.t.pre1[i];
+        se += sv * sv;
+      }
+      const double den = sqrt(se * cfg.te);
+      if (den > 0.001) {
+        const double m = corr / den;
+        if (m > bm) { bm = m; bx = d; }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double om = __shfl_xor(bm, o, 64);
+      const int oi = __shfl_xor(bx, o, 64);
+      if (om > bm || (om == bm && oi < bx)) { bm = om; bx = oi; }
+    }
+    __syncthreads();
+    if (lane == 0) { sm.rd[wave] = bm; sm.ri[wave] = bx; }
+    __syncthreads();
+    double B = sm.rd[0];
+    int I = sm.ri[0];
+    for (int i = 1; i < XT / 64; ++i)
+      if (sm.rd[i] > B || (sm.rd[i] == B && sm.ri[i] < I)) { B = sm.rd[i]; I = sm.ri[i]; }
+    if (I != 0x7fffffff) { b = B; bi = I; } // some offset beat the running best
+  };
+  scan(0, end, step, best, best_idx);
+  if (best_idx < 0 || best < 0.15) return -1;
+  const int f0 = max(0, best_idx - step), f1 = min(end, best_idx + step);
+  best = 0.0;
+  scan(f0, f1, 1, best, best_idx);
+  return best > 0.15 ? best_idx : -1;
+}
+
 __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const DevWork w) {
   __shared__ XSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -98,7 +148,8 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     int start = 0;
     const float *sig = xr; // samples the demodulator reads
 
-    if (cfg.mode == AMOD_MODE_RECEIVED) {
+    const bool loop = cfg.mode == AMOD_MODE_LOOPBACK; // analyzeLoopback's receive core
+    if (cfg.mode != AMOD_MODE_CHUNK) {
       // ---- preprocessSignal: sequential mean, then |f32(x - mean)| max, then scale
       double sum = 0.0;
       for (int c0 = 0; c0 < N; c0 += CH) {
@@ -174,6 +225,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       }
       __syncthreads();
       coarse = sm.coarse;
+      if (loop && coarse < 0) coarse = crosscorr_detect(xs, N, cfg, sm); // modem.js:982-985
       r.coarse_idx = coarse;
       if (D && tid == 0) { D->coarse_metric = sm.best; D->coarse_lo = coarse; D->coarse_hi = coarse; }
       if (coarse < 0) {
@@ -217,7 +269,9 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         __syncthreads();
         start = sm.start;
         r.fine_metric = (float)sm.best;
-        if (sm.best < 0.1) status = AMOD_E_LOW_CORR;
+        if (loop) {  // no correlation cut-off; the data part may be empty (modem.js:1012-1045)
+          if (start + 3 * SYM > N) status = AMOD_E_SHORT_CE;
+        } else if (sm.best < 0.1) status = AMOD_E_LOW_CORR;
         else if (start + 3 * SYM > N) status = AMOD_E_SHORT_CE;
         else if (start + 3 * SYM >= N) status = AMOD_E_NO_DATA;
         r.preamble_idx = start;
@@ -230,7 +284,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     if (status != AMOD_OK) {
       if (tid == 0) {
         r.status = status;
-        r.preamble_idx = -1;
+        if (!loop) r.preamble_idx = -1;
         w.res[f] = r;
       }
       __syncthreads();
@@ -256,7 +310,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     __syncthreads();
 
     // ---- demodulateOFDM (modem.js:365-418)
-    const int M = (N - data0) / SYM;
+    const int M = max(0, N - data0) / SYM;
     const int nbits = M * cfg.ndata * cfg.bps;
     const int nwords = (nbits + 31) >> 5;
     for (int i = tid; i < nwords + 8; i += XT) bits[i] = 0u;
@@ -324,6 +378,17 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       nv = block_vote(bits, nbits, cfg.rep, voted);
       wg_global_sync();
       v = voted;
+    }
+    if (loop) {  // analyzeLoopback parses nothing: the raw decoded bytes go back to the caller
+      const int nbytes = nv >> 3, nw = (nbytes + 3) >> 2, cap_w = (int)(w.stride >> 2);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(w.payload + (int64_t)f * w.stride);
+      for (int i = tid; i < nw && i < cap_w; i += XT) dst[i] = __builtin_bswap32(v[i]);
+      if (tid == 0) {
+        r.status = AMOD_OK; r.nbytes = nbytes; r.payload_valid = min(nbytes, 4 * cap_w); r.preamble_idx = start;
+        w.res[f] = r;
+      }
+      __syncthreads();
+      continue;
     }
     finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr, nv >> 3);
     __syncthreads();

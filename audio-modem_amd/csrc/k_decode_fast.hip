@@ -979,7 +979,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           int pflag = 0;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
-            const int b = ln + 64 * rr;
             const bool pil = di_l[rr] == -1;
             const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
             // 0/1 weights in VGPRs (no lane masks kept live across the loop)

@@ -11,6 +11,8 @@
  *          cfg: object, mode: number, options: number, device?: number)
  *       -> { results: ArrayBuffer (96 B per frame), payload: ArrayBuffer, stride: number }
  *   decodeAsync(...same...) -> Promise of the same object (napi_async_work)
+ *   loopback(samples, cfg, device?) -> analyzeLoopback receive core (status, preambleIdx,
+ *          fineMetric, hRe, hIm, bytes)                            modem.js:975-1082
  *   crc32(Uint8Array) -> number                     modem.js:443-457
  *   preamble1(cfg) -> Float32Array                  modem.js:158-170
  *   txLegacy(cfg, data: Uint8Array, name: Uint8Array) -> Float32Array   modem.js:498-555
@@ -323,6 +325,64 @@ static napi_value js_decode_async(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+/* loopback(samples: Float32Array, cfg, device?) -> { status, preambleIdx, fineMetric,
+     hRe: Float64Array, hIm: Float64Array, bytes: Uint8Array }   (modem.js:975-1082 core) */
+static napi_value js_loopback(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 2)
+    return napi_throw_type_error(env, NULL, "loopback(samples, cfg[, device])"), NULL;
+  void *sp;
+  size_t ns;
+  if (!typed(env, argv[0], napi_float32_array, &sp, &ns) || ns > INT32_MAX)
+    return napi_throw_type_error(env, NULL, "samples must be a Float32Array"), NULL;
+  amod_cfg c;
+  if (!to_cfg(env, argv[1], &c)) return NULL;
+  int32_t device = 0;
+  if (argc >= 3 && !is_nullish(env, argv[2])) napi_get_value_int32(env, argv[2], &device);
+  amod_ctx *ctx = get_ctx(env, device);
+  if (!ctx) return NULL;
+  amod_result res;
+  amod_debug *dbg = (amod_debug *)calloc(1, sizeof(amod_debug));
+  const int64_t cap = amod_payload_stride(&c, (int64_t)ns);
+  uint8_t *bytes = (uint8_t *)calloc(1, (size_t)(cap > 0 ? cap : 1));
+  if (!dbg || !bytes) { free(dbg); free(bytes); return throw_msg(env, "out of memory"); }
+  const int rc = amod_analyze_loopback(ctx, &c, (const float *)sp, (int64_t)ns, &res, dbg, bytes, cap);
+  if (rc != AMOD_SUCCESS) {
+    char msg[256];
+    const char *e = amod_last_error(ctx);
+    snprintf(msg, sizeof msg, "libamodem error %d: %s", rc, e ? e : "");
+    free(dbg); free(bytes);
+    return throw_msg(env, msg);
+  }
+  const int nband = c.sub_end - c.sub_start + 1;
+  napi_value out, v, ab, ta;
+  void *p;
+  NAPI_TRY(env, napi_create_object(env, &out));
+  NAPI_TRY(env, napi_create_int32(env, res.status, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "status", v));
+  NAPI_TRY(env, napi_create_int32(env, res.preamble_idx, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "preambleIdx", v));
+  NAPI_TRY(env, napi_create_double(env, dbg->fine_metric, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "fineMetric", v));
+  const double *src[2] = {dbg->h_re, dbg->h_im};
+  const char *names[2] = {"hRe", "hIm"};
+  for (int k = 0; k < 2; ++k) {
+    NAPI_TRY(env, napi_create_arraybuffer(env, sizeof(double) * (size_t)nband, &p, &ab));
+    memcpy(p, src[k], sizeof(double) * (size_t)nband);
+    NAPI_TRY(env, napi_create_typedarray(env, napi_float64_array, (size_t)nband, ab, 0, &ta));
+    NAPI_TRY(env, napi_set_named_property(env, out, names[k], ta));
+  }
+  const int64_t nb = res.status == AMOD_OK ? (res.nbytes < cap ? res.nbytes : cap) : 0;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)nb, &p, &ab));
+  if (nb) memcpy(p, bytes, (size_t)nb);
+  NAPI_TRY(env, napi_create_typedarray(env, napi_uint8_array, (size_t)nb, ab, 0, &ta));
+  NAPI_TRY(env, napi_set_named_property(env, out, "bytes", ta));
+  free(dbg);
+  free(bytes);
+  return out;
+}
+
 /* ------------------------------------------------------------ host utilities */
 static napi_value make_f32(napi_env env, int64_t n, float **data) {
   napi_value ab, ta;
@@ -478,6 +538,7 @@ static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decodeAsync", NULL, js_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"loopback", NULL, js_loopback, NULL, NULL, NULL, napi_enumerable, NULL},
       {"crc32", NULL, js_crc32, NULL, NULL, NULL, napi_enumerable, NULL},
       {"preamble1", NULL, js_preamble1, NULL, NULL, NULL, napi_enumerable, NULL},
       {"txLegacy", NULL, js_tx_legacy, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -236,7 +236,7 @@ struct amod_ctx {
   int nslots = 0;
   int64_t max_len = 0; // longest frame any reservation was sized for
   // host-path staging
-  DevBuf h_samples, h_off, h_len, h_res, h_payload;
+  DevBuf h_samples, h_off, h_len, h_res, h_payload, h_dbg;
   std::mutex mu;
   DevBuf stamps;
   int64_t nstamps = 0;
@@ -410,7 +410,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
                 int64_t max_len) {
   if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
   if (!validate(cfg)) return fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
-  if (mode != AMOD_MODE_RECEIVED && mode != AMOD_MODE_CHUNK) return fail(ctx, "invalid mode", AMOD_ERR_ARG);
+  if (mode != AMOD_MODE_RECEIVED && mode != AMOD_MODE_CHUNK && mode != AMOD_MODE_LOOPBACK)
+    return fail(ctx, "invalid mode", AMOD_ERR_ARG);
+  if (mode == AMOD_MODE_LOOPBACK) options |= AMOD_OPT_FORCE_EXACT; // diagnostics: exact kernel only
   if (nframes < 0) return fail(ctx, "nframes < 0", AMOD_ERR_ARG);
   if (nframes == 0) return AMOD_SUCCESS;
   if (payload_stride < 16 || payload_stride % 16) return fail(ctx, "payload_stride must be a positive multiple of 16", AMOD_ERR_ARG);
@@ -719,6 +721,41 @@ int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_n, double *e
   if (fast_n) *fast_n = (int64_t)ctx->ev_used.size();
   if (exact_n) *exact_n = (int64_t)ctx->ev_used.size();
   ctx->ev_used.clear();
+  return AMOD_SUCCESS;
+}
+
+int amod_analyze_loopback(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t nsamples,
+                          amod_result *res, amod_debug *dbg, uint8_t *bytes, int64_t cap) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  if (!res || !dbg || nsamples < 0 || nsamples > INT32_MAX || (nsamples && !samples) || cap < 0 || (cap && !bytes))
+    return fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  if (!validate(cfg)) return fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int64_t stride = amod_payload_stride(cfg, nsamples);
+  HIP_TRY(ctx->h_samples.ensure(sizeof(float) * (size_t)(nsamples + 4)));
+  HIP_TRY(ctx->h_off.ensure(sizeof(int64_t)));
+  HIP_TRY(ctx->h_len.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx->h_res.ensure(sizeof(amod_result)));
+  HIP_TRY(ctx->h_payload.ensure((size_t)stride));
+  HIP_TRY(ctx->h_dbg.ensure(sizeof(amod_debug)));
+  hipStream_t s = ctx->stream;
+  const int64_t off0 = 0;
+  const int32_t len0 = (int32_t)nsamples;
+  if (nsamples) HIP_TRY(hipMemcpyAsync(ctx->h_samples.p, samples, sizeof(float) * nsamples, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_off.p, &off0, sizeof off0, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_len.p, &len0, sizeof len0, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(ctx->h_dbg.p, 0, sizeof(amod_debug), s));
+  HIP_TRY(hipMemsetAsync(ctx->h_payload.p, 0, (size_t)stride, s));
+  int rc = decode_impl(ctx, cfg, AMOD_MODE_LOOPBACK, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p,
+                       (const int32_t *)ctx->h_len.p, 1, (amod_result *)ctx->h_res.p, (uint8_t *)ctx->h_payload.p,
+                       stride, 0, s, (amod_debug *)ctx->h_dbg.p, nsamples);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(res, ctx->h_res.p, sizeof(amod_result), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(dbg, ctx->h_dbg.p, sizeof(amod_debug), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int64_t nb = std::min<int64_t>(std::max<int32_t>(res->nbytes, 0), std::min<int64_t>(cap, stride));
+  if (nb > 0) HIP_TRY(hipMemcpy(bytes, ctx->h_payload.p, (size_t)nb, hipMemcpyDeviceToHost));
   return AMOD_SUCCESS;
 }
 

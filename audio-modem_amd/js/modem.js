@@ -337,12 +337,49 @@ function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
     });
 }
 
-// analyzeLoopback(recorded, modName, repetition, testData) (modem.js:975-1082):
-// the loopback self-test's RX core (cross-correlation fallback detection, no
-// low-correlation cut-off, channel magnitude and pilot SNR) is SURVEY.md §8f row 4
-// and not yet on the GPU; calling it fails loudly rather than running a CPU copy.
+// analyzeLoopback(recorded, modName, repetition, testData) (modem.js:975-1082).
+// The receive core runs on the GPU (exact kernel: preprocess, Schmidl-Cox with the
+// cross-correlation fallback, fine timing without the 0.1 cut-off, channel estimate,
+// demodulation, vote); the report below uses the reference's own arithmetic on the
+// returned channel estimate and bytes.
 function analyzeLoopback(recorded, modName, repetition, testData) {
-  throw new Error('analyzeLoopback: GPU loopback analysis is not implemented yet (SURVEY.md §8f-4)');
+  const known = Object.prototype.hasOwnProperty.call(MOD_ID, modName);
+  const cfg = nativeCfg(modName, repetition, known ? undefined : false);
+  const r = native.loopback(asFloat32(recorded), cfg);
+  const poor = (detected, correlation) =>
+    ({ detected, correlation, ber: 1, channelMagnitude: [], snrEstimate: 0, quality: 'poor' });
+  if (r.status === 1) return poor(false, 0);               // not detected (modem.js:986)
+  const correlation = Math.max(0, r.fineMetric);
+  if (r.status === 3) return poor(true, correlation);       // no room for the CE (modem.js:1017)
+  if (!known) modulationId(modName);                        // demodulateOFDM would throw here
+  const channelMagnitude = [];
+  for (let b = 0; b < r.hRe.length; b++) channelMagnitude.push(Math.sqrt(r.hRe[b] * r.hRe[b] + r.hIm[b] * r.hIm[b]));
+  let snrSum = 0, snrCount = 0;
+  for (const p of OFDM.PILOTS) {
+    if (p >= OFDM.SUB_START && p <= OFDM.SUB_END) {
+      const b = p - OFDM.SUB_START;
+      const mag = Math.sqrt(r.hRe[b] * r.hRe[b] + r.hIm[b] * r.hIm[b]);
+      if (mag > 1e-6) { snrSum += mag; snrCount++; }
+    }
+  }
+  const avgPilotMag = snrCount > 0 ? snrSum / snrCount : 0;
+  const snrEstimate = avgPilotMag > 0 ? 20 * Math.log10(avgPilotMag) : -Infinity;
+  let ber = 1;
+  const decoded = r.bytes;
+  const start = r.preambleIdx, dataStart = start + 3 * OFDM.SYMBOL_LEN;
+  if (dataStart < recorded.length && decoded.length >= 29) {
+    const dataOffset = 1 + decoded[0] + 4;
+    if (dataOffset + testData.length <= decoded.length) {
+      let errorBits = 0;
+      for (let i = 0; i < testData.length; i++) {
+        const x = decoded[dataOffset + i] ^ testData[i];
+        for (let b = 0; b < 8; b++) errorBits += (x >> b) & 1;
+      }
+      ber = errorBits / (testData.length * 8);
+    }
+  }
+  const quality = ber === 0 && correlation > 0.8 ? 'excellent' : (ber < 0.05 ? 'good' : 'poor');
+  return { detected: true, correlation, ber, channelMagnitude, snrEstimate, quality };
 }
 
 const api = {

@@ -47,6 +47,9 @@ extern "C" {
 /* ---- decode modes ---- */
 #define AMOD_MODE_RECEIVED 0 /* decodeReceivedSignal: preprocess + detect + demod + parse */
 #define AMOD_MODE_CHUNK 1    /* decodeChunkFrame: frame starts at preamble 1             */
+#define AMOD_MODE_LOOPBACK 2 /* analyzeLoopback's receive core (exact kernel): detection
+                                with the cross-correlation fallback, fine timing without the
+                                0.1 cut-off, channel estimate and the raw decoded bytes      */
 
 /* ---- decode option bits ---- */
 #define AMOD_OPT_FORCE_EXACT 1u /* run every frame through the exact-replica kernel */
@@ -177,6 +180,16 @@ int amod_decode_device_debug(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, c
                              const int64_t *offsets, const int32_t *lengths, int32_t nframes,
                              amod_result *results, uint8_t *payload, int64_t payload_stride,
                              uint32_t options, void *stream, amod_debug *debug);
+
+/* analyzeLoopback (modem.js:975-1082) receive core for one host signal: fills
+   res (status AMOD_E_PREAMBLE = not detected even by the cross-correlation fallback
+   (modem.js:235-284), AMOD_E_SHORT_CE = no room for the CE symbol; preamble_idx =
+   startIdx; nbytes = decoded bytes after the vote, stored in bytes[0, min(nbytes, cap))),
+   dbg->fine_metric (bestMetric, -inf if no offset passed the gate) and dbg->h_re/h_im
+   (the channel estimate over the band). The caller finishes the report (channel
+   magnitude, pilot SNR, BER, quality) with the reference's own arithmetic.        */
+int amod_analyze_loopback(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t nsamples,
+                          amod_result *res, amod_debug *dbg, uint8_t *bytes, int64_t cap);
 
 /* diagnostics: with AMOD_STAMPS set in the environment, the fast kernel records
    32 s_memtime marks per frame (wave 0); copies up to cap of them, returns count */

@@ -656,13 +656,17 @@ void orc_payload(uint32_t seed, int len, uint8_t *out) {
 }
 
 void orc_add_noise(const float *in, int n, int snr_db, uint32_t seed, float *out) {
+  double div = 1;
+  for (int k = 0; k < snr_db / 10; k++) div *= 10;
+  orc_add_noise_div(in, n, div, seed, out);
+}
+
+void orc_add_noise_div(const float *in, int n, double div, uint32_t seed, float *out) {
   double p = 0;
   int cnt = 0;
   for (int i = 0; i < n; i++)
     if (in[i] != 0.0f) { p += (double)in[i] * (double)in[i]; cnt++; }
   p = cnt > 0 ? p / (double)cnt : 0.0;
-  double div = 1;
-  for (int k = 0; k < snr_db / 10; k++) div *= 10;
   const double sigma = sqrt(p / div);
   uint32_t s = seed;
   for (int i = 0; i < n; i++) {

@@ -109,6 +109,8 @@ int orc_build_test_signal(const orc_cfg *c, int mod, int rep, float *out); /* 91
 uint32_t orc_xs32(uint32_t s);
 void orc_payload(uint32_t seed, int len, uint8_t *out);
 void orc_add_noise(const float *in, int n, int snr_db, uint32_t seed, float *out);
+/* same generator with an explicit signal/noise power divisor (test fixtures' `div`) */
+void orc_add_noise_div(const float *in, int n, double div, uint32_t seed, float *out);
 
 /* multi-threaded CPU baseline: decode nframes legacy frames laid out at offsets */
 double orc_bench_decode(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,

@@ -82,6 +82,7 @@ def lib():
             "orc_xs32": (C.c_uint32, [C.c_uint32]),
             "orc_payload": (None, [C.c_uint32, C.c_int, u8p]),
             "orc_add_noise": (None, [f32p, C.c_int, C.c_int, C.c_uint32, f32p]),
+            "orc_add_noise_div": (None, [f32p, C.c_int, C.c_double, C.c_uint32, f32p]),
             "orc_bench_decode": (C.c_double, [cfgp, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                               C.c_int, C.c_void_p, C.c_void_p]),
         }
@@ -141,11 +142,14 @@ def build_tx(c: Cfg, tx: dict) -> np.ndarray:
     raise ValueError(k)
 
 
-def add_noise(x: np.ndarray, snr: int, seed: int) -> np.ndarray:
+def add_noise(x: np.ndarray, snr: int, seed: int, div: float | None = None) -> np.ndarray:
     x = np.ascontiguousarray(x, np.float32)
     out = np.empty_like(x)
     if len(x):
-        lib().orc_add_noise(x, len(x), snr, seed & 0xFFFFFFFF, out)
+        if div is None:
+            lib().orc_add_noise(x, len(x), snr, seed & 0xFFFFFFFF, out)
+        else:
+            lib().orc_add_noise_div(x, len(x), float(div), seed & 0xFFFFFFFF, out)
     return out
 
 
@@ -154,7 +158,7 @@ def apply_post(x: np.ndarray, post) -> np.ndarray:
         if op["op"] == "slice":
             x = x[op["start"]:op.get("end")]
         elif op["op"] == "noise":
-            x = add_noise(x, op["snr"], op["seed"])
+            x = add_noise(x, op.get("snr", 0), op["seed"], op.get("div"))
         elif op["op"] == "dc":
             x = (x.astype(np.float64) + op["dc"]).astype(np.float32)
         else:

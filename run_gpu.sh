@@ -15,7 +15,6 @@ for s in "$@"; do
     pmcstages) run pmc_stages 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --kernel-trace -d gpurun_out/pmc_stages -o run --output-format csv -- python tools/stage_profile.py;;
     variants) for v in ${VARIANTS:-w5s8}; do run bench_$v 300 env AMODEM_LIB=audio-modem_amd/lib/variants/$v/libamodem.so python bench.py --steps 20 --warmup 3 --cpu-frames -1; done;;
     pmcic) run pmc_ic 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/pmc_ic -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-frames -1;;
-    pcs) run pcs 600 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method ${PCS_METHOD:-stochastic} --pc-sampling-unit ${PCS_UNIT:-cycles} --pc-sampling-interval ${PCS_INT:-65536} --kernel-trace -d gpurun_out/pcs -o run --output-format csv -- python bench.py --steps 30 --warmup 2 --cpu-frames -1;;
     pmcstages2) run pmc_stages2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LEVEL_WAVES SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_VMEM --kernel-trace -d gpurun_out/pmc_stages2 -o run --output-format csv -- python tools/stage_profile.py;;
     listpc) run listpc 120 rocprofv3 -L;;
   esac

@@ -41,11 +41,13 @@ function frameSeed(idx) { return (0x9E3779B9 ^ idx) >>> 0; }
 
 // Noise: sigma^2 = P_active / 10^(snr/10) with snr in {10,20,30} (exact divisor);
 // g = (sum of 12 uniforms u = x/2^32) - 6 ; y = fround(s + sigma*g).
-function addNoise(sig, snrDb, seed) {
+// (or an explicit divisor `div`, a dyadic/small-integer value, for in-between SNRs)
+function addNoise(sig, snrDb, seed, divOverride) {
   let p = 0, cnt = 0;
   for (let i = 0; i < sig.length; i++) { const v = sig[i]; if (v !== 0) { p += v * v; cnt++; } }
   p = cnt > 0 ? p / cnt : 0;
   let div = 1; for (let k = 0; k < snrDb / 10; k++) div *= 10;
+  if (divOverride !== undefined) div = divOverride;
   const sigma = Math.sqrt(p / div);
   let s = seed >>> 0;
   const out = new Float32Array(sig.length);
@@ -94,7 +96,7 @@ function buildTx(tx) {
 function applyPost(sig, post) {
   for (const op of post || []) {
     if (op.op === 'slice') sig = sig.slice(op.start, op.end);
-    else if (op.op === 'noise') sig = addNoise(sig, op.snr, op.seed);
+    else if (op.op === 'noise') sig = addNoise(sig, op.snr, op.seed, op.div);
     else if (op.op === 'dc') sig = addDC(sig, op.dc);
     else throw new Error('bad post op');
   }
@@ -413,12 +415,54 @@ for (const [cfg, mod, rep, len, name] of [['standard', 'QPSK', 1, 1024, 'f.bin']
 setOFDMConfig('standard');
 kat.payloadXs32 = { seed: frameSeed(0), hex16: hex(payloadBytes(frameSeed(0), 16)) };
 
+// ------------------------------------------------------- analyzeLoopback --
+const jsonNum = (v) => (Number.isFinite(v) ? v : String(v));
+const loopback = [];
+{
+  const td = new Uint8Array(16);
+  for (let i = 0; i < 16; i++) td[i] = i;
+  const L = (name, config, tx, post, mod, rep) => {
+    setOFDMConfig(config);
+    const sig = applyPost(buildTx(tx), post);
+    const res = analyzeLoopback(sig, mod, rep, td);
+    const sc = detectPreamble(preprocessSignal(sig));
+    loopback.push({
+      name, config, tx, post, mod, rep, n: sig.length, sigSha: sha(sig), scCoarse: sc,
+      result: { detected: res.detected, correlation: jsonNum(res.correlation), ber: res.ber,
+        channelMagnitude: res.channelMagnitude.map(jsonNum), snrEstimate: jsonNum(res.snrEstimate), quality: res.quality },
+    });
+  };
+  const T = (mod, rep) => ({ kind: 'test', mod, rep });
+  L('lb_std_qpsk', 'standard', T('QPSK', 1), [], 'QPSK', 1);
+  L('lb_std_qam16', 'standard', T('QAM16', 1), [], 'QAM16', 1);
+  L('lb_std_bpsk_rep3', 'standard', T('BPSK', 3), [], 'BPSK', 3);
+  L('lb_ac_bpsk', 'acoustic', T('BPSK', 1), [], 'BPSK', 1);
+  L('lb_ac_bpsk_rep3', 'acoustic', T('BPSK', 3), [], 'BPSK', 3);
+  L('lb_nb_bpsk_rep3', 'narrowband', T('BPSK', 3), [], 'BPSK', 3);
+  // div = P_signal / P_noise: 100 (20 dB), 10, 4 (~6 dB), 2 (~3 dB), 1 (0 dB), 0.5 (~-3 dB)
+  for (const div of [100, 10, 4, 2, 1, 0.5])
+    L(`lb_std_qpsk_div${div}`, 'standard', T('QPSK', 1), [{ op: 'noise', div, seed: 0x1234 + Math.round(div * 2) }], 'QPSK', 1);
+  for (const div of [4, 2, 1])
+    L(`lb_ac_bpsk_rep3_div${div}`, 'acoustic', T('BPSK', 3), [{ op: 'noise', div, seed: 0x777 + div }], 'BPSK', 3);
+  L('lb_zeros', 'standard', { kind: 'zeros', n: 30000 }, [], 'QPSK', 1);
+  L('lb_short', 'standard', { kind: 'zeros', n: 300 }, [], 'QPSK', 1);
+  L('lb_no_ce', 'standard', T('QPSK', 1), [{ op: 'slice', start: 0, end: 13230 + 2 * 576 + 300 }], 'QPSK', 1);
+  L('lb_no_data', 'standard', T('QPSK', 1), [{ op: 'slice', start: 0, end: 13230 + 3 * 576 }], 'QPSK', 1);
+  L('lb_one_sym', 'standard', T('QPSK', 1), [{ op: 'slice', start: 0, end: 13230 + 4 * 576 + 10 }], 'QPSK', 1);
+  L('lb_dc', 'standard', T('QPSK', 1), [{ op: 'dc', dc: 0.25 }], 'QPSK', 1);
+  L('lb_tone', 'standard', { kind: 'periodic', n: 20000, values: tonePeriod(64, 5, 0.5) }, [], 'QPSK', 1);
+  L('lb_wrong_mod', 'standard', T('QPSK', 1), [], 'QAM16', 1);
+  setOFDMConfig('standard');
+}
+
 const meta = {
   generator: 'tests/golden/gen_golden.js', node: process.version,
   reference: 'playok/audio-modem modem.js (loaded unmodified via vm.runInThisContext)',
 };
 fs.writeFileSync(path.join(OUT, 'kat.json'), JSON.stringify({ meta, ...kat }));
 fs.writeFileSync(path.join(OUT, 'frames.json'), JSON.stringify({ meta, frames }));
+fs.writeFileSync(path.join(OUT, 'loopback.json'), JSON.stringify({ meta, loopback }));
+for (const c of loopback) console.log('loopback', c.name.padEnd(26), 'sc', c.scCoarse, JSON.stringify(c.result).slice(0, 90));
 console.log('wrote', frames.length, 'frame cases;',
   'kat.json', fs.statSync(path.join(OUT, 'kat.json')).size, 'B; frames.json', fs.statSync(path.join(OUT, 'frames.json')).size, 'B');
 for (const f of frames) {

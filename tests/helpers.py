@@ -41,6 +41,12 @@ def frames():
         return json.load(f)["frames"]
 
 
+@functools.lru_cache(None)
+def loopback():
+    with open(os.path.join(GOLDEN, "loopback.json")) as f:
+        return json.load(f)["loopback"]
+
+
 def frame(name):
     for c in frames():
         if c["name"] == name:

@@ -47,6 +47,7 @@ async function main() {
         case 'ofdm': r = { cfg: Object.assign({}, M.OFDM, { isPilot: undefined, numDataSubs: undefined }), nds: M.OFDM.numDataSubs() }; break;
         case 'decode': r = M.decodeReceivedSignal(f32(j.file), j.mod, j.rep); break;
         case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
+        case 'loopback': r = M.analyzeLoopback(f32(j.file), j.mod, j.rep, Uint8Array.from(j.testData)); break;
         case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { mode: j.mode }); break;
         default: throw new Error('unknown op ' + j.op);
       }
