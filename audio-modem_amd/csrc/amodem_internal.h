@@ -71,7 +71,8 @@ struct DevWork {
   uint32_t options;
   unsigned long long *stamps; // diagnostics (AMOD_STAMPS=1): per-frame s_memtime marks, 32 per frame
   int32_t nb_cap;     // fast kernel: Schmidl-Cox moment blocks per frame (dynamic LDS)
-  int32_t bits_cap;   // fast kernel: raw bit words per frame (dynamic LDS)
+  int32_t bits_cap;   // fast kernel: packed bit-stream words per frame (dynamic LDS)
+  int32_t rows_cap;   // fast kernel: symbol-row words per frame (dynamic LDS)
 };
 
 // ---------------------------------------------------------------- helpers --
@@ -357,5 +358,5 @@ __device__ inline void init_result(amod_result &r) {
 extern "C" {
 hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
-int amod_fast_lds_bytes(int nb_cap, int bits_cap); // dynamic LDS of one fast-kernel workgroup
+int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap); // dynamic LDS of one fast-kernel workgroup
 }

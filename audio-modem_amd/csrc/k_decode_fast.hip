@@ -38,6 +38,7 @@ constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
 constexpr int FINE_MAX = 1024;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
+constexpr int SC_CACHE = 16;                 // candidate blocks whose per-position results stay in LDS
 constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT round (+ CE)
 #ifndef AMOD_SB
 #define AMOD_SB 8
@@ -49,16 +50,20 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 
 // Dynamic LDS, sized per launch from the reserved frame length (amod_fast_lds_bytes):
 // one region reused by the stages, addressed by float / float2 / word index.
-//   stages 0-1: s1[nbc] s2[nbc] sx[nbc] (block moments -> caps / E_b / Z_b), cand[256]
+//   stages 0-1: s1[nbc] s2[nbc] sx[nbc] (block moments -> caps / E_b / Z_b), cand[256] (int16),
+//               cmax[256], pass-1 cache[SC_CACHE][32] (float2: top metric, uncertainty bits)
 //   stage 2   : tmpl[768] m[FINE_MAX + 8] yw[FINE_MAX + 800] q[FINE_MAX + 280] (folded window)
-//   stage 3-4 : xch[4][512] float2 (FFT exchange; voted bits at finish), g[256] float2,
-//               bits[bitc] (raw demodulated bits)
+//               E[FINE_MAX + 800] (prefix of squares of yw)
+//   stage 3-4 : xch[4][512] float2 (FFT exchange; decision bytes after each FFT; voted bits
+//               at finish), g[256] float2, twiddles, bits[bitc] (packed stream),
+//               rows[rows_cap + 1] (word-aligned bit row per data symbol)
 extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_F (reinterpret_cast<float *>(amod_dyn))
 #define LDS_F2 (reinterpret_cast<float2 *>(amod_dyn))
 #define LDS_U (reinterpret_cast<uint32_t *>(amod_dyn))
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
 constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
+constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the window, span + 1 entries
 constexpr int FQ_G = NWAVE * 512;             // float2 index of g
 #ifndef AMOD_TW_LDS
 #define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
@@ -148,6 +153,32 @@ __device__ void fft512_wave(float2 (&v)[8], const int xb, const float2 *__restri
   __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ float2 spec_read(const int xb, int n) { return LDS_F2[xb + spec_idx(n & 511)]; }
+
+// Symbol rows (one word-aligned row of wsym words per data symbol, MSB-first) ->
+// the frame's contiguous MSB-first bit stream (bitsToBytes order, modem.js:468-476):
+// word W takes bits [32 W, 32 W + 32) across as many rows as it spans. Bits past
+// nsym rows are zero. Row storage needs one readable word past the last row.
+__device__ void repack_rows(const uint32_t *rows, int wsym, int per_sym, int nsym, uint32_t *out) {
+  const int nw = (nsym * per_sym + 31) >> 5;
+  for (int W = ltid(); W < nw; W += WG) {
+    const int g = 32 * W;
+    int s = g / per_sym, l = g - s * per_sym;
+    uint32_t acc = 0;
+    int got = 0;
+    while (got < 32 && s < nsym) {
+      const int n = min(32 - got, per_sym - l);
+      const uint32_t *rw = rows + s * wsym + (l >> 5);
+      const int o = l & 31;
+      uint32_t x = o ? (rw[0] << o) | (rw[1] >> (32 - o)) : rw[0];
+      x &= n >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> n);
+      acc |= x >> got;
+      got += n;
+      ++s;
+      l = 0;
+    }
+    out[W] = acc;
+  }
+}
 
 // Constellation decision (modem.js:140-150) and its distance to the nearest
 // decision boundary. Ties resolve to the lowest index like the reference loop.
@@ -278,9 +309,9 @@ __device__ __forceinline__ const KArgs &kargs() {
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
-  (void)cfg_arg;
-  (void)w_arg;
+// SCAN_ONLY: the same code stopped after the Schmidl-Cox decision (k_corr_scan, the
+// correlation-scan phase measured on its own; nothing is written)
+template <bool SCAN_ONLY> __device__ __forceinline__ void decode_fast() {
   __shared__ Smem sm;
   FRESH_ARGS;
   const int nbc = w.nb_cap, bitc = w.bits_cap; // dynamic LDS capacities of this launch
@@ -340,6 +371,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc((void *)(X - ph), (short)0, 16 * nfull, 0x00020000);
       const float c0 = X[0];
+      // the <= 3 samples of a trailing partial float4, requested now (lanes 0-2) so that
+      // thread 0's tail step below does not wait for memory after the pass
+      float tailv = 0.f;
+      {
+        const int k = kfull + (lane & 3);
+        if (lane < 3 && k < K && k >= ph) tailv = X[k - ph];
+      }
       const int q0 = (wave * nch) / NWAVE, q1 = ((wave + 1) * nch) / NWAVE;
       float sacc = 0.f;
       float mn = INFINITY, mxv = -INFINITY;
@@ -389,6 +427,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       sacc_d = wave_sum(sacc_d);
       mn = -wmax(-mn);
       mxv = wmax(mxv);
+      const float tail0 = rlane(tailv, 0), tail1 = rlane(tailv, 1), tail2 = rlane(tailv, 2);
       if (lane == 0) { sm.rd[wave] = sacc_d; sm.rf[wave] = mn; sm.rf[NWAVE + wave] = mxv; }
       __syncthreads();
       if (tid == 0) {
@@ -396,7 +435,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         float MN = INFINITY, MX = -INFINITY;
         for (int i = 0; i < NWAVE; ++i) { S += sm.rd[i]; MN = fminf(MN, sm.rf[i]); MX = fmaxf(MX, sm.rf[NWAVE + i]); }
         for (int k = max(kfull, ph); k < K; ++k) { // trailing partial float4
-          const float x = X[k - ph], u = x - c0;
+          const float x = k == kfull ? tail0 : (k == kfull + 1 ? tail1 : tail2), u = x - c0;
           S += (double)u; MN = fminf(MN, x); MX = fmaxf(MX, x);
           LDS_F[k >> 5] += u;
           LDS_F[nbc + (k >> 5)] = fmaf(u, u, LDS_F[nbc + (k >> 5)]);
@@ -483,6 +522,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       const float gate_lo = 0.01f * (1.f - eps_g) - errw, gate_hi = 0.01f * (1.f + eps_g) + errw;
       const float *const Eb = LDS_F + nbc, *const Zb = LDS_F + 2 * nbc;
       const int CMAX = 3 * nbc + SC_MAXCAND / 2;   // per-candidate max metric (after cand[])
+      const int PCACHE = CMAX + SC_MAXCAND;        // pass-1 results of the first SC_CACHE blocks
       float *const cap = LDS_F;
       const int ncb = (E + ph) / BLK + 1; // blocks holding at least one position d in [0, E]
       // (a) window sums at block starts: a rigorous lower bound Lb on the best metric,
@@ -517,10 +557,17 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       float Lb = -1.f;
       for (int i = 0; i < NWAVE; ++i) Lb = fmaxf(Lb, sm.rf[i]);
       // (b) blocks whose cap reaches Lb - eps_c
-      for (int c = tid; c < ncb; c += WG) {
-        if (cap[c] >= Lb - eps_c) {
-          const int slot = atomicAdd(&sm.ncand, 1);
-          if (slot < SC_MAXCAND) LDS_I16[6 * nbc + slot] = (int16_t)c;
+      //     compacted per wave with a ballot: one LDS atomic per wave and 64 blocks
+      for (int c0 = 64 * wave; c0 < ncb; c0 += WG) {
+        const int c = c0 + lane;
+        const bool pred = c < ncb && cap[c] >= Lb - eps_c;
+        const uint64_t mask = __ballot(pred);
+        if (mask) {
+          int base = 0;
+          if (lane == 0) base = atomicAdd(&sm.ncand, (int)__popcll(mask));
+          base = __shfl(base, 0);
+          const int slot = base + (int)__popcll(mask & ((1ull << lane) - 1ull));
+          if (pred && slot < SC_MAXCAND) LDS_I16[6 * nbc + slot] = (int16_t)c;
         }
       }
       __syncthreads();
@@ -571,6 +618,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
             blo = fmaxf(blo, mlo);
             bhi = fmaxf(bhi, mhi);
           }
+          // pass 2 reads the first SC_CACHE blocks' positions from LDS instead of memory
+          if (g < SC_CACHE) {
+            const int u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > 0.25f * eps_c) << 1);
+            LDS_F[PCACHE + 2 * (32 * g + (lane & 31))] = ok ? fmaxf(m, mhi) : -INFINITY;
+            LDS_U[PCACHE + 2 * (32 * g + (lane & 31)) + 1] = (uint32_t)u;
+          }
           // the block's highest possible metric, for pass 2's filter
           float top = ok ? fmaxf(m, mhi) : -2.f;
           top = fmaxf(top, AMOD_DPP_F(top, 0xB1)); top = fmaxf(top, AMOD_DPP_F(top, 0x4E));
@@ -605,12 +658,21 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
       if (CBH >= 0.5f - eps_c) {
         for (int g = 2 * wave + (lane >> 5); g - (lane >> 5) < ncand; g += 2 * NWAVE) {
           if (g < ncand && LDS_F[CMAX + g] >= CBL - eps_c) { // blocks that can reach the band
-            float m, mlo, mhi, ra, rb;
-            int d;
-            if (cand_eval(g, m, mlo, mhi, d, ra, rb) && fmaxf(m, mhi) >= CBL - eps_c) {
+            float v;
+            int d, u;
+            if (g < SC_CACHE) {
+              v = LDS_F[PCACHE + 2 * (32 * g + (lane & 31))];
+              u = (int)LDS_U[PCACHE + 2 * (32 * g + (lane & 31)) + 1];
+              d = BLK * (int)LDS_I16[6 * nbc + g] - ph + (lane & 31);
+            } else {
+              float m, mlo, mhi, ra, rb;
+              const bool ok = cand_eval(g, m, mlo, mhi, d, ra, rb);
+              v = ok ? fmaxf(m, mhi) : -INFINITY;
+              u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > 0.25f * eps_c) << 1);
+            }
+            if (v >= CBL - eps_c) {
               lo = min(lo, d); hi = max(hi, d);
-              unc |= (ra <= gate_hi || rb <= gate_hi);
-              unc |= (mhi - mlo) > 0.25f * eps_c; // block-sum error not negligible here
+              unc |= u != 0; // energy gate or block-sum error not negligible here
             }
           }
         }
@@ -633,7 +695,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
     if (sm.flags) goto to_exact;
     if (sm.status != AMOD_OK) goto finish_error;
     STAMP(5);
-    if (cfg.stop_after == 1) return;
+    if (SCAN_ONLY || cfg.stop_after == 1) return;
 
     // ---------------------------------------------- stage 2: fine timing
     {
@@ -653,10 +715,32 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         __syncthreads();
         goto finish_error;
       }
-      // template + the normalised search window, staged once in LDS
-      for (int i = tid; i < SYM; i += WG) LDS_F[FINE_TM + i] = cfg.t.pre1[i];
+      // template + the normalised search window, staged once in LDS. All loads of a
+      // thread are issued before its first store (one memory latency, not one per
+      // loop trip): raw buffer loads past the frame end return 0 without a branch.
       const int span = P + SYM + 16;
-      for (int j = tid; j < span; j += WG) LDS_F[FINE_YW + j] = (w0 + j < N) ? fmaf(X[w0 + j], A, B) : 0.f;
+      {
+        constexpr int TR = (768 + WG - 1) / WG, YR = (FINE_MAX + 768 + 16 + WG - 1) / WG;
+        const __amdgpu_buffer_rsrc_t rx =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(X + w0), (short)0, 4 * (N - w0), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rt =
+            __builtin_amdgcn_make_buffer_rsrc((void *)cfg.t.pre1, (short)0, 4 * SYM, 0x00020000);
+        float tv[TR], yv[YR];
+#pragma unroll
+        for (int r = 0; r < TR; ++r)
+          tv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, 4 * (tid + r * WG), 0, 0));
+#pragma unroll
+        for (int r = 0; r < YR; ++r)
+          yv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, 4 * (tid + r * WG), 0, 0));
+#pragma unroll
+        for (int r = 0; r < TR; ++r)
+          if (tid + r * WG < SYM) LDS_F[FINE_TM + tid + r * WG] = tv[r];
+#pragma unroll
+        for (int r = 0; r < YR; ++r) {
+          const int j = tid + r * WG;
+          if (j < span) LDS_F[FINE_YW + j] = (w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
+        }
+      }
       __syncthreads();
       const float te = cfg.te_f;
       const int noct = (P + 7) >> 3;
@@ -667,13 +751,45 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         // corr(d) = sum_{i<256} t[i] (y[d+i] + fold y[d+i+256]) + sum_{i<CP} t[i] y[d+i+512]
         // (t[i+256] = fold t[i]): 256 + CP taps instead of SYM
         for (int j = tid; j < 8 * noct + 264; j += WG) LDS_F[FINE_Q + j] = fmaf((float)fold, yw[j + 256], yw[j]);
-        __syncthreads();
       }
+      // window energies from a prefix of squares: E[j] = sum_{i<j} y[i]^2, en(d) = E[d+SYM] - E[d].
+      // Each E[j] carries <= ~26 roundings of partial sums <= E[span]: |err en| <= en_err.
+      float en_err;
+      {
+        float sq[8], s = 0.f;
+        const int b0 = 8 * tid;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float v = b0 + k < span ? yw[b0 + k] : 0.f;
+          sq[k] = v * v;
+          s += sq[k];
+        }
+        float inc = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float t = __shfl_up(inc, o, 64);
+          if (lane >= o) inc += t;
+        }
+        if (lane == 63) sm.rf[wave] = inc;
+        __syncthreads();
+        float run = -s + inc, tot = 0.f;
+        for (int i = 0; i < NWAVE; ++i) {
+          const float wv = sm.rf[i];
+          if (i < wave) run += wv;
+          tot += wv;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (b0 + k <= span) LDS_F[FINE_E + b0 + k] = run;
+          run += sq[k];
+        }
+        en_err = 4e-6f * tot + 1e-30f;
+      }
+      __syncthreads();
       const float *qw = LDS_F + FINE_Q;
       // lane = (octet of 8 positions, one of 8 tap ranges): per tap one window read,
-      // one template read, 8 correlations; the energy of the octet's first position
-      // runs over its own SYM/8 range. The 8 ranges of an octet are 8 aligned lanes,
-      // combined by DPP.
+      // one template read, 8 correlations. The 8 ranges of an octet are 8 aligned
+      // lanes, combined by DPP; energies come from the prefix E.
       for (int task = tid; task < noct * 8; task += WG) {
         const int oc = task >> 3, sp = task & 7;
         const int j0 = 8 * oc; // window offset of the octet's first position
@@ -710,22 +826,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           split(SYM, i0, cnt);
           corr(yw, j0, i0, cnt);
         }
-        float e0 = 0.f; // energy of position j0 over this lane's share of the SYM taps
-        split(SYM, i0, cnt);
-#pragma unroll 8
-        for (int i = i0; i < i0 + cnt; ++i) e0 = fmaf(yw[j0 + i], yw[j0 + i], e0);
 #pragma unroll
         for (int r = 0; r < 8; ++r) c[r] = dpp_sum8(c[r]);
-        e0 = dpp_sum8(e0);
         if (j0 + sp < P) {
-          // lane sp finishes position j0 + sp: slide the energy forward sp samples
+          // lane sp finishes position j0 + sp
           float cj = c[0];
 #pragma unroll
           for (int r = 1; r < 8; ++r) cj = sp == r ? c[r] : cj;
-          float en = e0;
-          for (int j = 0; j < sp; ++j) {
-            const float yo = yw[j0 + j], yn = yw[j0 + j + SYM];
-            en = fmaf(yn, yn, fmaf(-yo, yo, en));
+          const int d = j0 + sp;
+          float en = LDS_F[FINE_E + d + SYM] - LDS_F[FINE_E + d];
+          if (en < 1e4f * en_err) { // low-energy window: the difference is not accurate enough
+            en = 0.f;
+            for (int i = 0; i < SYM; ++i) en = fmaf(yw[d + i], yw[d + i], en);
           }
           const float den = sqrtf(fmaxf(en, 0.f) * te);
           float m;
@@ -815,27 +927,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
     const int nbits = M * per_sym;
     const int nbytes_total = (nbits / cfg.rep) >> 3;
     const int nband = cfg.nband;
-    // tables
-    for (int i = tid; i < bitc; i += WG) LDS_U[FQ_BITS + i] = 0u;
-    if (AMOD_TW_LDS) {
-      for (int i = tid; i < 8 * 64; i += WG) LDS_F2[FQ_TW + i] = cfg.t.tw1[i];
-      for (int i = tid; i < 8 * 8; i += WG) LDS_F2[FQ_TW + 8 * 64 + i] = cfg.t.tw2[i];
-    }
-    // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
-    int di_l[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) di_l[rr] = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
-    if (tid == 0) {
-      sm.gmax = 0.f; sm.zce = 0.f;
-      sm.target = dbg ? M : min(M, FIRST_SYMS);
-      if (sm.target * per_sym > bitc * 32) sm.flags |= AMOD_FLAG_BIG;
-    }
-    __syncthreads();
-    if (sm.flags) goto to_exact;
-    STAMP(7);
-    int done = 0;                  // data symbols decoded so far (a prefix)
-    int need_bytes = 0;
-    int wflags = 0;
+    const int wsym = (per_sym + 31) >> 5;      // words per symbol row
+    const int fq_sa = FQ_BITS + bitc;          // word index of the symbol rows
     // Jobs are numbered over the whole frame: job 0 = (CE, symbol 0), job j = (2j-1, 2j);
     // wave w owns jobs w, w+4, ... and prefetches its next job's samples while it
     // transforms and demaps the current one (across the round boundary too: the
@@ -857,7 +950,37 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         r2[m] = X[p2 + CP + lane + 64 * m];
       }
     };
-    int jdone = 0;                 // jobs completed in earlier rounds
+    // this wave's first-round job (job `wave`: its symbols are the same for the round-1
+    // target and for M) is requested before the tables, so its latency overlaps them
+    if (wave == 0 || 2 * wave - 1 < M) { load_job(wave, M, pf1, pf2); pf_job = wave; }
+    // tables: every load issued before the first LDS store
+    {
+      const float2 t1a = cfg.t.tw1[tid], t1b = cfg.t.tw1[tid + WG], t2 = cfg.t.tw2[tid & 63];
+      const float kn = cfg.t.known[min(tid, nband - 1)];
+      if (AMOD_TW_LDS) {
+        LDS_F2[FQ_TW + tid] = t1a;
+        LDS_F2[FQ_TW + WG + tid] = t1b;
+        if (tid < 64) LDS_F2[FQ_TW + 8 * 64 + tid] = t2;
+      }
+      // the CE signs ride in the G slots until the CE job overwrites them with G
+      if (tid < nband) LDS_F[2 * (FQ_G + tid)] = kn;
+    }
+    // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
+    int di_l[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) di_l[rr] = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
+    if (tid == 0) {
+      sm.gmax = 0.f; sm.zce = 0.f;
+      sm.target = dbg ? M : min(M, FIRST_SYMS);
+      if (sm.target * per_sym > bitc * 32 || sm.target * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
+    }
+    __syncthreads();
+    if (sm.flags) goto to_exact;
+    STAMP(7);
+    int done = 0;                  // data symbols decoded so far (a prefix)
+    int need_bytes = 0;
+    int wflags = 0;
+    int jdone = 0;                // jobs completed in earlier rounds
     for (;;) {
       FRESH_ARGS;
       const int target = sm.target;
@@ -915,7 +1038,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
               if (!const1) {
                 const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
                 const float2 y = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-                const float kn = cfg.t.known[b];
+                const float kn = LDS_F[2 * (FQ_G + b)]; // staged CE sign (overwritten with G below)
                 h = make_float2(y.x * kn, y.y * kn);
               }
               const float m2 = h.x * h.x + h.y * h.y;
@@ -941,7 +1064,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
           int ln = lane;
           asm volatile("" : "+v"(ln)); // per-round lane (keeps debug/bit addresses out of registers)
           const bool live1 = s1 >= 0 && !const1, live2 = s2 >= 0 && !const2;
-          uint32_t *bits = (LDS_U + FQ_BITS);
           float2 e1[4], e2[4];
           float zm = 0.f, em1 = 0.f, em2 = 0.f;
 #pragma unroll
@@ -1009,8 +1131,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
             if (s2 >= 0 && s2 < AMOD_DBG_SYMS) D->phase[s2] = const2 ? 0.f : ph2;
           }
           // a constant FFT window has an all-zero spectrum in the reference: every data
-          // subcarrier takes the origin decision (ties resolve to the first point)
+          // subcarrier takes the origin decision (ties resolve to the first point).
+          // Decisions are staged as bytes by data index in the wave's exchange buffer
+          // (free once the band is read), then packed below.
           int dflag = 0;
+          uint8_t *const stg = reinterpret_cast<uint8_t *>(LDS_F2 + xb);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int b = ln + 64 * rr;
@@ -1032,19 +1157,44 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
                 idx = decide(cfg.mod, cr, ci, margin);
                 dflag |= margin <= (which == 0 ? tau1 : tau2);
               }
-              const int pos = sidx * per_sym + di * cfg.bps;
-              const uint32_t val = (uint32_t)idx << (32 - cfg.bps - (pos & 31));
-              if (val) atomicOr(&bits[pos >> 5], val);
+              stg[256 * which + di] = (uint8_t)idx;
             }
           }
           if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
+          __builtin_amdgcn_wave_barrier();
+          // pack: lane t takes data subcarrier 64 q + t; each aligned group of 32/bps lanes
+          // ORs (DPP) its bits into one word of the symbol's word-aligned row, written by
+          // the group's first lane (no atomics: a symbol belongs to one wave)
+          {
+            const int bps = cfg.bps, ndata = cfg.ndata;
+#pragma unroll
+            for (int which = 0; which < 2; ++which) {
+              const int sidx = which == 0 ? s1 : s2;
+              if (sidx < 0) continue;
+              uint32_t *const row = LDS_U + fq_sa + sidx * wsym;
+              for (int q = 0; 64 * q < ndata; ++q) {
+                const int di = 64 * q + ln;
+                const uint32_t idx = di < ndata ? (uint32_t)stg[256 * which + di] : 0u;
+                uint32_t v = idx << (32 - bps - ((di * bps) & 31));
+                v |= (uint32_t)AMOD_DPP_I((int)v, 0xB1);
+                v |= (uint32_t)AMOD_DPP_I((int)v, 0x4E);
+                v |= (uint32_t)AMOD_DPP_I((int)v, 0x141); // groups of 8 (16-QAM)
+                if (bps < 4) v |= (uint32_t)AMOD_DPP_I((int)v, 0x140); // 16 (QPSK)
+                if (bps < 2) v |= (uint32_t)__shfl_xor((int)v, 16, 32); // 32 (BPSK)
+                if ((ln & (32 / bps - 1)) == 0 && di < ndata) row[(di * bps) >> 5] = v;
+              }
+            }
+          }
           if (r == 0) STAMP(first ? 11 : 18);
         }
       }
-      __syncthreads(); // the round's bits are complete
+      __syncthreads(); // the round's symbol rows are complete
       STAMP(first ? 12 : 19);
       done = target;
       jdone = jend;
+      // rows [0, done) -> the MSB-first bit stream the parse, vote and CRC read
+      repack_rows(LDS_U + fq_sa, wsym, per_sym, min(done, M), LDS_U + FQ_BITS);
+      __syncthreads();
       // how much of the voted stream the parse reads; decode more symbols if needed
       if (tid == 0) {
         const int avail = ((min(done * per_sym, nbits) / cfg.rep) >> 3);
@@ -1053,7 +1203,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
         if (need_bytes > avail) {
           const int64_t raw = (int64_t)need_bytes * 8 * cfg.rep;
           t = (int)min<int64_t>((int64_t)M, ((raw + per_sym - 1) / per_sym) | 1); // whole jobs
-          if ((int64_t)t * per_sym > bitc * 32) sm.flags |= AMOD_FLAG_BIG;
+          if ((int64_t)t * per_sym > bitc * 32 || t * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
         }
         sm.target = t;
         sm.ru[0] = (uint32_t)need_bytes;
@@ -1115,20 +1265,34 @@ to_exact:
   }
 }
 
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  decode_fast<false>();
+}
+// stream pass + Schmidl-Cox only (diagnostics: AMOD_STOP_AFTER=1); launched with the same
+// dynamic LDS as k_decode_fast, so the same number of workgroups share a CU
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  decode_fast<true>();
+}
+
 } // namespace
 } // namespace amod
 
 extern "C" hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s) {
   if (w.nframes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_decode_fast, dim3(w.nframes), dim3(amod::WG),
-                     (unsigned)amod_fast_lds_bytes(w.nb_cap, w.bits_cap), s, cfg, w);
+  hipLaunchKernelGGL(cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_decode_fast, dim3(w.nframes), dim3(amod::WG),
+                     (unsigned)amod_fast_lds_bytes(w.nb_cap, w.bits_cap, w.rows_cap), s, cfg, w);
   return hipGetLastError();
 }
-// dynamic LDS bytes of a launch with nb_cap moment blocks and bits_cap bit words
-extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap) {
+// dynamic LDS bytes of a launch with nb_cap moment blocks, bits_cap stream words and
+// rows_cap symbol-row words
+extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap) {
   using namespace amod;
-  const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND;
-  const int fine = 4 * (FINE_Q + FINE_MAX + 280);
-  const int fq = 4 * (FQ_BITS + bits_cap);
+  const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND + 8 * 32 * SC_CACHE;
+  const int fine = 4 * (FINE_E + FINE_MAX + 800);
+  const int fq = 4 * (FQ_BITS + bits_cap + rows_cap + 1);
   return (std::max(mom, std::max(fine, fq)) + 15) & ~15;
 }

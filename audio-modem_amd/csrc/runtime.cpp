@@ -438,6 +438,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.nb_cap = 8 * (int)((flen + 3 + 255) / 256) + 8;
     const int64_t words = (flen / cfg->symbol_len) * amod_num_data_subs(cfg) * bps_of(cfg->modulation) / 32 + 2;
     w.bits_cap = (int)std::min<int64_t>(2048, words);
+    const int64_t wsym = ((int64_t)amod_num_data_subs(cfg) * bps_of(cfg->modulation) + 31) / 32;
+    w.rows_cap = (int)std::min<int64_t>(4096, (flen / cfg->symbol_len) * wsym + 2);
   }
   if (getenv("AMOD_STAMPS")) { // diagnostics: per-frame s_memtime marks of the fast kernel
     HIP_TRY(ctx->stamps.ensure(sizeof(unsigned long long) * 32 * (size_t)nframes));
