@@ -245,6 +245,23 @@ __device__ __forceinline__ int wor_i(int v) {
          (__builtin_amdgcn_readlane(v, 32) | __builtin_amdgcn_readlane(v, 48));
 }
 
+// Whole-wave sum / max to a wave-uniform value with one readlane: row reductions by DPP,
+// then row_bcast:15 (rows 1, 3 take rows 0, 2) and row_bcast:31 (rows 2, 3 take lane 31),
+// so lane 63 holds the total. Whole wave active.
+__device__ __forceinline__ float wsum_b(float v) {
+  v += AMOD_DPP_F(v, 0xB1); v += AMOD_DPP_F(v, 0x4E); v += AMOD_DPP_F(v, 0x141); v += AMOD_DPP_F(v, 0x140);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  return rlane(v, 63);
+}
+__device__ __forceinline__ float wmax_b(float v) {
+  v = fmaxf(v, AMOD_DPP_F(v, 0xB1)); v = fmaxf(v, AMOD_DPP_F(v, 0x4E));
+  v = fmaxf(v, AMOD_DPP_F(v, 0x141)); v = fmaxf(v, AMOD_DPP_F(v, 0x140));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x142, 0xA, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x143, 0xC, 0xF, false)));
+  return rlane(v, 63);
+}
+
 // inclusive prefix sum inside each aligned 32-lane group: row_shr 1/2/4/8 inside rows of
 // 16, then row_bcast:15 carries row 0 (2) into row 1 (3). The group's lanes all active.
 __device__ __forceinline__ float scan32(float v) {
@@ -310,8 +327,10 @@ __device__ __forceinline__ const KArgs &kargs() {
   } while (0)
 
 // SCAN_ONLY: the same code stopped after the Schmidl-Cox decision (k_corr_scan, the
-// correlation-scan phase measured on its own; nothing is written)
-template <bool SCAN_ONLY> __device__ __forceinline__ void decode_fast() {
+// correlation-scan phase measured on its own; nothing is written).
+// DBG: parity-test build that also records intermediates (amod_decode_device_debug);
+// the production instantiation carries none of that code.
+template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast() {
   __shared__ Smem sm;
   FRESH_ARGS;
   const int nbc = w.nb_cap, bitc = w.bits_cap; // dynamic LDS capacities of this launch
@@ -327,7 +346,7 @@ template <bool SCAN_ONLY> __device__ __forceinline__ void decode_fast() {
   const int K = ph + N;                      // k-space end (exclusive)
   const float *const X = w.samples + off;    // frame sample i at X[i]
   const int SYM = cfg.sym, CP = cfg.cp;
-  const bool dbg = w.dbg != nullptr;
+  constexpr bool dbg = DBG;
   amod_debug *D = dbg ? w.dbg + f : nullptr;
   STAMP(0);
   {
@@ -969,6 +988,13 @@ template <bool SCAN_ONLY> __device__ __forceinline__ void decode_fast() {
     int di_l[4];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) di_l[rr] = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
+    // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
+    // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
+    int prr = -1, npl = 0;
+#pragma unroll
+    for (int rr = 3; rr >= 0; --rr)
+      if (di_l[rr] == -1) { prr = rr; ++npl; }
+    const bool pil_multi = __ballot(npl > 1) != 0;
     if (tid == 0) {
       sm.gmax = 0.f; sm.zce = 0.f;
       sm.target = dbg ? M : min(M, FIRST_SYMS);
@@ -1094,31 +1120,41 @@ template <bool SCAN_ONLY> __device__ __forceinline__ void decode_fast() {
           // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
           const float gsc = 2e-6f * cfg.guard * gmax;
           float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
-          d1 = wmax(d1); d2 = wmax(d2);
+          d1 = wmax_b(d1); d2 = wmax_b(d2);
           d1 += 1e-12f; d2 += 1e-12f;
           // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
           float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
           int pflag = 0;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const bool pil = di_l[rr] == -1;
-            const float a1 = fabsf(e1[rr].x), a2 = fabsf(e2[rr].x);
-            // 0/1 weights in VGPRs (no lane masks kept live across the loop)
+          auto pilot = [&](bool pil, float2 q1e, float2 q2e) {
+            const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
+            // 0/1 weights in VGPRs (no lane masks kept live)
             const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
             // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below
             // signed 1/eqRe, finite for every lane (weight 0 where the reference skips)
-            const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), e1[rr].x));
-            const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), e2[rr].x));
+            const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), q1e.x));
+            const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), q2e.x));
             const float r1 = fabsf(q1), r2 = fabsf(q2);
-            ps1 = fmaf(w1 * q1, e1[rr].y, ps1);
-            ps2 = fmaf(w2 * q2, e2[rr].y, ps2);
-            pe1 = fmaf(w1 * r1, fmaf(fabsf(e1[rr].y), r1, 1.f), pe1);
-            pe2 = fmaf(w2 * r2, fmaf(fabsf(e2[rr].y), r2, 1.f), pe2);
+            ps1 = fmaf(w1 * q1, q1e.y, ps1);
+            ps2 = fmaf(w2 * q2, q2e.y, ps2);
+            pe1 = fmaf(w1 * r1, fmaf(fabsf(q1e.y), r1, 1.f), pe1);
+            pe2 = fmaf(w2 * r2, fmaf(fabsf(q2e.y), r2, 1.f), pe2);
             pc1 += w1;
             pc2 += w2;
             pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
+          };
+          if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
+            float2 p1 = e1[0], p2 = e2[0];
+#pragma unroll
+            for (int rr = 1; rr < 4; ++rr) {
+              p1 = prr == rr ? e1[rr] : p1;
+              p2 = prr == rr ? e2[rr] : p2;
+            }
+            pilot(prr >= 0, p1, p2);
+          } else {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) pilot(di_l[rr] == -1, e1[rr], e2[rr]);
           }
-          ps1 = wsum(ps1); pe1 = wsum(pe1); ps2 = wsum(ps2); pe2 = wsum(pe2); pc1 = wsum(pc1); pc2 = wsum(pc2);
+          ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); pc1 = wsum_b(pc1); pc2 = wsum_b(pc2);
           if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
           const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
           const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
@@ -1268,14 +1304,19 @@ to_exact:
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  decode_fast<false>();
+  decode_fast<false, false>();
+}
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  decode_fast<false, true>();
 }
 // stream pass + Schmidl-Cox only (diagnostics: AMOD_STOP_AFTER=1); launched with the same
 // dynamic LDS as k_decode_fast, so the same number of workgroups share a CU
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  decode_fast<true>();
+  decode_fast<true, false>();
 }
 
 } // namespace
@@ -1283,7 +1324,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
 
 extern "C" hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s) {
   if (w.nframes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_decode_fast, dim3(w.nframes), dim3(amod::WG),
+  auto *k = w.dbg ? amod::k_decode_fast_dbg : (cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_decode_fast);
+  hipLaunchKernelGGL(k, dim3(w.nframes), dim3(amod::WG),
                      (unsigned)amod_fast_lds_bytes(w.nb_cap, w.bits_cap, w.rows_cap), s, cfg, w);
   return hipGetLastError();
 }
