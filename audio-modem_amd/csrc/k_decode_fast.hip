@@ -44,6 +44,9 @@ constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT ro
 #define AMOD_SB 8
 #endif
 constexpr int SB = AMOD_SB;                  // stream pass: chunks per load batch
+#ifndef AMOD_RING
+#define AMOD_RING 1                          // stream pass: rolling ring of SB + 1 chunk loads
+#endif
 #ifndef AMOD_WPE
 #define AMOD_WPE 5                           // waves per SIMD the register budget is sized for
 #endif
@@ -379,6 +382,20 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     const int nch = (K + 255) >> 8;
     const int NB = (K + BLK - 1) / BLK;
     const int bz_edge = max(0, (K - 256) >> 5); // blocks >= this have pairs past the frame end
+    // Samples of the blocks whose pairs leave the frame (and of block 0 when the frame
+    // starts mid-float4), summed directly below: requested now, so their latency hides
+    // under the stream pass. Edge slot e: block 0 (e = 0) or bz_edge + e - 1; there are
+    // at most NB - bz_edge <= 9 such blocks, so two rounds of 8 32-lane groups cover them.
+    float ex0[2], ex1[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int e = 2 * wave + (lane >> 5) + 2 * NWAVE * it;
+      const int b = e == 0 ? 0 : bz_edge + e - 1;
+      const int i = BLK * b + (lane & 31) - ph;
+      const bool use = b < NB && !(e == 0 && (ph == 0 || bz_edge == 0)) && i >= 0 && i + 256 < N;
+      ex0[it] = use ? X[i] : 0.f;
+      ex1[it] = use ? X[i + 256] : 0.f;
+    }
     {
       FRESH_ARGS;
       // Vector pass over the float4s wholly inside the frame's k-range (k < kfull);
@@ -429,6 +446,30 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           LDS_F[b] = s1; LDS_F[nbc + b] = s2; LDS_F[2 * nbc + b] = sx;
         }
       };
+#if AMOD_RING
+      // a ring of R chunk registers kept full: chunk q is stepped with its partner q + 1
+      // (next slot), then its slot is refilled with chunk q + R, so about R - 1 loads per
+      // wave stay in flight through the whole pass (no drain between batches). The
+      // wave's last chunk q1 - 1 takes chunk q1 as partner; refills past q1 re-read
+      // chunk q1 (a cache hit): every load is unconditional, so the in-order vmcnt
+      // accounting stays exact and each step waits only for its own two chunks.
+      constexpr int R = SB + 1;
+      float4 c[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        c[j] = LD(min(q0 + j, q1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      for (int qb = q0; qb < q1; qb += R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const int q = qb + j;
+          if (q < q1) step(q, c[j], c[(j + 1) % R]);
+          c[j] = LD(min(q + R, q1));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
       // batches of SB chunks (+ the partner chunk): SB + 1 loads in flight, then SB steps
       // in straight-line code so each step waits only for its own two chunks
       for (int qb = q0; qb < q1; qb += SB) {
@@ -442,6 +483,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         for (int j = 0; j < SB; ++j)
           if (qb + j < q1) step(qb + j, c[j], c[j + 1]); // partner of chunk q is chunk q + 1 (k + 256)
       }
+#endif
       double sacc_d = (lane & 7) == 0 ? (double)sacc : 0.0;
       sacc_d = wave_sum(sacc_d);
       mn = -wmax(-mn);
@@ -502,13 +544,14 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       // blocks whose pairs leave the frame (and block 0 when the frame starts mid-float4):
       // summed directly from the samples, one 32-lane group per block
       const float Af = sm.A, Bf = sm.B;
-      for (int e = 2 * wave + (lane >> 5);; e += 2 * NWAVE) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int e = 2 * wave + (lane >> 5) + 2 * NWAVE * it;
         const int b = e == 0 ? 0 : bz_edge + e - 1;
-        if (b >= NB) break;
-        if (e == 0 && (ph == 0 || bz_edge == 0)) continue;
-        const int k = BLK * b + (lane & 31), i = k - ph;
+        if (b >= NB || (e == 0 && (ph == 0 || bz_edge == 0))) continue; // uniform per 32-lane group
+        const int i = BLK * b + (lane & 31) - ph;
         float z = 0.f;
-        if (i >= 0 && i + 256 < N) z = fmaf(X[i], Af, Bf) * fmaf(X[i + 256], Af, Bf);
+        if (i >= 0 && i + 256 < N) z = fmaf(ex0[it], Af, Bf) * fmaf(ex1[it], Af, Bf);
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) z += __shfl_xor(z, o, 32);
         if ((lane & 31) == 0) LDS_F[2 * nbc + b] = z;
@@ -602,7 +645,14 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       // sums at d0 + j are the block-start sums plus an exclusive prefix (across the
       // group) of the per-position slide increments. m_lo/m_hi bracket the metric
       // given the block-sum error errw.
-      auto cand_eval = [&](int cidx, float &m, float &mlo, float &mhi, int &d, float &ra, float &rb) -> bool {
+      // raw samples of candidate block cidx at d, d + 256, d + 512 (0 outside the frame)
+      auto cand_load = [&](int cidx, float (&xr)[3]) {
+        const int d = BLK * (int)LDS_I16[6 * nbc + cidx] - ph + (lane & 31);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) xr[t] = (d + 256 * t >= 0 && d + 256 * t < N) ? X[d + 256 * t] : 0.f;
+      };
+      auto cand_eval = [&](int cidx, const float (&xr)[3], float &m, float &mlo, float &mhi, int &d, float &ra,
+                           float &rb) -> bool {
         const int j = lane & 31;
         const int c = LDS_I16[6 * nbc + cidx];
         float p = 0.f;
@@ -610,9 +660,9 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
 #pragma unroll
         for (int q = 0; q < 8; ++q) { p += Zb[c + q]; ra += Eb[c + q]; rb += Eb[c + 8 + q]; }
         d = BLK * c - ph + j;
-        const float y0 = (d >= 0 && d < N) ? fmaf(X[d], A, B) : 0.f;
-        const float y1 = (d + 256 >= 0 && d + 256 < N) ? fmaf(X[d + 256], A, B) : 0.f;
-        const float y2 = (d + 512 >= 0 && d + 512 < N) ? fmaf(X[d + 512], A, B) : 0.f;
+        const float y0 = (d >= 0 && d < N) ? fmaf(xr[0], A, B) : 0.f;
+        const float y1 = (d + 256 >= 0 && d + 256 < N) ? fmaf(xr[1], A, B) : 0.f;
+        const float y2 = (d + 512 >= 0 && d + 512 < N) ? fmaf(xr[2], A, B) : 0.f;
         const float z0 = (d >= 0 && d < N - 256) ? y0 * y1 : 0.f;
         const float z1 = (d + 256 >= 0 && d + 256 < N - 256) ? y1 * y2 : 0.f;
         const float vp = z1 - z0, va = fmaf(y1, y1, -y0 * y0), vb = fmaf(y2, y2, -y1 * y1);
@@ -627,11 +677,25 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       };
       float best = -1.f, blo = -1.f, bhi = -1.f;
       int bidx = 0x7fffffff;
-      for (int g = 2 * wave + (lane >> 5); g - (lane >> 5) < ncand; g += 2 * NWAVE) {
+      // the samples of a group's first two blocks (16 per workgroup: the usual plateau
+      // neighbourhood) are requested together, one memory latency for both
+      const int g0 = 2 * wave + (lane >> 5);
+      float xq[2][3];
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+        if (g0 + 2 * NWAVE * it < ncand) cand_load(g0 + 2 * NWAVE * it, xq[it]);
+      for (int g = g0, it = 0; g - (lane >> 5) < ncand; g += 2 * NWAVE, ++it) {
         if (g < ncand) {
           float m, mlo, mhi, ra, rb;
           int d;
-          const bool ok = cand_eval(g, m, mlo, mhi, d, ra, rb);
+          float xr[3];
+          if (it < 2) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) xr[t] = it == 0 ? xq[0][t] : xq[1][t];
+          } else {
+            cand_load(g, xr);
+          }
+          const bool ok = cand_eval(g, xr, m, mlo, mhi, d, ra, rb);
           if (ok) {
             if (m > best || (m == best && d < bidx)) { best = m; bidx = d; }
             blo = fmaxf(blo, mlo);
@@ -684,8 +748,9 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
               u = (int)LDS_U[PCACHE + 2 * (32 * g + (lane & 31)) + 1];
               d = BLK * (int)LDS_I16[6 * nbc + g] - ph + (lane & 31);
             } else {
-              float m, mlo, mhi, ra, rb;
-              const bool ok = cand_eval(g, m, mlo, mhi, d, ra, rb);
+              float m, mlo, mhi, ra, rb, xr[3];
+              cand_load(g, xr);
+              const bool ok = cand_eval(g, xr, m, mlo, mhi, d, ra, rb);
               v = ok ? fmaxf(m, mhi) : -INFINITY;
               u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > 0.25f * eps_c) << 1);
             }

@@ -17,5 +17,6 @@ for s in "$@"; do
     pmcic) run pmc_ic 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/pmc_ic -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-frames -1;;
     pmcstages2) run pmc_stages2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LEVEL_WAVES SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_VMEM --kernel-trace -d gpurun_out/pmc_stages2 -o run --output-format csv -- python tools/stage_profile.py;;
     listpc) run listpc 120 rocprofv3 -L;;
+    ab) run ab 600 python tools/ab.py $(for v in ${VARIANTS}; do echo audio-modem_amd/lib/variants/$v/libamodem.so; done);;
   esac
 done
