@@ -17,6 +17,7 @@ MAX_PILOTS = 32
 BPSK, QPSK, QAM16 = 0, 1, 2
 MODS = {"BPSK": BPSK, "QPSK": QPSK, "QAM16": QAM16}
 MODE_RECEIVED, MODE_CHUNK, MODE_LOOPBACK = 0, 1, 2
+TX_LEGACY, TX_META, TX_CHUNK = 0, 1, 2
 OPT_FORCE_EXACT = 1
 
 OK = 0
@@ -87,6 +88,14 @@ SIGNATURES = {
     "amod_tx_chunk": (C.c_int64, [C.POINTER(Cfg), C.c_char_p, C.c_int32, C.c_int32, _P]),
     "amod_tx_test_signal": (C.c_int64, [C.POINTER(Cfg), _P]),
     "amod_synth_payload": (None, [C.c_uint32, C.c_int32, _P]),
+    "amod_packet_legacy": (C.c_int64, [C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, _P]),
+    "amod_packet_meta": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P]),
+    "amod_packet_chunk": (C.c_int64, [C.c_char_p, C.c_int32, C.c_int32, _P]),
+    "amod_tx_silence": (C.c_int, [C.POINTER(Cfg), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "amod_tx_frame_samples": (C.c_int64, [C.POINTER(Cfg), C.c_int64, C.c_int32, C.c_int32]),
+    "amod_tx_device": (C.c_int, [_P, C.POINTER(Cfg), _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P]),
+    "amod_tx_host": (C.c_int64, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P]),
+    "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),
 }

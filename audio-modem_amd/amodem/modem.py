@@ -205,6 +205,39 @@ class Demodulator:
     def synchronize(self):
         L.check(self._L.amod_synchronize(self.ctx), self.ctx)
 
+    # ------------------------------------------------------------ transmitter
+    def transmit_device(self, cfg: L.Cfg, packets_ptr: int, pkt_off_ptr: int, pkt_len_ptr: int, pre_ptr: int,
+                        post_ptr: int, nframes: int, out_ptr: int, out_off_ptr: int, stream: int = 0):
+        """Enqueue k_tx (GPU modulateOFDM + frame builder) over device-resident packets."""
+        L.check(self._L.amod_tx_device(self.ctx, C.byref(cfg), packets_ptr, pkt_off_ptr, pkt_len_ptr, pre_ptr,
+                                       post_ptr, int(nframes), out_ptr, out_off_ptr, stream or None), self.ctx)
+
+    def transmit_batch(self, cfg: L.Cfg, packets, kinds):
+        """Frames of the given packets (bytes) and builder kinds (TX_LEGACY / TX_META /
+        TX_CHUNK, one per packet or one for all) through the GPU transmitter.
+        Returns (samples float32, offsets int64, lengths int32), frames back to back."""
+        packets = [bytes(p) for p in packets]
+        n = len(packets)
+        kinds = [kinds] * n if isinstance(kinds, int) else list(kinds)
+        plen = np.array([len(p) for p in packets], np.int32)
+        poff = np.concatenate([[0], np.cumsum(plen)[:-1]]).astype(np.int64) if n else np.zeros(0, np.int64)
+        buf = np.frombuffer(b"".join(packets) or b"\0", np.uint8).copy()
+        pre = np.zeros(n, np.int32)
+        post = np.zeros(n, np.int32)
+        for i, k in enumerate(kinds):
+            pre[i], post[i] = tx_silence(cfg, k)
+        args = (self.ctx, C.byref(cfg), buf.ctypes.data, int(plen.sum()), poff.ctypes.data, plen.ctypes.data,
+                pre.ctypes.data, post.ctypes.data, n)
+        with self._lock:
+            total = self._L.amod_tx_host(*args, None, None)
+            if total < 0:
+                raise RuntimeError(f"libamodem error {total}: {L.last_error(self.ctx)}")
+            out = np.zeros(max(int(total), 1), np.float32)
+            offs = np.zeros(n, np.int64)
+            L.check(0 if self._L.amod_tx_host(*args, out.ctypes.data, offs.ctypes.data) == total else -1, self.ctx)
+        lens = np.diff(np.append(offs, total)).astype(np.int32)
+        return out[:total], offs, lens
+
 
 # ------------------------------------------------------------ host utilities --
 def crc32(data: bytes) -> int:
@@ -260,6 +293,54 @@ def build_data_chunk_frame(data: bytes, seq: int, mod="QPSK", rep=1, cfg=None):
 def generate_test_signal(mod="QPSK", rep=1, cfg=None):
     cfg = cfg or make_cfg(mod, rep)
     return _tx(L.load().amod_tx_test_signal, C.byref(cfg)), bytes(range(16))
+
+
+def _packet(fn, *args) -> bytes:
+    n = fn(*args, None)
+    if n < 0:
+        raise ValueError("invalid packet arguments")
+    out = np.zeros(max(int(n), 1), np.uint8)
+    fn(*args, out.ctypes.data)
+    return out[:n].tobytes()
+
+
+def packet_legacy(data: bytes, file_name="file") -> bytes:
+    """buildTransmitSignal's packet [nameLen][name][dataLen:4][data][CRC:4] (modem.js:500-521)."""
+    data = bytes(data)
+    name = (file_name or "file").encode("utf-8")
+    return _packet(L.load().amod_packet_legacy, data, len(data), name, len(name))
+
+
+def packet_meta(total_chunks: int, total_size: int, chunk_size: int, file_name="file") -> bytes:
+    """buildMetadataPayload (modem.js:666-692)."""
+    name = (file_name or "file").encode("utf-8")
+    return _packet(L.load().amod_packet_meta, int(total_chunks), int(total_size), int(chunk_size), name, len(name))
+
+
+def packet_chunk(data: bytes, seq: int) -> bytes:
+    """buildDataChunkPayload (modem.js:694-714)."""
+    data = bytes(data)
+    return _packet(L.load().amod_packet_chunk, data, len(data), int(seq))
+
+
+def tx_silence(cfg: L.Cfg, kind: int):
+    pre, post = C.c_int32(), C.c_int32()
+    L.check(L.load().amod_tx_silence(C.byref(cfg), int(kind), C.byref(pre), C.byref(post)))
+    return pre.value, post.value
+
+
+def synth_legacy_packets(nframes: int, payload_len: int = 1024, name: str = "f.bin", first: int = 0):
+    """Packets of the synthetic legacy workload (payload seed 0x9E3779B9 ^ frame index),
+    back to back: (bytes uint8, offsets int64, lengths int32)."""
+    lib = L.load()
+    nm = name.encode()
+    total = lib.amod_synth_legacy_packets(nframes, first, payload_len, nm, len(nm), None, None, None)
+    buf = np.zeros(max(int(total), 1), np.uint8)
+    offs = np.zeros(nframes, np.int64)
+    lens = np.zeros(nframes, np.int32)
+    lib.amod_synth_legacy_packets(nframes, first, payload_len, nm, len(nm), buf.ctypes.data, offs.ctypes.data,
+                                  lens.ctypes.data)
+    return buf, offs, lens
 
 
 def synth_payload(seed: int, length: int) -> bytes:

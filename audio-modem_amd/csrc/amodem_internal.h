@@ -2,14 +2,17 @@
 //
 // Frame pipeline (per frame, mirrors modem.js decodeReceivedSignal 557-654 and
 // decodeChunkFrame 770-803):
-//   k_decode_fast  (k_decode_fast.hip)  one 1024-thread workgroup per frame, frame
-//                   resident in LDS, fp32 arithmetic with guard bands on every
-//                   discrete decision; a frame whose decision falls inside a guard
-//                   band (or that does not fit LDS) is appended to the exact list.
+//   k_decode_fast  (k_decode_fast.hip)  one 256-thread workgroup per frame, the
+//                   frame streamed once from HBM, fp32 arithmetic with guard bands on
+//                   every discrete decision; a frame whose decision falls inside a
+//                   guard band (or that exceeds the launch's LDS capacities) is
+//                   appended to the exact list.
 //   k_decode_exact (k_decode_exact.hip) replays the reference arithmetic in IEEE
 //                   double, operation for operation, for the listed frames.
 // Both end in finish_frame() below: majority vote, MSB-first byte packing, frame
 // parsing and CRC-32 — integer work, bit-exact by construction.
+//   k_tx           (k_tx.hip) the transmitter (modulateOFDM + frame builders) in
+//                   IEEE double, bit-exact, for synthetic input at HBM rate.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,6 +40,8 @@ struct DevTables {
   const uint32_t *crc_m2;  // [32][4][256] shift-by-(512*q) operators, q<32
   const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
   const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
+  const double2 *tw_inv;   // [511] inverse-transform recurrence twiddles (fftIterative, ifft)
+  const float *tmpl;       // [3][symbol_len] pre1, pre2, CE symbols (f32, before normalisation)
 };
 
 struct DevCfg {
@@ -49,7 +54,20 @@ struct DevCfg {
   int32_t fold;        // +-1: pre1[i + 256] = fold * pre1[i] (fast fine stage folds on it), 0: no fold
   float guard;         // fast-path guard scale (1 = default)
   int32_t stop_after;  // diagnostics only (AMOD_STOP_AFTER): fast kernel returns after this stage
+  float tx_tmax;       // max |tmpl| (k_tx normalisation)
   DevTables t;
+};
+
+// k_tx: one frame per workgroup; every pointer device memory
+struct DevTxWork {
+  const uint8_t *pkt;     // packet bytes (legacy packet / metadata / data-chunk payload)
+  const int64_t *pkt_off; // [nframes] byte offset of frame f's packet
+  const int32_t *pkt_len; // [nframes]
+  const int32_t *pre;     // [nframes] leading silence samples
+  const int32_t *post;    // [nframes] trailing silence samples
+  float *out;             // output samples
+  const int64_t *out_off; // [nframes] first output sample of frame f
+  int32_t nframes;
 };
 
 struct DevWork {
@@ -358,5 +376,6 @@ __device__ inline void init_result(amod_result &r) {
 extern "C" {
 hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
+hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
 int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap); // dynamic LDS of one fast-kernel workgroup
 }

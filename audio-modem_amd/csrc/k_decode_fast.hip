@@ -703,7 +703,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           }
           // pass 2 reads the first SC_CACHE blocks' positions from LDS instead of memory
           if (g < SC_CACHE) {
-            const int u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > 0.25f * eps_c) << 1);
+            const int u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > eps_c) << 1);
             LDS_F[PCACHE + 2 * (32 * g + (lane & 31))] = ok ? fmaxf(m, mhi) : -INFINITY;
             LDS_U[PCACHE + 2 * (32 * g + (lane & 31)) + 1] = (uint32_t)u;
           }
@@ -752,11 +752,11 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
               cand_load(g, xr);
               const bool ok = cand_eval(g, xr, m, mlo, mhi, d, ra, rb);
               v = ok ? fmaxf(m, mhi) : -INFINITY;
-              u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > 0.25f * eps_c) << 1);
+              u = (ra <= gate_hi || rb <= gate_hi) | (((mhi - mlo) > eps_c) << 1);
             }
             if (v >= CBL - eps_c) {
               lo = min(lo, d); hi = max(hi, d);
-              unc |= u != 0; // energy gate or block-sum error not negligible here
+              unc |= u != 0; // near the energy gate, or a metric interval wider than the guard
             }
           }
         }
@@ -772,6 +772,14 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         else if (CBL <= 0.5f + eps_c || U) flags |= AMOD_FLAG_COARSE;  // threshold, gate or error ambiguous
         else if (HI - LO > 2 * 3 * CP) flags |= AMOD_FLAG_COARSE;      // no common fine window
         sm.flags = flags; sm.clo = LO; sm.chi = HI;
+#ifdef AMOD_DIAG
+        if (w.stamps) { // diagnostics build only: the coarse decision's inputs
+          unsigned long long *st = w.stamps + (int64_t)f * 32 + 20;
+          st[0] = __float_as_uint(CB); st[1] = __float_as_uint(CBL); st[2] = __float_as_uint(CBH);
+          st[3] = (unsigned)U; st[4] = (unsigned)LO; st[5] = (unsigned)HI; st[6] = (unsigned)ncand;
+          st[7] = __float_as_uint(sm.errw);
+        }
+#endif
         if (dbg) { D->coarse_metric = CB; D->coarse_lo = LO; D->coarse_hi = HI; }
       }
       __syncthreads();

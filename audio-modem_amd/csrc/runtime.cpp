@@ -239,6 +239,7 @@ struct amod_ctx {
   DevBuf h_samples, h_off, h_len, h_res, h_payload, h_dbg;
   std::mutex mu;
   DevBuf stamps;
+  DevBuf tx_pkt, tx_meta, tx_out; // amod_tx_host staging
   int64_t nstamps = 0;
   // kernel timing (amod_set_profiling)
   bool profiling = false;
@@ -303,10 +304,15 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     const char *sa = getenv("AMOD_STOP_AFTER"); // stage-cost diagnostics; results are not written
     d.stop_after = sa ? atoi(sa) : 99;
     // host images
-    std::vector<float> pre1(sym), ce(sym);
+    std::vector<float> pre1(sym), ce(sym), tmpl(3 * (size_t)sym);
     double known_full[amod::kFft] = {0};
     template_symbol(*c, 42.0, 2, pre1.data(), nullptr);
     template_symbol(*c, 44.0, 1, ce.data(), known_full);
+    template_symbol(*c, 42.0, 2, tmpl.data(), nullptr);
+    template_symbol(*c, 43.0, 1, tmpl.data() + sym, nullptr);
+    template_symbol(*c, 44.0, 1, tmpl.data() + 2 * sym, nullptr);
+    d.tx_tmax = 0.f;
+    for (float v : tmpl) d.tx_tmax = std::max(d.tx_tmax, std::fabs(v));
     double te = 0.0;
     for (int i = 0; i < sym; ++i) te += (double)pre1[i] * (double)pre1[i];
     d.te = te; d.te_f = (float)te;
@@ -339,7 +345,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
         const double a = -2.0 * M_PI * (double)((8 * l1 * p) % amod::kFft) / amod::kFft;
         tw2[2 * (p * 8 + l1)] = (float)std::cos(a); tw2[2 * (p * 8 + l1) + 1] = (float)std::sin(a);
       }
-    const std::vector<double> twx = stage_twiddles(false);
+    const std::vector<double> twx = stage_twiddles(false), twi = stage_twiddles(true);
     std::vector<double> pts(2 * 16, 0.0);
     for (int i = 0; i < npoints(c->modulation); ++i) constellation(c->modulation, i, pts[2 * i], pts[2 * i + 1]);
     // one device allocation, 256-byte aligned pieces
@@ -347,7 +353,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_pre1 = carve(sym * 4), o_tw1 = carve(tw1.size() * 4), o_tw2 = carve(tw2.size() * 4),
                  o_twx = carve(twx.size() * 8), o_known = carve(nband * 4), o_di = carve(nband * 2),
-                 o_pts = carve(pts.size() * 8);
+                 o_pts = carve(pts.size() * 8), o_twi = carve(twi.size() * 8), o_tmpl = carve(tmpl.size() * 4);
     if (ts->buf.ensure(off) != hipSuccess) return fail(ctx, "hipMalloc(tables)", AMOD_ERR_NOMEM);
     char *base = (char *)ts->buf.p;
     HIP_TRY(hipMemcpy(base + o_pre1, pre1.data(), sym * 4, hipMemcpyHostToDevice));
@@ -357,6 +363,8 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     HIP_TRY(hipMemcpy(base + o_known, known.data(), nband * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_di, band_di.data(), nband * 2, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_pts, pts.data(), pts.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_twi, twi.data(), twi.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(base + o_tmpl, tmpl.data(), tmpl.size() * 4, hipMemcpyHostToDevice));
     d.t.pre1 = (const float *)(base + o_pre1);
     d.t.tw1 = (const float2 *)(base + o_tw1);
     d.t.tw2 = (const float2 *)(base + o_tw2);
@@ -364,6 +372,8 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.t.known = (const float *)(base + o_known);
     d.t.band_di = (const int16_t *)(base + o_di);
     d.t.points = (const double2 *)(base + o_pts);
+    d.t.tw_inv = (const double2 *)(base + o_twi);
+    d.t.tmpl = (const float *)(base + o_tmpl);
     const uint32_t *crc = (const uint32_t *)ctx->crc.p;
     d.t.crc_s4 = crc;
     d.t.crc_m1 = crc + 1024;
@@ -532,6 +542,32 @@ std::vector<uint8_t> legacy_packet(const uint8_t *data, int32_t len, const uint8
   p.push_back((uint8_t)name_len);
   p.insert(p.end(), name, name + name_len);
   put_be32(p, len);
+  p.insert(p.end(), data, data + len);
+  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
+  return p;
+}
+
+// buildMetadataPayload (modem.js:666-692): [0xFE][chunks:4][size:4][chunkSize:2][nameLen:1][name][CRC:4]
+std::vector<uint8_t> meta_packet(int32_t total_chunks, int32_t total_size, int32_t chunk_size, const uint8_t *name,
+                                 int32_t name_len) {
+  name_len = std::min(name_len, 255);
+  std::vector<uint8_t> p = {0xFE};
+  put_be32(p, total_chunks);
+  put_be32(p, total_size);
+  p.push_back((uint8_t)((chunk_size >> 8) & 0xFF));
+  p.push_back((uint8_t)(chunk_size & 0xFF));
+  p.push_back((uint8_t)name_len);
+  p.insert(p.end(), name, name + name_len);
+  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
+  return p;
+}
+
+// buildDataChunkPayload (modem.js:694-714): [0xFF][seq:4][dataLen:2][data][CRC:4]
+std::vector<uint8_t> chunk_packet(const uint8_t *data, int32_t len, int32_t seq) {
+  std::vector<uint8_t> p = {0xFF};
+  put_be32(p, seq);
+  p.push_back((uint8_t)((len >> 8) & 0xFF));
+  p.push_back((uint8_t)(len & 0xFF));
   p.insert(p.end(), data, data + len);
   put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
   return p;
@@ -792,28 +828,135 @@ int64_t amod_tx_legacy(const amod_cfg *cfg, const uint8_t *data, int32_t len, co
 int64_t amod_tx_meta(const amod_cfg *cfg, int32_t total_chunks, int32_t total_size, int32_t chunk_size,
                      const uint8_t *name, int32_t name_len, float *out) {
   if (!validate(cfg) || name_len < 0) return AMOD_ERR_ARG;
-  name_len = std::min(name_len, 255);
-  std::vector<uint8_t> p = {0xFE};
-  put_be32(p, total_chunks);
-  put_be32(p, total_size);
-  p.push_back((uint8_t)((chunk_size >> 8) & 0xFF));
-  p.push_back((uint8_t)(chunk_size & 0xFF));
-  p.push_back((uint8_t)name_len);
-  p.insert(p.end(), name, name + name_len);
-  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
-  const int pre = rounded_silence(*cfg, cfg->cp_len >= 128 ? 0.5 : 0.3);
-  return assemble_frame(*cfg, p, pre, rounded_silence(*cfg, 0.02), out);
+  const auto p = meta_packet(total_chunks, total_size, chunk_size, name, name_len);
+  int32_t pre, post;
+  amod_tx_silence(cfg, AMOD_TX_META, &pre, &post);
+  return assemble_frame(*cfg, p, pre, post, out);
 }
 
 int64_t amod_tx_chunk(const amod_cfg *cfg, const uint8_t *data, int32_t len, int32_t seq, float *out) {
   if (!validate(cfg) || len < 0) return AMOD_ERR_ARG;
-  std::vector<uint8_t> p = {0xFF};
-  put_be32(p, seq);
-  p.push_back((uint8_t)((len >> 8) & 0xFF));
-  p.push_back((uint8_t)(len & 0xFF));
-  p.insert(p.end(), data, data + len);
-  put_be32(p, (int32_t)amod_crc32(p.data(), p.size()));
-  return assemble_frame(*cfg, p, rounded_silence(*cfg, 0.05), rounded_silence(*cfg, 0.02), out);
+  const auto p = chunk_packet(data, len, seq);
+  int32_t pre, post;
+  amod_tx_silence(cfg, AMOD_TX_CHUNK, &pre, &post);
+  return assemble_frame(*cfg, p, pre, post, out);
+}
+
+int amod_tx_silence(const amod_cfg *cfg, int32_t kind, int32_t *pre, int32_t *post) {
+  if (!validate(cfg) || !pre || !post) return AMOD_ERR_ARG;
+  switch (kind) {
+  case AMOD_TX_LEGACY: *pre = silence_len(*cfg, 0.3, 0.5); *post = silence_len(*cfg, 0.2, 0.5); break;
+  case AMOD_TX_META: *pre = rounded_silence(*cfg, cfg->cp_len >= 128 ? 0.5 : 0.3); *post = rounded_silence(*cfg, 0.02); break;
+  case AMOD_TX_CHUNK: *pre = rounded_silence(*cfg, 0.05); *post = rounded_silence(*cfg, 0.02); break;
+  default: return AMOD_ERR_ARG;
+  }
+  return AMOD_SUCCESS;
+}
+
+int64_t amod_packet_legacy(const uint8_t *data, int32_t len, const uint8_t *name, int32_t name_len, uint8_t *out) {
+  if (len < 0 || name_len < 0) return AMOD_ERR_ARG;
+  const auto p = legacy_packet(data, len, name, name_len);
+  if (out) std::copy(p.begin(), p.end(), out);
+  return (int64_t)p.size();
+}
+
+int64_t amod_packet_meta(int32_t total_chunks, int32_t total_size, int32_t chunk_size, const uint8_t *name,
+                         int32_t name_len, uint8_t *out) {
+  if (name_len < 0) return AMOD_ERR_ARG;
+  const auto p = meta_packet(total_chunks, total_size, chunk_size, name, name_len);
+  if (out) std::copy(p.begin(), p.end(), out);
+  return (int64_t)p.size();
+}
+
+int64_t amod_packet_chunk(const uint8_t *data, int32_t len, int32_t seq, uint8_t *out) {
+  if (len < 0) return AMOD_ERR_ARG;
+  const auto p = chunk_packet(data, len, seq);
+  if (out) std::copy(p.begin(), p.end(), out);
+  return (int64_t)p.size();
+}
+
+int64_t amod_tx_frame_samples(const amod_cfg *cfg, int64_t pkt_len, int32_t pre, int32_t post) {
+  if (!validate(cfg) || pkt_len < 0 || pre < 0 || post < 0) return AMOD_ERR_ARG;
+  const int64_t per_sym = (int64_t)amod_num_data_subs(cfg) * bps_of(cfg->modulation);
+  const int64_t nsym = (pkt_len * 8 * cfg->repetition + per_sym - 1) / per_sym;
+  return pre + (3 + nsym) * (int64_t)cfg->symbol_len + post;
+}
+
+int amod_tx_device(amod_ctx *ctx, const amod_cfg *cfg, const uint8_t *packets, const int64_t *pkt_off,
+                   const int32_t *pkt_len, const int32_t *pre, const int32_t *post, int32_t nframes, float *out,
+                   const int64_t *out_off, void *stream) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  if (!validate(cfg)) return fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  if (nframes < 0) return fail(ctx, "nframes < 0", AMOD_ERR_ARG);
+  if (nframes == 0) return AMOD_SUCCESS;
+  if (!packets || !pkt_off || !pkt_len || !pre || !post || !out || !out_off)
+    return fail(ctx, "null device pointer", AMOD_ERR_ARG);
+  HIP_TRY(hipSetDevice(ctx->device));
+  amod::DevCfg d;
+  const int rc = get_tables(ctx, cfg, d);
+  if (rc) return rc;
+  amod::DevTxWork w{packets, pkt_off, pkt_len, pre, post, out, out_off, nframes};
+  HIP_TRY(amod_launch_tx(d, w, stream ? (hipStream_t)stream : ctx->stream));
+  return AMOD_SUCCESS;
+}
+
+int64_t amod_tx_host(amod_ctx *ctx, const amod_cfg *cfg, const uint8_t *packets, int64_t nbytes,
+                     const int64_t *pkt_off, const int32_t *pkt_len, const int32_t *pre, const int32_t *post,
+                     int32_t nframes, float *out, int64_t *out_off) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  if (!validate(cfg)) return fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  if (nframes < 0 || nbytes < 0) return fail(ctx, "negative size", AMOD_ERR_ARG);
+  std::vector<int64_t> oo(nframes);
+  int64_t total = 0;
+  for (int32_t i = 0; i < nframes; ++i) {
+    if (pkt_off[i] < 0 || pkt_len[i] < 0 || pkt_off[i] + pkt_len[i] > nbytes)
+      return fail(ctx, "packet " + std::to_string(i) + " lies outside the packet buffer", AMOD_ERR_ARG);
+    const int64_t n = amod_tx_frame_samples(cfg, pkt_len[i], pre[i], post[i]);
+    if (n < 0) return fail(ctx, "invalid silence length", AMOD_ERR_ARG);
+    oo[i] = total;
+    total += n;
+  }
+  if (!out) return total;
+  if (out_off) std::copy(oo.begin(), oo.end(), out_off);
+  if (nframes == 0) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(ctx->tx_pkt.ensure((size_t)std::max<int64_t>(nbytes, 1)));
+  HIP_TRY(ctx->tx_meta.ensure((size_t)nframes * (2 * sizeof(int64_t) + 3 * sizeof(int32_t))));
+  HIP_TRY(ctx->tx_out.ensure(sizeof(float) * (size_t)total));
+  int64_t *d_po = (int64_t *)ctx->tx_meta.p, *d_oo = d_po + nframes;
+  int32_t *d_pl = (int32_t *)(d_oo + nframes), *d_pre = d_pl + nframes, *d_post = d_pre + nframes;
+  hipStream_t s = ctx->stream;
+  if (nbytes) HIP_TRY(hipMemcpyAsync(ctx->tx_pkt.p, packets, (size_t)nbytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_po, pkt_off, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_oo, oo.data(), sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_pl, pkt_len, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_pre, pre, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_post, post, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
+  amod::DevCfg d;
+  const int rc = get_tables(ctx, cfg, d);
+  if (rc) return rc;
+  amod::DevTxWork w{(const uint8_t *)ctx->tx_pkt.p, d_po, d_pl, d_pre, d_post, (float *)ctx->tx_out.p, d_oo, nframes};
+  HIP_TRY(amod_launch_tx(d, w, s));
+  HIP_TRY(hipMemcpyAsync(out, ctx->tx_out.p, sizeof(float) * (size_t)total, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return total;
+}
+
+int64_t amod_synth_legacy_packets(int32_t nframes, int32_t first, int32_t payload_len, const uint8_t *name,
+                                  int32_t name_len, uint8_t *out, int64_t *offsets, int32_t *lengths) {
+  if (nframes < 0 || payload_len < 0 || name_len < 0) return AMOD_ERR_ARG;
+  std::vector<uint8_t> data(payload_len);
+  const int64_t plen = (int64_t)legacy_packet(data.data(), payload_len, name, name_len).size();
+  if (!out) return plen * nframes;
+  for (int32_t i = 0; i < nframes; ++i) {
+    amod_synth_payload(0x9E3779B9u ^ (uint32_t)(first + i), payload_len, data.data());
+    const auto p = legacy_packet(data.data(), payload_len, name, name_len);
+    std::copy(p.begin(), p.end(), out + plen * i);
+    offsets[i] = plen * i;
+    lengths[i] = (int32_t)plen;
+  }
+  return plen * nframes;
 }
 
 int64_t amod_tx_test_signal(const amod_cfg *cfg, float *out) {

@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "audio samples/s demodulated + payload MB/s, QPSK 512-FFT, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-SAMPLES_PER_FRAME = 35874
+SAMPLES_PER_FRAME = 35874     # C2: QPSK 1 KB legacy frame
+SAMPLES_PER_FRAME_C3 = 30114  # C3: 16-QAM 1 KB legacy frame
 PAYLOAD = 1024
 
 
@@ -35,7 +36,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=10000, help="frames per GPU (C2 = 10,000)")
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2: 10k QPSK 1 KB frames per GPU (the metric's config); c3: 100k 16-QAM 1 KB frames")
+    ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0: the config's, C2 10,000 / C3 100,000)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="CPU-baseline sample (0 = auto, -1 = skip)")
     args = ap.parse_args()
 
@@ -58,27 +61,50 @@ def main():
         if world > 1:
             dist.barrier()
 
-    cfg = amodem.preset("standard", "QPSK", 1)
-    F = args.frames
-    # ---- synthetic input (host), uploaded once; the timed region is device-resident
-    x, offs, lens = amodem.synth_legacy_batch(cfg, F, payload_len=PAYLOAD, name="f.bin", first=rank * F,
-                                              threads=min(16, os.cpu_count() or 1))
-    assert (lens == SAMPLES_PER_FRAME).all()
+    C3 = args.config == "c3"
+    cfg = amodem.preset("standard", "QAM16" if C3 else "QPSK", 1)
+    F = args.frames if args.frames > 0 else (100000 if C3 else 10000)
+    spf = SAMPLES_PER_FRAME_C3 if C3 else SAMPLES_PER_FRAME
+    dm = amodem.Demodulator(local)
+    # ---- synthetic input, built on the GPU by k_tx (the reference transmitter, bit-exact)
+    # from the workload's packets; the timed region is device-resident
+    pk, po, pl = amodem.synth_legacy_packets(F, PAYLOAD, "f.bin", first=rank * F)
+    pre, post = amodem.tx_silence(cfg, L.TX_LEGACY)
+    offs = (np.arange(F, dtype=np.int64) * spf)
+    lens = np.full(F, spf, np.int32)
     nsamples = int(lens.sum())
-    t0 = time.perf_counter()
-    xs = torch.empty(len(x) + 16, dtype=torch.float32, device=dev)
-    xs[: len(x)].copy_(torch.from_numpy(x), non_blocking=False)
-    torch.cuda.synchronize(dev)
-    h2d_s = time.perf_counter() - t0
+    xs = torch.empty(nsamples + 16, dtype=torch.float32, device=dev)
+    d_pk = torch.from_numpy(pk).to(dev)
+    d_po, d_pl = torch.from_numpy(po).to(dev), torch.from_numpy(pl).to(dev)
+    d_pre = torch.full((F,), pre, dtype=torch.int32, device=dev)
+    d_post = torch.full((F,), post, dtype=torch.int32, device=dev)
     d_off = torch.from_numpy(offs).to(dev)
     d_len = torch.from_numpy(lens).to(dev)
-    stride = amodem.payload_stride(cfg, SAMPLES_PER_FRAME)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    tx_stream = torch.cuda.Stream(dev)  # a real (non-null) stream, so events and kernel share it
+
+    def tx():
+        dm.transmit_device(cfg, d_pk.data_ptr(), d_po.data_ptr(), d_pl.data_ptr(), d_pre.data_ptr(),
+                           d_post.data_ptr(), F, xs.data_ptr(), d_off.data_ptr(), stream=tx_stream.cuda_stream)
+
+    torch.cuda.synchronize(dev)
+    tx()
+    tx_stream.synchronize()
+    tx_ms = []
+    for _ in range(5):  # k_tx timed with HIP events on its launch stream
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(tx_stream)
+        tx()
+        e1.record(tx_stream)
+        e1.synchronize()
+        tx_ms.append(e0.elapsed_time(e1))
+    torch.cuda.synchronize(dev)
+    tx_avg_ms = sum(tx_ms) / len(tx_ms)
+    stride = amodem.payload_stride(cfg, spf)
     d_res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
     d_pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
 
-    dm = amodem.Demodulator(local)
-    dm.reserve(cfg, F, SAMPLES_PER_FRAME)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    dm.reserve(cfg, F, spf)
 
     def step():
         dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
@@ -98,7 +124,7 @@ def main():
 
     lib = L.load()
     # correlation-scan phase alone (k_corr_scan), measured before the timed region
-    scan = scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream)
+    scan = scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, spf)
     lib.amod_set_profiling(dm.ctx, 1)
     barrier()
     torch.cuda.synchronize(dev)
@@ -133,11 +159,19 @@ def main():
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
-            if tj.get("frames") == F and tj.get("samples_per_frame") == SAMPLES_PER_FRAME:
+            if tj.get("frames") == F and tj.get("samples_per_frame") == spf:
                 traffic = tj.get("hbm_bytes_per_launch")
-        cpu = None
+        mod = "QAM16" if C3 else "QPSK"
+        cpu, tx_cpu, d2h = None, None, None
         if args.cpu_frames >= 0:
-            cpu = cpu_baseline(x, offs, lens, args.cpu_frames)
+            # the CPU legs need the samples on the host: copy back the sample's frames
+            ncpu = args.cpu_frames if args.cpu_frames > 0 else min(F, 1000 * min(16, os.cpu_count() or 1))
+            t0 = time.perf_counter()
+            xh = xs[: ncpu * spf].cpu().numpy()
+            d2h = 4.0 * ncpu * spf / (time.perf_counter() - t0) / 1e9
+            cpu = cpu_baseline(xh, offs[:ncpu], lens[:ncpu], mod, "C3" if C3 else "C2")
+            tx_cpu = tx_cpu_baseline(amodem, cfg, min(ncpu, 4000), spf)
+        tx_bytes = 4.0 * nsamples + float(pl.sum())  # samples written + packet bytes read
         out = {
             "metric": METRIC,
             "value": value,
@@ -151,13 +185,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference-equivalent TX, xorshift32 payloads)",
-            "config": {"workload": "C2: 10k-frame QPSK batch demod per GPU (decodeReceivedSignal, legacy 1 KB frames)",
-                       "frames_per_gpu": F, "samples_per_frame": SAMPLES_PER_FRAME, "fft": 512,
-                       "modulation": "QPSK", "payload_bytes": PAYLOAD, "parallelism": f"frame-sharded x{world}"},
+            "config": {"workload": ("C3: 100k-frame 16-QAM batch demod per GPU" if C3 else
+                                    "C2: 10k-frame QPSK batch demod per GPU") +
+                                   " (decodeReceivedSignal, legacy 1 KB frames)",
+                       "frames_per_gpu": F, "samples_per_frame": spf, "fft": 512,
+                       "modulation": mod, "payload_bytes": PAYLOAD, "parallelism": f"frame-sharded x{world}"},
             "payload_MB_per_s": payload_mbps,
             "frames_ok": ok,
             "frames_exact_fallback": fallback,
-            "h2d_GBps_upload": 4.0 * len(x) / h2d_s / 1e9,
+            "d2h_GBps": d2h,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_decode_fast", "kernel_ms_avg": fast_avg_s * 1e3,
@@ -168,6 +204,12 @@ def main():
                               "kernel": "k_corr_scan", "kernel_ms_avg": scan, "achieved": algo_bytes / (scan / 1e3) / 1e9,
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": algo_bytes / (scan / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "tx": {"kernel": "k_tx", "what": "GPU transmitter (modulateOFDM + buildTransmitSignal, bit-exact) "
+                                             "building this run's input", "kernel_ms_avg": tx_avg_ms,
+                   "samples_per_s": nsamples / (tx_avg_ms / 1e3),
+                   "roofline": {"bound": "hbm", "achieved": tx_bytes / (tx_avg_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": tx_bytes / (tx_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                   "cpu_baseline": tx_cpu},
         }
         print(json.dumps(out), flush=True)
     dm.close()
@@ -175,7 +217,7 @@ def main():
         dist.destroy_process_group()
 
 
-def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, reps=20):
+def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, spf, reps=20):
     """Average duration of the correlation-scan phase alone on the same resident batch:
     k_corr_scan, the fast kernel's code instantiated to stop after the Schmidl-Cox
     decision (selected by AMOD_STOP_AFTER=1, read when a context builds its tables),
@@ -183,7 +225,7 @@ def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, st
     os.environ["AMOD_STOP_AFTER"] = "1"
     try:
         dm = amodem.Demodulator(local)
-        dm.reserve(cfg, F, SAMPLES_PER_FRAME)
+        dm.reserve(cfg, F, spf)
         run = lambda: dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
                                        d_res.data_ptr(), d_pay.data_ptr(), stride, stream=stream)
         for _ in range(10):  # clocks settle over the first launches
@@ -200,20 +242,36 @@ def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, st
         del os.environ["AMOD_STOP_AFTER"]
 
 
-def cpu_baseline(x, offs, lens, nframes):
+def cpu_baseline(x, offs, lens, mod, name):
     """The C restatement of the reference RX (oracle/, kind 'port') on this host's
-    cores over a bounded sample of the same frames."""
+    cores over a bounded sample of the same frames, repeated to ~1 s of wall time
+    (~16 s of CPU work on 16 threads)."""
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
-    if nframes <= 0:
-        nframes = min(len(offs), 1000 * threads)  # ~1 ms per frame per core: ~10-20 s of CPU work
     c = O.cfg("standard")
-    t, st, _ = O.bench_decode(c, x, offs[:nframes], lens[:nframes], "QPSK", 1, threads)
-    assert (st == 0).all()
-    samples = float(lens[:nframes].sum())
+    t, reps = 0.0, 0
+    while t < 1.0 and reps < 8:
+        dt, st, _ = O.bench_decode(c, x, offs, lens, mod, 1, threads)
+        assert (st == 0).all()
+        t += dt
+        reps += 1
+    samples = float(lens.sum()) * reps
     return {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{nframes} C2 frames ({int(samples)} samples), oracle/amodem_oracle.c, {threads} threads",
-            "payload_MB_per_s": PAYLOAD * nframes / t / 1e6, "seconds": t}
+            "sample": f"{len(offs)} {name} frames x {reps} passes ({int(samples)} samples), "
+                      f"oracle/amodem_oracle.c, {threads} threads",
+            "payload_MB_per_s": PAYLOAD * len(offs) * reps / t / 1e6, "seconds": t}
+
+
+def tx_cpu_baseline(amodem, cfg, nframes, spf):
+    """The host C++ builders (libamodem's amod_synth_legacy_batch, the same arithmetic
+    as the reference TX) on this host's cores over nframes frames."""
+    threads = min(16, os.cpu_count() or 1)
+    out = np.empty(nframes * spf, np.float32)
+    t0 = time.perf_counter()
+    amodem.synth_legacy_batch(cfg, nframes, payload_len=PAYLOAD, name="f.bin", threads=threads, out=out)
+    t = time.perf_counter() - t0
+    return {"value": nframes * spf / t, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{nframes} frames, libamodem host builders, {threads} threads", "seconds": t}
 
 
 if __name__ == "__main__":

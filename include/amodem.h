@@ -205,6 +205,35 @@ int64_t amod_tx_meta(const amod_cfg *cfg, int32_t total_chunks, int32_t total_si
                      const uint8_t *name, int32_t name_len, float *out);
 int64_t amod_tx_chunk(const amod_cfg *cfg, const uint8_t *data, int32_t len, int32_t seq, float *out);
 int64_t amod_tx_test_signal(const amod_cfg *cfg, float *out);
+/* ---- GPU transmitter (k_tx): modulateOFDM (modem.js:322-362) + buildTransmitSignal (498-555) /
+ * buildChunkOFDMFrame (718-756), bit-exact with the builders above.
+ * Packets are the bytes the reference frames: buildTransmitSignal's packet (amod_packet_legacy),
+ * buildMetadataPayload (amod_packet_meta, modem.js:666-692) or buildDataChunkPayload
+ * (amod_packet_chunk, 694-714); each returns its size (out NULL: sizing only).
+ * amod_tx_silence gives the builder's silence lengths; amod_tx_frame_samples the
+ * frame length. amod_tx_device: every pointer device memory; frame f's packet is
+ * packets[pkt_off[f], +pkt_len[f]), its samples go to out + out_off[f]; enqueued on
+ * `stream` (NULL = the context's stream). */
+#define AMOD_TX_LEGACY 0 /* buildTransmitSignal: 0.3 / 0.2 s silence (acoustic 0.5 / 0.5) */
+#define AMOD_TX_META 1   /* buildMetadataFrame (first frame): 0.3 s (acoustic 0.5) / 0.02 s */
+#define AMOD_TX_CHUNK 2  /* buildDataChunkFrame: 0.05 s / 0.02 s */
+int64_t amod_packet_legacy(const uint8_t *data, int32_t len, const uint8_t *name, int32_t name_len, uint8_t *out);
+int64_t amod_packet_meta(int32_t total_chunks, int32_t total_size, int32_t chunk_size, const uint8_t *name,
+                         int32_t name_len, uint8_t *out);
+int64_t amod_packet_chunk(const uint8_t *data, int32_t len, int32_t seq, uint8_t *out);
+int amod_tx_silence(const amod_cfg *cfg, int32_t kind, int32_t *pre, int32_t *post);
+int64_t amod_tx_frame_samples(const amod_cfg *cfg, int64_t pkt_len, int32_t pre, int32_t post);
+int amod_tx_device(amod_ctx *ctx, const amod_cfg *cfg, const uint8_t *packets, const int64_t *pkt_off,
+                   const int32_t *pkt_len, const int32_t *pre, const int32_t *post, int32_t nframes, float *out,
+                   const int64_t *out_off, void *stream);
+/* host staging of amod_tx_device: frames back to back in out (out_off filled, may be
+   NULL); returns the total sample count (out NULL: sizing only), < 0 on error */
+int64_t amod_tx_host(amod_ctx *ctx, const amod_cfg *cfg, const uint8_t *packets, int64_t nbytes,
+                     const int64_t *pkt_off, const int32_t *pkt_len, const int32_t *pre, const int32_t *post,
+                     int32_t nframes, float *out, int64_t *out_off);
+/* the synthetic legacy workload's packets (payload seed 0x9E3779B9 ^ (first+i)), back to back */
+int64_t amod_synth_legacy_packets(int32_t nframes, int32_t first, int32_t payload_len, const uint8_t *name,
+                                  int32_t name_len, uint8_t *out, int64_t *offsets, int32_t *lengths);
 /* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
 void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
 /* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),
