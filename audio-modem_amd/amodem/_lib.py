@@ -57,6 +57,15 @@ class Debug(C.Structure):
 
 assert C.sizeof(Result) == 96, C.sizeof(Result)
 
+
+class AsmState(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("total_chunks", "total_size", "chunk_size", "received", "crc_errors",
+                                          "complete", "has_bitmap", "frames_decoded", "frame_errors", "name_len",
+                                          "reserved")] + [("bitmap_len", C.c_int64)]
+
+
+ASM_RANGE_ERROR, ASM_TYPE_ERROR = -10, -11
+
 # (restype, argtypes) for every symbol the header declares
 _P = C.c_void_p
 SIGNATURES = {
@@ -95,6 +104,16 @@ SIGNATURES = {
     "amod_tx_frame_samples": (C.c_int64, [C.POINTER(Cfg), C.c_int64, C.c_int32, C.c_int32]),
     "amod_tx_device": (C.c_int, [_P, C.POINTER(Cfg), _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P]),
     "amod_tx_host": (C.c_int64, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P]),
+    "amod_asm_open": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    "amod_asm_close": (C.c_int, [_P]),
+    "amod_asm_metadata": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
+    "amod_asm_chunk": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_int32, C.c_int32]),
+    "amod_asm_feed": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32]),
+    "amod_asm_state": (C.c_int, [_P, C.POINTER(AsmState)]),
+    "amod_asm_bitmap": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_asm_name": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_asm_missing": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_asm_file": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),

@@ -362,3 +362,98 @@ def synth_legacy_batch(cfg: L.Cfg, nframes: int, payload_len: int = 1024, name: 
     lib.amod_synth_legacy_batch(C.byref(cfg), nframes, first, payload_len, nm, len(nm), out.ctypes.data,
                                 offs.ctypes.data, lens.ctypes.data, threads)
     return out, offs, lens
+
+
+# ---------------------------------------------------------------- assembly --
+class AssemblerError(Exception):
+    """An error the reference's ChunkAssembler throws (name: 'RangeError' / 'TypeError')."""
+
+    def __init__(self, name: str):
+        super().__init__(name)
+        self.name = name
+
+
+def _asm_check(rc):
+    if rc == L.ASM_RANGE_ERROR:
+        raise AssemblerError("RangeError")
+    if rc == L.ASM_TYPE_ERROR:
+        raise AssemblerError("TypeError")
+    if rc < 0:
+        raise RuntimeError(f"libamodem assembler error {rc}")
+    return rc
+
+
+class ChunkAssembler:
+    """app.js ChunkAssembler (597-704) over libamodem's host assembler: same method
+    names (snake_case), same state and the same thrown errors. directory: keep the
+    chunks as files there (the IndexedDB store's stand-in) instead of in memory."""
+
+    def __init__(self, directory: str | None = None):
+        self._L = L.load()
+        h = C.c_void_p()
+        _asm_check(self._L.amod_asm_open(directory.encode() if directory else None, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            self._L.amod_asm_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def handle_metadata_frame(self, total_chunks: int, total_file_size: int, chunk_size: int, file_name: bytes):
+        name = bytes(file_name)
+        _asm_check(self._L.amod_asm_metadata(self._h, int(total_chunks), int(total_file_size), int(chunk_size), name,
+                                             len(name)))
+
+    def handle_data_chunk(self, seq_num: int, data: bytes, crc_valid: bool) -> bool:
+        data = bytes(data)
+        return _asm_check(self._L.amod_asm_chunk(self._h, int(seq_num), data, len(data), int(bool(crc_valid)))) == 1
+
+    def feed(self, records: np.ndarray, payload: np.ndarray):
+        """StreamingReceiver's dispatch over decodeChunkFrame results (RESULT_DTYPE
+        records + [n, stride] payload slots), in order."""
+        records = np.ascontiguousarray(records)
+        payload = np.ascontiguousarray(payload, np.uint8)
+        _asm_check(self._L.amod_asm_feed(self._h, records.ctypes.data, payload.ctypes.data, payload.shape[1],
+                                         len(records)))
+
+    def state(self) -> dict:
+        s = L.AsmState()
+        _asm_check(self._L.amod_asm_state(self._h, C.byref(s)))
+        return {n: getattr(s, n) for n, _ in L.AsmState._fields_ if n != "reserved"}
+
+    def bitmap(self):
+        n = self._L.amod_asm_bitmap(self._h, None, 0)
+        out = np.zeros(max(n, 1), np.uint8)
+        self._L.amod_asm_bitmap(self._h, out.ctypes.data, n)
+        return out[:n]
+
+    def file_name(self) -> bytes:
+        n = self._L.amod_asm_name(self._h, None, 0)
+        out = np.zeros(max(n, 1), np.uint8)
+        self._L.amod_asm_name(self._h, out.ctypes.data, n)
+        return out[:n].tobytes()
+
+    def is_complete(self) -> bool:
+        return bool(self.state()["complete"])
+
+    def is_received(self, seq: int) -> bool:
+        b = self.bitmap()
+        return 0 <= seq and (seq >> 3) < len(b) and bool(b[seq >> 3] & (1 << (seq & 7)))
+
+    def get_missing_chunks(self):
+        n = self._L.amod_asm_missing(self._h, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        self._L.amod_asm_missing(self._h, out.ctypes.data, n)
+        return out[:n].tolist()
+
+    def assemble_file(self) -> bytes:
+        n = _asm_check(self._L.amod_asm_file(self._h, None, 0))
+        out = np.zeros(max(n, 1), np.uint8)
+        _asm_check(self._L.amod_asm_file(self._h, out.ctypes.data, n))
+        return out[:n].tobytes()

@@ -1,0 +1,218 @@
+// assembler.cpp — the chunk protocol's receive-side bookkeeping (host C++).
+//
+// Restates app.js ChunkAssembler (597-704) and the result dispatch of
+// StreamingReceiver._demodulateFrame (926-961) over amod_result records: received
+// bitmap, duplicate suppression, CRC-error count, completion test, missing list and
+// assembleFile's offsets. The IndexedDB object store becomes an in-memory map, or one
+// file per chunk under a directory. The reference's quirks are kept, because a
+// drop-in must behave the same on the same inputs:
+//   * a metadata frame with totalChunks <= -8 raises RangeError (new Uint8Array of a
+//     negative length) after the header fields were assigned; the bitmap stays;
+//   * a negative seqNum below totalChunks is never seen as a duplicate (typed-array
+//     reads past the ends are undefined, writes are dropped), so it counts every time;
+//   * assembleFile raises TypeError before any metadata (no store), RangeError for a
+//     negative totalFileSize or a chunk that runs past the end of the file.
+// Pinned by tests/golden/assembler.json (the reference class run under Node).
+#include <stdint.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "amodem.h"
+
+struct amod_assembler {
+  int32_t total_chunks = 0, total_size = 0, chunk_size = 0;
+  std::vector<uint8_t> name;
+  bool has_bitmap = false;
+  std::vector<uint8_t> bitmap;
+  int32_t received = 0, crc_errors = 0;
+  bool has_store = false;                          // IndexedDB opened by a metadata frame
+  std::map<int32_t, std::vector<uint8_t>> chunks;  // seqNum -> data (memory store)
+  std::string dir;                                 // file store when not empty
+  int32_t frames_decoded = 0, frame_errors = 0;    // StreamingReceiver counters
+
+  std::string path(int32_t seq) const { return dir + "/chunk_" + std::to_string(seq) + ".bin"; }
+  void clear_store() {
+    if (!dir.empty())
+      for (const auto &kv : chunks) remove(path(kv.first).c_str());
+    chunks.clear();
+  }
+  bool put(int32_t seq, const uint8_t *d, int32_t n) {
+    if (dir.empty()) {
+      chunks[seq].assign(d, d + n);
+      return true;
+    }
+    FILE *f = fopen(path(seq).c_str(), "wb");
+    if (!f) return false;
+    const bool ok = n == 0 || fwrite(d, 1, (size_t)n, f) == (size_t)n;
+    fclose(f);
+    chunks[seq].clear(); // key only; bytes live in the file
+    return ok;
+  }
+  bool get(int32_t seq, std::vector<uint8_t> &out) const {
+    auto it = chunks.find(seq);
+    if (it == chunks.end()) return false;
+    if (dir.empty()) {
+      out = it->second;
+      return true;
+    }
+    FILE *f = fopen(path(seq).c_str(), "rb");
+    if (!f) return false;
+    out.clear();
+    uint8_t buf[65536];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + k);
+    fclose(f);
+    return true;
+  }
+  bool is_received(int64_t seq) const {
+    if (!has_bitmap || seq < 0 || (seq >> 3) >= (int64_t)bitmap.size()) return false;
+    return bitmap[seq >> 3] & (1u << (seq & 7));
+  }
+};
+
+extern "C" {
+
+int amod_asm_open(const char *dir, amod_assembler **out) {
+  if (!out) return AMOD_ERR_ARG;
+  auto *a = new (std::nothrow) amod_assembler();
+  if (!a) return AMOD_ERR_NOMEM;
+  if (dir && *dir) a->dir = dir;
+  *out = a;
+  return AMOD_SUCCESS;
+}
+
+int amod_asm_close(amod_assembler *a) {
+  delete a;
+  return AMOD_SUCCESS;
+}
+
+// handleMetadataFrame (app.js:610-626)
+int amod_asm_metadata(amod_assembler *a, int32_t total_chunks, int32_t total_size, int32_t chunk_size,
+                      const uint8_t *name, int32_t name_len) {
+  if (!a || name_len < 0) return AMOD_ERR_ARG;
+  a->total_chunks = total_chunks;
+  a->total_size = total_size;
+  a->chunk_size = chunk_size;
+  a->name.assign(name, name + name_len);
+  // new Uint8Array(Math.ceil(totalChunks / 8)): -7..-1 give -0 = length 0
+  const int64_t len = total_chunks >= 0 ? ((int64_t)total_chunks + 7) / 8 : -((-(int64_t)total_chunks) / 8);
+  if (len < 0) return AMOD_ASM_RANGE_ERROR;
+  a->bitmap.assign((size_t)len, 0);
+  a->has_bitmap = true;
+  a->received = 0;
+  a->crc_errors = 0;
+  a->clear_store();
+  a->has_store = true;
+  return AMOD_SUCCESS;
+}
+
+// handleDataChunk (app.js:628-648); returns 1 if the chunk was stored, 0 if ignored
+int amod_asm_chunk(amod_assembler *a, int32_t seq, const uint8_t *data, int32_t len, int32_t crc_valid) {
+  if (!a || len < 0) return AMOD_ERR_ARG;
+  if (!a->has_bitmap) return 0;
+  if (seq >= a->total_chunks) return 0;
+  if (!crc_valid) {
+    ++a->crc_errors;
+    return 0;
+  }
+  const int64_t byte = (int64_t)seq >> 3;
+  const int bit = seq & 7;
+  const bool inside = byte >= 0 && byte < (int64_t)a->bitmap.size();
+  if (inside && (a->bitmap[byte] & (1u << bit))) return 0; // duplicate
+  if (inside) a->bitmap[byte] |= (uint8_t)(1u << bit);
+  ++a->received;
+  if (!a->put(seq, data, len)) return AMOD_ERR_NOMEM;
+  return 1;
+}
+
+// StreamingReceiver._demodulateFrame's dispatch (app.js:926-961) over n decode results
+int amod_asm_feed(amod_assembler *a, const amod_result *res, const uint8_t *payload, int64_t stride, int32_t n) {
+  if (!a || n < 0 || (n && (!res || !payload))) return AMOD_ERR_ARG;
+  for (int32_t i = 0; i < n; ++i) {
+    const amod_result &r = res[i];
+    const uint8_t *slot = payload + (int64_t)i * stride;
+    if (r.status != AMOD_OK) { ++a->frame_errors; continue; }
+    ++a->frames_decoded;
+    if (r.frame_type == 0xFE) {
+      if (r.crc_valid) {
+        if (amod_asm_metadata(a, r.total_chunks, r.total_size, r.chunk_size, slot + r.name_off, r.name_len) ==
+            AMOD_ASM_RANGE_ERROR)
+          ++a->frame_errors; // the thrown RangeError lands in the receiver's catch
+      } else {
+        ++a->frame_errors;
+      }
+    } else if (r.frame_type == 0xFF) {
+      const int rc = amod_asm_chunk(a, r.seq_num, slot + r.data_off, r.data_len, r.crc_valid);
+      if (rc < 0) return rc;
+    }
+  }
+  return AMOD_SUCCESS;
+}
+
+int amod_asm_state(const amod_assembler *a, amod_asm_info *out) {
+  if (!a || !out) return AMOD_ERR_ARG;
+  out->total_chunks = a->total_chunks;
+  out->total_size = a->total_size;
+  out->chunk_size = a->chunk_size;
+  out->received = a->received;
+  out->crc_errors = a->crc_errors;
+  out->complete = a->received == a->total_chunks; // isComplete (app.js:655-657)
+  out->has_bitmap = a->has_bitmap;
+  out->bitmap_len = a->has_bitmap ? (int64_t)a->bitmap.size() : -1;
+  out->frames_decoded = a->frames_decoded;
+  out->frame_errors = a->frame_errors;
+  out->name_len = (int32_t)a->name.size();
+  out->reserved = 0;
+  return AMOD_SUCCESS;
+}
+
+int64_t amod_asm_bitmap(const amod_assembler *a, uint8_t *out, int64_t cap) {
+  if (!a) return AMOD_ERR_ARG;
+  const int64_t n = (int64_t)a->bitmap.size();
+  if (out) std::copy(a->bitmap.begin(), a->bitmap.begin() + std::min(n, std::max<int64_t>(cap, 0)), out);
+  return n;
+}
+
+int64_t amod_asm_name(const amod_assembler *a, uint8_t *out, int64_t cap) {
+  if (!a) return AMOD_ERR_ARG;
+  const int64_t n = (int64_t)a->name.size();
+  if (out) std::copy(a->name.begin(), a->name.begin() + std::min(n, std::max<int64_t>(cap, 0)), out);
+  return n;
+}
+
+// getMissingChunks (app.js:659-665): count, first min(count, cap) indices in out
+int64_t amod_asm_missing(const amod_assembler *a, int32_t *out, int64_t cap) {
+  if (!a) return AMOD_ERR_ARG;
+  int64_t k = 0;
+  for (int64_t i = 0; i < a->total_chunks; ++i)
+    if (!a->is_received(i)) {
+      if (out && k < cap) out[k] = (int32_t)i;
+      ++k;
+    }
+  return k;
+}
+
+// assembleFile (app.js:667-686): the file's size (out NULL: sizing), or an error
+int64_t amod_asm_file(const amod_assembler *a, uint8_t *out, int64_t cap) {
+  if (!a) return AMOD_ERR_ARG;
+  if (!a->has_store) return AMOD_ASM_TYPE_ERROR;
+  if (a->total_size < 0) return AMOD_ASM_RANGE_ERROR;
+  const int64_t size = a->total_size;
+  if (!out) return size;
+  if (cap < size) return AMOD_ERR_ARG;
+  std::fill(out, out + size, 0);
+  std::vector<uint8_t> d;
+  for (int64_t i = 0; i < a->total_chunks; ++i) {
+    if (!a->get((int32_t)i, d)) continue;
+    const int64_t off = i * (int64_t)a->chunk_size;
+    if (off + (int64_t)d.size() > size) return AMOD_ASM_RANGE_ERROR; // Uint8Array.set past the end
+    std::copy(d.begin(), d.end(), out + off);
+  }
+  return size;
+}
+
+} // extern "C"

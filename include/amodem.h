@@ -234,6 +234,34 @@ int64_t amod_tx_host(amod_ctx *ctx, const amod_cfg *cfg, const uint8_t *packets,
 /* the synthetic legacy workload's packets (payload seed 0x9E3779B9 ^ (first+i)), back to back */
 int64_t amod_synth_legacy_packets(int32_t nframes, int32_t first, int32_t payload_len, const uint8_t *name,
                                   int32_t name_len, uint8_t *out, int64_t *offsets, int32_t *lengths);
+/* ---- chunk assembly (host): app.js ChunkAssembler (597-704) and the result dispatch of
+ * StreamingReceiver._demodulateFrame (926-961), with the reference's quirks (assembler.cpp).
+ * dir != NULL keeps chunks as files under dir (the IndexedDB store's stand-in), else memory.
+ * amod_asm_chunk returns 1 if stored, 0 if ignored; amod_asm_file returns the file size
+ * (out NULL: sizing) or one of the errors the reference throws: */
+#define AMOD_ASM_RANGE_ERROR (-10) /* RangeError: negative sizes, a chunk past the file end */
+#define AMOD_ASM_TYPE_ERROR (-11)  /* TypeError: assembleFile before any metadata frame     */
+typedef struct amod_assembler amod_assembler;
+typedef struct amod_asm_info {
+  int32_t total_chunks, total_size, chunk_size; /* last metadata frame                     */
+  int32_t received, crc_errors, complete;       /* receivedCount, crcErrors, isComplete()  */
+  int32_t has_bitmap;                           /* a metadata frame created the bitmap     */
+  int32_t frames_decoded, frame_errors;         /* StreamingReceiver counters (feed only)  */
+  int32_t name_len, reserved;
+  int64_t bitmap_len;                           /* -1 without bitmap                       */
+} amod_asm_info;
+int amod_asm_open(const char *dir, amod_assembler **out);
+int amod_asm_close(amod_assembler *a);
+int amod_asm_metadata(amod_assembler *a, int32_t total_chunks, int32_t total_size, int32_t chunk_size,
+                      const uint8_t *name, int32_t name_len);
+int amod_asm_chunk(amod_assembler *a, int32_t seq, const uint8_t *data, int32_t len, int32_t crc_valid);
+int amod_asm_feed(amod_assembler *a, const amod_result *res, const uint8_t *payload, int64_t stride, int32_t n);
+int amod_asm_state(const amod_assembler *a, amod_asm_info *out);
+int64_t amod_asm_bitmap(const amod_assembler *a, uint8_t *out, int64_t cap);
+int64_t amod_asm_name(const amod_assembler *a, uint8_t *out, int64_t cap);
+int64_t amod_asm_missing(const amod_assembler *a, int32_t *out, int64_t cap);
+int64_t amod_asm_file(const amod_assembler *a, uint8_t *out, int64_t cap);
+
 /* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
 void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
 /* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),
