@@ -1,6 +1,6 @@
 """amodem — MI355X-native OFDM demodulator (host mirror of modem.js over libamodem)."""
 from . import _lib
-from .modem import (AssemblerError, ChunkAssembler, FRAME_DATA, FRAME_META, OFDM, OFDM_CONFIGS, RESULT_DTYPE, Demodulator, build_data_chunk_frame,
+from .modem import (STREAM_FRAME_DTYPE, AssemblerError, ChunkAssembler, FRAME_DATA, FRAME_META, OFDM, OFDM_CONFIGS, RESULT_DTYPE, Demodulator, build_data_chunk_frame,
                     build_metadata_frame, build_transmit_signal, crc32, estimate_frame_samples,
                     generate_preamble_symbol1, generate_test_signal, make_cfg, packet_chunk, packet_legacy,
                     packet_meta, payload_stride, preset, set_ofdm_config, synth_legacy_batch, synth_legacy_packets,

@@ -65,6 +65,18 @@ class AsmState(C.Structure):
 
 
 ASM_RANGE_ERROR, ASM_TYPE_ERROR = -10, -11
+E_STREAM_LOST = 101
+
+
+class StreamFrame(C.Structure):
+    _fields_ = [("pos", C.c_int64), ("end", C.c_int64), ("window_len", C.c_int32), ("reserved", C.c_int32),
+                ("result", Result)]
+
+
+class StreamStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("nframes", "nrefine_fail", "frames_decoded", "frame_errors", "final_state",
+                                          "final_scan_pos", "ema_chunks_fixed", "fine_host_positions")] + \
+               [(n, C.c_double) for n in ("t_ema_ms", "t_fine_ms", "t_decode_ms", "t_host_ms", "t_total_ms")]
 
 # (restype, argtypes) for every symbol the header declares
 _P = C.c_void_p
@@ -114,6 +126,8 @@ SIGNATURES = {
     "amod_asm_name": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_asm_missing": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_asm_file": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_stream_receive": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, C.c_int64, C.POINTER(C.c_int64),
+                                      _P, C.c_int64, C.POINTER(StreamStats)]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),

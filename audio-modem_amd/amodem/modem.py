@@ -128,6 +128,11 @@ def to_reference(rec, slot: bytes, via_legacy: bool) -> dict:
     return out
 
 
+STREAM_FRAME_DTYPE = np.dtype([("pos", np.int64), ("end", np.int64), ("window_len", np.int32),
+                               ("reserved", np.int32), ("result", RESULT_DTYPE)])
+assert STREAM_FRAME_DTYPE.itemsize == C.sizeof(L.StreamFrame)
+
+
 class Demodulator:
     """One HIP device context (stream + workspace) of libamodem."""
 
@@ -204,6 +209,24 @@ class Demodulator:
 
     def synchronize(self):
         L.check(self._L.amod_synchronize(self.ctx), self.ctx)
+
+    # ------------------------------------------------------------ streaming
+    def stream_receive(self, cfg: L.Cfg, samples: np.ndarray, assembler: "ChunkAssembler | None" = None,
+                       max_frames: int = 1 << 20):
+        """app.js StreamingReceiver over a recorded stream (4096-sample blocks): returns
+        (frames: STREAM_FRAME_DTYPE records, refine_fail: list of positions, stats: dict).
+        Decoded chunks go to `assembler` (a private one if None)."""
+        x = np.ascontiguousarray(samples, np.float32)
+        frames = np.zeros(max_frames, STREAM_FRAME_DTYPE)
+        rf = np.zeros(1 << 16, np.int64)
+        n = C.c_int64()
+        st = L.StreamStats()
+        with self._lock:
+            L.check(self._L.amod_stream_receive(self.ctx, C.byref(cfg), x.ctypes.data, len(x),
+                                                assembler._h if assembler is not None else None, frames.ctypes.data,
+                                                max_frames, C.byref(n), rf.ctypes.data, len(rf), C.byref(st)), self.ctx)
+        stats = {k: getattr(st, k) for k, _ in L.StreamStats._fields_}
+        return frames[:min(n.value, max_frames)], rf[:min(st.nrefine_fail, len(rf))].tolist(), stats
 
     # ------------------------------------------------------------ transmitter
     def transmit_device(self, cfg: L.Cfg, packets_ptr: int, pkt_off_ptr: int, pkt_len_ptr: int, pre_ptr: int,

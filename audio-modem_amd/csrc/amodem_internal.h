@@ -378,4 +378,17 @@ hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hip
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
 int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap); // dynamic LDS of one fast-kernel workgroup
+// streaming receiver pieces (k_stream.hip)
+hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, float *y, double *warm, double *end,
+                           unsigned long long *fixed, hipStream_t s);
+hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, uint8_t *hot, hipStream_t s);
+hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, const int64_t *first,
+                            const int64_t *base, const int64_t *count, int nranges, int64_t maxcount, double2 *out,
+                            hipStream_t s);
+hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,
+                              int nwin, float *out, hipStream_t s);
+// runtime.cpp: a context's device and stream for the host-side orchestrators
+int amod_ctx_device(const amod_ctx *ctx);
+hipStream_t amod_ctx_stream(const amod_ctx *ctx);
+int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code);
 }

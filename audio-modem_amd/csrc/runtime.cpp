@@ -587,6 +587,10 @@ extern "C" {
 
 int amod_abi_version(void) { return AMOD_ABI_VERSION; }
 
+int amod_ctx_device(const amod_ctx *ctx) { return ctx ? ctx->device : 0; }
+hipStream_t amod_ctx_stream(const amod_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
+int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code) { return fail(ctx, msg, code); }
+
 int amod_open(int device, amod_ctx **out) {
   if (!out) return fail(nullptr, "null out", AMOD_ERR_ARG);
   int n = 0;

@@ -1,0 +1,466 @@
+// stream.cpp — app.js StreamingReceiver (706-998) over a whole recorded stream.
+//
+// The reference runs per 4096-sample audio block (ScriptProcessor, app.js:1103):
+// EMA DC removal, ring buffer, then one step of its state machine (scan for a
+// Schmidl-Cox preamble / refine by cross-correlation / collect / demodulate with
+// decodeChunkFrame + ChunkAssembler dispatch). Here:
+//
+//   GPU   k_ema       the DC removal, bit-exact (k_stream.hip)
+//         k_sc_screen hot 32-sample blocks (metric >= 0.25 at the block start)
+//         k_fine      the refinement's cross-correlation sums, in the reference's
+//                     order, for every position within 448 samples of a hot block
+//         k_window    per-frame peak normalisation, then k_decode_fast/_exact in chunk
+//                     mode over all windows of a batch
+//   host  the state machine itself, replayed exactly in IEEE double: the sliding
+//         Schmidl-Cox recurrence with its block-boundary behaviour (the state left at
+//         scanEnd is re-read one position later, app.js:782-847), the 0.5 threshold,
+//         the 0.7 x best commit and the end-of-block commit, refine windows clipped to
+//         the ring buffer, frame windows from estimateFrameSamples(chunkSize + 11 | 280).
+//         The fine metric comes from k_fine's exact sums (host fallback for a position
+//         outside the precomputed ranges); frames are decoded in batches on the GPU,
+//         and a batch is rolled back to the frame after which a metadata result
+//         changed the window length (metaReceived / chunkSize, app.js:889-896).
+// Decisions are the reference's own arithmetic, so outcomes match it exactly; pinned
+// by tests/golden/stream.json (the reference receiver run on recipe streams).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "amodem_internal.h"
+
+namespace {
+
+constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
+constexpr int64_t kEmaChunk = 65536;  // k_ema chunk per lane
+constexpr int64_t kEmaWarm = 65536;   // warm-up run before each chunk
+constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
+enum { IDLE = 0, DETECTED = 1, COLLECTING = 2 };
+
+struct DBuf {
+  void *p = nullptr;
+  ~DBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t n) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    return hipMalloc(&p, std::max<size_t>(n, 256));
+  }
+  template <typename T> T *as() const { return (T *)p; }
+};
+
+#define S_TRY(expr)                                                                     \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return amod_ctx_fail(ctx, hipGetErrorString(e_), AMOD_ERR_HIP); \
+  } while (0)
+
+// receiver state that a rollback restores (everything the next block depends on)
+struct RxState {
+  int64_t block = 0;             // next block to process
+  int state = IDLE;
+  bool ac_init = false;
+  int64_t ac_pos = 0;
+  double ac_p = 0, ac_ra = 0, ac_rb = 0;
+  int64_t pre_pos = -1, frame_end = -1;
+  bool meta_received = false;
+  int32_t chunk_size = 0;        // assembler.chunkSize as the window length sees it
+};
+
+struct FineTable {
+  std::vector<int64_t> first, base, count;
+  std::vector<double> corr_se; // pairs
+  bool lookup(int64_t d, double &corr, double &se) const {
+    auto it = std::upper_bound(first.begin(), first.end(), d);
+    if (it == first.begin()) return false;
+    const size_t r = (size_t)(it - first.begin()) - 1;
+    if (d >= first[r] + count[r]) return false;
+    const int64_t k = base[r] + (d - first[r]);
+    corr = corr_se[2 * k];
+    se = corr_se[2 * k + 1];
+    return true;
+  }
+};
+
+struct Receiver {
+  const amod_cfg *cfg;
+  int64_t n = 0, npad = 0, cap = 0;
+  const float *y = nullptr; // cleaned stream (host)
+  std::vector<float> pre1;
+  double pre1_energy = 0;
+  const FineTable *fine = nullptr;
+  RxState st;
+  std::vector<int64_t> refine_fail;
+  int64_t fine_host = 0; // positions the host had to correlate itself
+
+  double S(int64_t i) const { return (i >= 0 && i < npad) ? (double)y[i] : 0.0; }
+  int64_t tw() const { return (st.block + 1) * kBlock; } // totalWritten after this block's write
+
+  // _scanForPreamble (app.js:775-847)
+  void scan() {
+    const int64_t half = 256, total = tw(), oldest = total - cap;
+    if (st.ac_pos < oldest + 2 * half) { st.ac_pos = std::max<int64_t>(oldest + 2 * half, 0); st.ac_init = false; }
+    const int64_t scan_end = total - 2 * half;
+    if (st.ac_pos > scan_end) return;
+    if (!st.ac_init) {
+      st.ac_p = 0; st.ac_ra = 0; st.ac_rb = 0;
+      for (int64_t m = 0; m < half; ++m) {
+        const double a = S(st.ac_pos + m), b = S(st.ac_pos + m + half);
+        st.ac_p += a * b; st.ac_ra += a * a; st.ac_rb += b * b;
+      }
+      st.ac_init = true;
+    }
+    const double min_e = 0.001;
+    double best = 0;
+    int64_t best_pos = -1;
+    while (st.ac_pos <= scan_end) {
+      if (st.ac_ra > min_e && st.ac_rb > min_e) {
+        const double metric = (st.ac_p * st.ac_p) / (st.ac_ra * st.ac_rb);
+        if (metric > 0.5 && metric > best) { best = metric; best_pos = st.ac_pos; }
+      }
+      if (st.ac_pos < scan_end) {
+        const double a_out = S(st.ac_pos), mid = S(st.ac_pos + half), b_in = S(st.ac_pos + 2 * half);
+        st.ac_p += mid * b_in - a_out * mid;
+        st.ac_ra += mid * mid - a_out * a_out;
+        st.ac_rb += b_in * b_in - mid * mid;
+      }
+      st.ac_pos++;
+      if (best > 0.5 && best_pos >= 0 && st.ac_ra > min_e && st.ac_rb > min_e) {
+        const double cur = (st.ac_p * st.ac_p) / (st.ac_ra * st.ac_rb);
+        if (cur < best * 0.7) { st.pre_pos = best_pos; st.state = DETECTED; return; }
+      }
+    }
+    if (best > 0.5 && best_pos >= 0) { st.pre_pos = best_pos; st.state = DETECTED; }
+  }
+
+  // _refineAndCollect (app.js:849-898)
+  void refine() {
+    const int64_t plen = cfg->symbol_len, radius = 3 * (int64_t)cfg->cp_len, total = tw();
+    if (total < st.pre_pos + plen + radius) return;
+    const int64_t fs = std::max(total - cap, st.pre_pos - radius), fe = std::min(total - plen, st.pre_pos + radius);
+    double best = -INFINITY;
+    int64_t best_pos = st.pre_pos;
+    for (int64_t d = fs; d <= fe; ++d) {
+      double corr = 0, se = 0;
+      if (!fine || !fine->lookup(d, corr, se)) {
+        for (int64_t i = 0; i < plen; ++i) {
+          const double s = S(d + i);
+          corr += s * (double)pre1[i];
+          se += s * s;
+        }
+        ++fine_host;
+      }
+      const double denom = std::sqrt(se * pre1_energy);
+      if (denom > 0.001) {
+        const double metric = corr / denom;
+        if (metric > best) { best = metric; best_pos = d; }
+      }
+    }
+    if (best < 0.1) {
+      refine_fail.push_back(st.pre_pos);
+      st.state = IDLE;
+      st.ac_init = false;
+      return;
+    }
+    st.pre_pos = best_pos;
+    const int32_t max_payload = st.meta_received ? (st.chunk_size ? st.chunk_size : 4096) + 11 : 280;
+    st.frame_end = st.pre_pos + amod_estimate_frame_samples(cfg, max_payload);
+    st.state = COLLECTING;
+  }
+
+  // _resetToIdle (app.js:974-981)
+  void reset() {
+    st.ac_pos = st.frame_end ? st.frame_end : st.pre_pos + cfg->symbol_len;
+    st.ac_init = false;
+    st.pre_pos = -1;
+    st.frame_end = -1;
+    st.state = IDLE;
+  }
+};
+
+} // namespace
+
+extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
+                                   amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                                   int64_t *nframes_out, int64_t *refine_fail, int64_t max_refine_fail,
+                                   amod_stream_stats *stats) {
+  using clk = std::chrono::steady_clock;
+  const auto t_start = clk::now();
+  if (!ctx || !cfg || n < 0 || (n && !samples) || (max_frames > 0 && !frames) || !nframes_out)
+    return amod_ctx_fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  S_TRY(hipSetDevice(amod_ctx_device(ctx)));
+  hipStream_t s = amod_ctx_stream(ctx);
+  const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
+  amod_stream_stats stt{};
+  // ---- GPU: DC removal (exact), screening, fine sums
+  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot;
+  const int64_t nchunks = std::max<int64_t>(1, (npad + kEmaChunk - 1) / kEmaChunk);
+  S_TRY(d_x.alloc(sizeof(float) * (size_t)npad + 64));
+  S_TRY(d_y.alloc(sizeof(float) * (size_t)npad + 64));
+  S_TRY(d_warm.alloc(sizeof(double) * nchunks));
+  S_TRY(d_end.alloc(sizeof(double) * nchunks));
+  S_TRY(d_fixed.alloc(8));
+  S_TRY(d_hot.alloc((size_t)(npad / 32 + 1)));
+  if (npad) {
+    S_TRY(hipMemsetAsync(d_x.p, 0, sizeof(float) * (size_t)npad, s));
+    if (n) S_TRY(hipMemcpyAsync(d_x.p, samples, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
+  }
+  hipEvent_t ev[4];
+  for (auto &e : ev) S_TRY(hipEventCreate(&e));
+  S_TRY(hipEventRecord(ev[0], s));
+  S_TRY(amod_launch_ema(d_x.as<float>(), npad, kEmaChunk, kEmaWarm, d_y.as<float>(), d_warm.as<double>(),
+                        d_end.as<double>(), d_fixed.as<unsigned long long>(), s));
+  S_TRY(hipEventRecord(ev[1], s));
+  S_TRY(amod_launch_sc_screen(d_y.as<float>(), npad, 0.25f, d_hot.as<uint8_t>(), s));
+  std::vector<uint8_t> hot((size_t)(npad / 32));
+  if (!hot.empty()) S_TRY(hipMemcpyAsync(hot.data(), d_hot.p, hot.size(), hipMemcpyDeviceToHost, s));
+  S_TRY(hipStreamSynchronize(s));
+  unsigned long long fixed = 0;
+  S_TRY(hipMemcpy(&fixed, d_fixed.p, 8, hipMemcpyDeviceToHost));
+  stt.ema_chunks_fixed = (int64_t)fixed;
+  // fine ranges: every position within 448 samples of a hot block
+  FineTable ft;
+  {
+    const int64_t pad = 448;
+    int64_t lo = -1, hi = -1, total = 0;
+    auto flush = [&]() {
+      if (lo < 0 && hi < 0) return;
+      ft.first.push_back(lo); ft.count.push_back(hi - lo + 1); ft.base.push_back(total);
+      total += hi - lo + 1;
+    };
+    bool open = false;
+    for (int64_t b = 0; b < (int64_t)hot.size(); ++b) {
+      if (!hot[b]) continue;
+      const int64_t a = 32 * b - pad, z = 32 * b + 31 + pad;
+      if (open && a <= hi + 1) hi = std::max(hi, z);
+      else { if (open) flush(); lo = a; hi = z; open = true; }
+    }
+    if (open) flush();
+    ft.corr_se.assign(2 * (size_t)total, 0.0);
+    if (total) {
+      DBuf d_pre1, d_first, d_base, d_count, d_out;
+      std::vector<float> p1(cfg->symbol_len);
+      amod_preamble1(cfg, p1.data());
+      const int nr = (int)ft.first.size();
+      S_TRY(d_pre1.alloc(sizeof(float) * p1.size()));
+      S_TRY(d_first.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_base.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_count.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_out.alloc(sizeof(double) * 2 * (size_t)total));
+      S_TRY(hipMemcpyAsync(d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_first.p, ft.first.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
+      for (int r0 = 0; r0 < nr; r0 += 65535) {
+        const int k = std::min(65535, nr - r0);
+        S_TRY(amod_launch_fine(d_y.as<float>(), npad, d_pre1.as<float>(), cfg->symbol_len, d_first.as<int64_t>() + r0,
+                               d_base.as<int64_t>() + r0, d_count.as<int64_t>() + r0, k, maxc, d_out.as<double2>(), s));
+      }
+      S_TRY(hipMemcpyAsync(ft.corr_se.data(), d_out.p, sizeof(double) * 2 * (size_t)total, hipMemcpyDeviceToHost, s));
+    }
+  }
+  S_TRY(hipEventRecord(ev[2], s));
+  // the state machine reads the cleaned stream on the host
+  std::vector<float> yh((size_t)npad);
+  if (npad) S_TRY(hipMemcpyAsync(yh.data(), d_y.p, sizeof(float) * (size_t)npad, hipMemcpyDeviceToHost, s));
+  S_TRY(hipStreamSynchronize(s));
+  {
+    float a = 0, b = 0;
+    S_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    S_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    stt.t_ema_ms = a;
+    stt.t_fine_ms = b;
+  }
+  const auto t_gpu_pre = clk::now();
+
+  // ---- host: the receiver
+  amod_assembler *own = nullptr;
+  if (!assembler) {
+    if (amod_asm_open(nullptr, &own) != AMOD_SUCCESS) return amod_ctx_fail(ctx, "assembler", AMOD_ERR_NOMEM);
+    assembler = own;
+  }
+  struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
+  Receiver rx;
+  rx.cfg = cfg;
+  rx.n = n; rx.npad = npad; rx.y = yh.data(); rx.fine = &ft;
+  rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
+  rx.pre1.resize(cfg->symbol_len);
+  amod_preamble1(cfg, rx.pre1.data());
+  for (float v : rx.pre1) rx.pre1_energy += (double)v * (double)v;
+
+  struct Pending {
+    int64_t pos, end, window_len;
+    RxState after; // receiver state right after this frame was demodulated (reset included)
+  };
+  std::vector<Pending> pend;
+  int64_t nfr = 0, frames_decoded = 0, frame_errors = 0;
+  double t_decode = 0;
+  DBuf d_pos, d_len, d_woff, d_win, d_off, d_res, d_pay;
+  std::vector<amod_result> hres;
+  std::vector<uint8_t> hpay;
+
+  // decode the pending windows on the GPU, dispatch results in order; returns the
+  // index of a frame after which the window length changed (rollback), or -1
+  auto flush = [&](int64_t &rollback) -> int {
+    rollback = -1;
+    if (pend.empty()) return AMOD_SUCCESS;
+    const auto t0 = clk::now();
+    const int nw = (int)pend.size();
+    std::vector<int64_t> pos(nw), woff(nw);
+    std::vector<int32_t> len(nw);
+    int64_t tot = 0, maxlen = 0;
+    for (int i = 0; i < nw; ++i) {
+      pos[i] = pend[i].pos; len[i] = (int32_t)pend[i].window_len; woff[i] = tot;
+      tot += (pend[i].window_len + 3) & ~int64_t(3);
+      maxlen = std::max<int64_t>(maxlen, pend[i].window_len);
+    }
+    const int64_t stride = amod_payload_stride(cfg, maxlen);
+    S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
+    S_TRY(d_len.alloc(sizeof(int32_t) * nw));
+    S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
+    S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
+    S_TRY(d_res.alloc(sizeof(amod_result) * nw));
+    S_TRY(d_pay.alloc((size_t)stride * nw));
+    S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+    S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
+    S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+    S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
+    S_TRY(amod_launch_window(d_y.as<float>(), npad, d_pos.as<int64_t>(), d_len.as<int32_t>(), d_woff.as<int64_t>(),
+                             nw, d_win.as<float>(), s));
+    int rc = amod_reserve(ctx, cfg, nw, maxlen);
+    if (rc) return rc;
+    rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
+                            nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
+    if (rc) return rc;
+    hres.resize(nw);
+    hpay.resize((size_t)stride * nw);
+    S_TRY(hipMemcpyAsync(hres.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
+    S_TRY(hipMemcpyAsync(hpay.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
+    S_TRY(hipStreamSynchronize(s));
+    // _demodulateFrame's dispatch (app.js:926-961), in order
+    int i = 0;
+    for (; i < nw; ++i) {
+      const amod_result &r = hres[i];
+      if (nfr < max_frames) {
+        amod_stream_frame &f = frames[nfr];
+        f.pos = pend[i].pos; f.end = pend[i].end; f.window_len = (int32_t)pend[i].window_len; f.reserved = 0;
+        f.result = r;
+      }
+      ++nfr;
+      RxState &after = pend[i].after;
+      if (r.status != AMOD_OK) { ++frame_errors; continue; }
+      ++frames_decoded;
+      if (r.frame_type == 0xFE) {
+        if (r.crc_valid) {
+          const uint8_t *slot = hpay.data() + (size_t)stride * i;
+          const int m = amod_asm_metadata(assembler, r.total_chunks, r.total_size, r.chunk_size, slot + r.name_off,
+                                          r.name_len);
+          // the header fields are assigned even when the bitmap allocation throws
+          amod_asm_info inf;
+          amod_asm_state(assembler, &inf);
+          bool meta = after.meta_received;
+          if (m == AMOD_ASM_RANGE_ERROR) ++frame_errors; // caught by the receiver; metaReceived unchanged
+          else meta = true;
+          const bool changed = meta != after.meta_received || (meta && inf.chunk_size != after.chunk_size);
+          after.meta_received = meta;
+          after.chunk_size = inf.chunk_size;
+          if (changed) {
+            rollback = i;
+            if (i + 1 < nw) { ++i; break; }
+          }
+        } else {
+          ++frame_errors;
+        }
+      } else if (r.frame_type == 0xFF) {
+        const uint8_t *slot = hpay.data() + (size_t)stride * i;
+        const int c = amod_asm_chunk(assembler, r.seq_num, slot + r.data_off, r.data_len, r.crc_valid);
+        if (c < 0) return amod_ctx_fail(ctx, "assembler store", c);
+      }
+    }
+    (void)i;
+    t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return AMOD_SUCCESS;
+  };
+
+  rx.st.block = 0;
+  {
+    amod_asm_info inf;
+    amod_asm_state(assembler, &inf);
+    rx.st.chunk_size = inf.chunk_size; // this.assembler.chunkSize as the receiver starts
+  }
+  while (rx.st.block < nblocks) {
+    // processAudioBlock (app.js:749-773): the block is written, then one state step
+    switch (rx.st.state) {
+    case IDLE: rx.scan(); break;
+    case DETECTED: rx.refine(); break;
+    case COLLECTING:
+      if (rx.tw() >= rx.st.frame_end) {
+        // _demodulateFrame (app.js:907-972)
+        const int64_t len = rx.st.frame_end - rx.st.pre_pos;
+        const bool lost = rx.st.pre_pos < rx.tw() - rx.cap; // getRange: already overwritten
+        if (lost) {
+          if (nfr < max_frames) {
+            amod_stream_frame &f = frames[nfr];
+            std::memset(&f, 0, sizeof f);
+            f.pos = rx.st.pre_pos; f.end = rx.st.frame_end; f.window_len = 0;
+            f.result.status = AMOD_E_STREAM_LOST;
+            f.result.preamble_idx = -1; f.result.coarse_idx = -1; f.result.frame_type = -1;
+          }
+          ++nfr;
+          ++frame_errors;
+          rx.reset();
+        } else {
+          Pending p{rx.st.pre_pos, rx.st.frame_end, len, RxState{}};
+          rx.reset();
+          p.after = rx.st;
+          p.after.block = rx.st.block + 1;
+          pend.push_back(p);
+          // before the metadata frame every frame is decoded at once: its result decides
+          // the window length of the next one
+          if (!rx.st.meta_received || (int)pend.size() >= kBatch) {
+            int64_t rb;
+            const int rc = flush(rb);
+            if (rc) return rc;
+            const RxState resume = rb >= 0 ? pend[rb].after : pend.back().after;
+            pend.clear();
+            rx.st = resume;
+            continue;
+          }
+        }
+      }
+      break;
+    }
+    ++rx.st.block;
+    if (rx.st.block >= nblocks && !pend.empty()) {
+      int64_t rb;
+      const int rc = flush(rb);
+      if (rc) return rc;
+      if (rb >= 0) { // the window length changed after frame rb: redo what followed it
+        const RxState resume = pend[rb].after;
+        pend.clear();
+        rx.st = resume;
+      } else {
+        pend.clear();
+      }
+    }
+  }
+  *nframes_out = nfr;
+  for (size_t i = 0; i < rx.refine_fail.size() && (int64_t)i < max_refine_fail; ++i) refine_fail[i] = rx.refine_fail[i];
+  for (auto &e : ev) (void)hipEventDestroy(e);
+  if (stats) {
+    stt.nframes = nfr;
+    stt.nrefine_fail = (int64_t)rx.refine_fail.size();
+    stt.frames_decoded = frames_decoded;
+    stt.frame_errors = frame_errors;
+    stt.final_state = rx.st.state;
+    stt.final_scan_pos = rx.st.ac_pos;
+    stt.fine_host_positions = rx.fine_host;
+    stt.t_decode_ms = t_decode;
+    stt.t_total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
+    stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - t_decode;
+    *stats = stt;
+  }
+  return AMOD_SUCCESS;
+}

@@ -262,6 +262,33 @@ int64_t amod_asm_name(const amod_assembler *a, uint8_t *out, int64_t cap);
 int64_t amod_asm_missing(const amod_assembler *a, int32_t *out, int64_t cap);
 int64_t amod_asm_file(const amod_assembler *a, uint8_t *out, int64_t cap);
 
+/* ---- streaming receive: app.js StreamingReceiver (706-998) over a recorded stream ----
+ * The stream is cut into 4096-sample blocks (the ScriptProcessor size; a last partial
+ * block is completed with zeros) and run through the reference's receiver: EMA DC
+ * removal, Schmidl-Cox scan, cross-correlation refine, frame collection, per-window
+ * peak normalisation, decodeChunkFrame (GPU, chunk mode) and the ChunkAssembler
+ * dispatch into `assembler` (NULL: a private one). frames[0..min(*nframes, max_frames))
+ * receive every demodulated window: pos = preambleGlobalPos, end = expectedFrameEnd,
+ * result = decodeChunkFrame's outcome (AMOD_E_STREAM_LOST: the window had left the
+ * ring buffer, counted as a frame error). refine_fail lists preamble positions whose
+ * refinement found no correlation >= 0.1 (app.js:880-884). samples: host memory.    */
+#define AMOD_E_STREAM_LOST 101 /* not a decode outcome: getRange() returned null */
+typedef struct amod_stream_frame {
+  int64_t pos, end;
+  int32_t window_len, reserved;
+  amod_result result;
+} amod_stream_frame;
+typedef struct amod_stream_stats {
+  int64_t nframes, nrefine_fail, frames_decoded, frame_errors; /* receiver counters */
+  int64_t final_state, final_scan_pos;        /* RECV_STATE and acScanPos after the last block */
+  int64_t ema_chunks_fixed;                    /* EMA chunks recomputed after the warm-up check */
+  int64_t fine_host_positions;                 /* refine positions outside the GPU precompute */
+  double t_ema_ms, t_fine_ms, t_decode_ms, t_host_ms, t_total_ms;
+} amod_stream_stats;
+int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
+                        amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                        int64_t *nframes, int64_t *refine_fail, int64_t max_refine_fail, amod_stream_stats *stats);
+
 /* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
 void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
 /* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),

@@ -161,6 +161,8 @@ def apply_post(x: np.ndarray, post) -> np.ndarray:
             x = add_noise(x, op.get("snr", 0), op["seed"], op.get("div"))
         elif op["op"] == "dc":
             x = (x.astype(np.float64) + op["dc"]).astype(np.float32)
+        elif op["op"] == "gain":
+            x = (x.astype(np.float64) * op["gain"]).astype(np.float32)
         else:
             raise ValueError(op)
     return np.ascontiguousarray(x, np.float32)

@@ -1,0 +1,102 @@
+"""Streaming receive (app.js StreamingReceiver 706-998) against the reference itself.
+
+tests/golden/stream.json holds, for recipe streams (a chunked file as metadata + data
+frames from the reference builders, with leading silence, gaps, gain, DC offset,
+AWGN, a corrupted and retransmitted chunk, acoustic / narrowband presets, a stream
+without metadata), what the reference receiver did when fed the stream in 4096-sample
+blocks: every demodulated window (preambleGlobalPos, expectedFrameEnd, length) with
+its decodeChunkFrame result, the failed refinements, its counters, its scan position
+at the end and the file it offered. The stream is rebuilt here bit for bit (SHA-256)
+and run through amod_stream_receive; every one of those must match exactly.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import ERRORS, GOLDEN
+
+import amodem
+from amodem import _lib as L
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def streams():
+    with open(os.path.join(GOLDEN, "stream.json")) as f:
+        return json.load(f)["streams"]
+
+
+def build_stream(sp):
+    """gen_stream.js buildStream with the product's (bit-exact) transmit builders."""
+    cfg = amodem.preset(sp["config"], sp["mod"], sp["rep"])
+    data = amodem.synth_payload(sp["fileSeed"], sp["fileLen"])
+    nch = -(-sp["fileLen"] // sp["chunkSize"])
+    parts = [np.zeros(sp.get("lead") or 0, np.float32)]
+    for f in sp["recipe"]:
+        if f["kind"] == "meta":
+            s = amodem.build_metadata_frame(nch, sp["fileLen"], sp["chunkSize"], sp["fileName"], cfg=cfg)
+        else:
+            cs = sp["chunkSize"]
+            s = amodem.build_data_chunk_frame(data[f["seq"] * cs:(f["seq"] + 1) * cs], f["seq"], cfg=cfg)
+        if f.get("corrupt"):
+            s = s.copy()
+            c = f["corrupt"]
+            s[c["start"]:c["end"]] = np.float32(c["value"])
+        parts.append(s)
+        if f.get("gap"):
+            parts.append(np.zeros(f["gap"], np.float32))
+    parts.append(np.zeros(sp.get("tail") or 0, np.float32))
+    x = np.concatenate(parts)
+    total = -(-len(x) // 4096) * 4096
+    x = np.concatenate([x, np.zeros(total - len(x), np.float32)])
+    return cfg, O.apply_post(x, sp.get("post")), data
+
+
+def result_view(r):
+    st = int(r["status"])
+    if st != 0:
+        if st == 13:
+            return {"error": f"Unknown frame type: 0x{int(r['aux']):x}"}
+        if st == 7:
+            return {"error": f"Invalid data length: {int(r['aux'])}"}
+        return {"error": ERRORS[st]}
+    out = {"frameType": int(r["frame_type"]), "crcValid": bool(r["crc_valid"])}
+    if out["frameType"] == 255:
+        out.update(seqNum=int(r["seq_num"]), dataLen=int(r["data_len"]))
+    else:
+        out.update(totalChunks=int(r["total_chunks"]), chunkSize=int(r["chunk_size"]))
+    return out
+
+
+@pytest.mark.parametrize("sp", streams(), ids=lambda s: s["name"])
+def test_stream_matches_reference(sp):
+    cfg, x, data = build_stream(sp)
+    assert len(x) == sp["n"]
+    assert hashlib.sha256(x.tobytes()).hexdigest() == sp["sha256"]
+    dm = amodem.Demodulator(0)
+    asm = amodem.ChunkAssembler()
+    frames, refine_fail, stats = dm.stream_receive(cfg, x, asm)
+    dm.close()
+    assert stats["ema_chunks_fixed"] >= 0
+    want = sp["frames"]
+    got = [{"pos": int(f["pos"]), "end": int(f["end"]), "len": int(f["window_len"]), **result_view(f["result"])}
+           for f in frames]
+    want_v = [{k: v for k, v in w.items() if k != "fileName"} for w in want]
+    assert got == want_v
+    assert refine_fail == sp["refineFail"]
+    assert (stats["frames_decoded"], stats["frame_errors"]) == (sp["framesDecoded"], sp["frameErrors"])
+    assert (stats["final_state"], stats["final_scan_pos"]) == (sp["final"]["state"], sp["final"]["acScanPos"])
+    st, a = asm.state(), sp["assembler"]
+    assert (st["total_chunks"], st["total_size"], st["chunk_size"], st["received"], st["crc_errors"],
+            bool(st["complete"])) == (a["totalChunks"], a["totalFileSize"], a["chunkSize"], a["receivedCount"],
+                                      a["crcErrors"], a["complete"])
+    assert asm.file_name() == a["fileName"].encode()
+    if sp["offered"] is not None:
+        f = asm.assemble_file()
+        assert len(f) == sp["offered"]["size"]
+        assert hashlib.sha256(f).hexdigest() == sp["offered"]["sha256"] == sp["fileSha256"]
+        assert f == data[:len(f)]
