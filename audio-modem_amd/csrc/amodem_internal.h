@@ -381,7 +381,7 @@ int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap); // dynamic LDS 
 // streaming receiver pieces (k_stream.hip)
 hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, float *y, double *warm, double *end,
                            unsigned long long *fixed, hipStream_t s);
-hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, uint8_t *hot, hipStream_t s);
+hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
 hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, const int64_t *first,
                             const int64_t *base, const int64_t *count, int nranges, int64_t maxcount, double2 *out,
                             hipStream_t s);

@@ -11,9 +11,10 @@
 //   k_ema_fix    one lane walks the chunks in order: a chunk whose warm-up state is
 //                not bit-equal to its predecessor's true end state is recomputed from
 //                that state. Afterwards every cleaned sample equals the reference's.
-//   k_sc_screen  hot-block screening for the fine precompute: per 32-sample block the
-//                Schmidl-Cox metric at the block start from fp64 block sums; only a
-//                hint (the host recomputes anything the hint missed).
+//   k_sc_blocks  fp64 32-sample block sums (coalesced, 32-lane reductions), then
+//   k_sc_screen  hot-block screening for the fine precompute: the Schmidl-Cox metric
+//                at each block start from 8-block window sums; only a hint (the host
+//                recomputes anything the hint missed).
 //   k_fine       _refineAndCollect's cross-correlation sums (app.js:864-877) for a
 //                list of position ranges: corr = sum seg[i] pre1[i] and sEnergy =
 //                sum seg[i]^2 in the reference's order, one lane per position, IEEE
@@ -95,20 +96,31 @@ __global__ void k_ema_fix(const float *__restrict__ x, int64_t n, int64_t L, flo
   *fixed = nf;
 }
 
-// per 32-sample block b: metric at position 32 b from fp64 block sums (window = 8 blocks)
-__global__ __launch_bounds__(256) void k_sc_screen(const float *__restrict__ y, int64_t n, int64_t nblk,
-                                                   float thresh, uint8_t *__restrict__ hot) {
+// 32-sample block sums of the cleaned stream in fp64: z_b = sum y[k] y[k+256], e_b =
+// sum y[k]^2 over k in [32 b, 32 b + 32); one lane per sample, 32-lane reductions
+__global__ __launch_bounds__(256) void k_sc_blocks(const float *__restrict__ y, int64_t n, int64_t nblk,
+                                                   double2 *__restrict__ ze) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const double a = sample_at(y, n, k), c = sample_at(y, n, k + 256);
+  double z = a * c, e = a * a;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) { z += __shfl_xor(z, o, 32); e += __shfl_xor(e, o, 32); }
+  const int64_t b = k >> 5;
+  if ((threadIdx.x & 31) == 0 && b < nblk) ze[b] = make_double2(z, e);
+}
+
+// hot flag per block: the metric at position 32 b (window = 8 blocks) >= thresh
+__global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ ze, int64_t nblk, float thresh,
+                                                   uint8_t *__restrict__ hot) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= nblk) return;
   double p = 0.0, ra = 0.0, rb = 0.0;
-  const int64_t d = 32 * b;
-  for (int m = 0; m < 256; ++m) {
-    const double a = sample_at(y, n, d + m), c = sample_at(y, n, d + m + 256);
-    p += a * c; ra += a * a; rb += c * c;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (b + q < nblk) { const double2 v = ze[b + q]; p += v.x; ra += v.y; }
+    if (b + 8 + q < nblk) rb += ze[b + 8 + q].y;
   }
-  uint8_t h = 0;
-  if (ra > 0.001 && rb > 0.001 && (p * p) / (ra * rb) >= (double)thresh) h = 1;
-  hot[b] = h;
+  hot[b] = (ra > 0.001 && rb > 0.001 && (p * p) / (ra * rb) >= (double)thresh) ? 1 : 0;
 }
 
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
@@ -164,10 +176,11 @@ hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, floa
   hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, n, L, y, warm, end, nchunks, fixed);
   return hipGetLastError();
 }
-hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, uint8_t *hot, hipStream_t s) {
+hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {
   const int64_t nblk = (n + 31) / 32;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_sc_screen, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, y, n, nblk, thresh, hot);
+  hipLaunchKernelGGL(amod::k_sc_blocks, dim3((unsigned)((32 * nblk + 255) / 256)), dim3(256), 0, s, y, n, nblk, ze);
+  hipLaunchKernelGGL(amod::k_sc_screen, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, ze, nblk, thresh, hot);
   return hipGetLastError();
 }
 hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, const int64_t *first,

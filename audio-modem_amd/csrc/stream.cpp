@@ -35,7 +35,7 @@
 namespace {
 
 constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
-constexpr int64_t kEmaChunk = 65536;  // k_ema chunk per lane
+constexpr int64_t kEmaChunk = 8192;   // k_ema chunk per lane (more lanes than warm-up length: latency bound)
 constexpr int64_t kEmaWarm = 65536;   // warm-up run before each chunk
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
 enum { IDLE = 0, DETECTED = 1, COLLECTING = 2 };
@@ -71,10 +71,15 @@ struct RxState {
 struct FineTable {
   std::vector<int64_t> first, base, count;
   std::vector<double> corr_se; // pairs
+  mutable size_t last = 0; // refine walks consecutive positions: try the last range first
   bool lookup(int64_t d, double &corr, double &se) const {
-    auto it = std::upper_bound(first.begin(), first.end(), d);
-    if (it == first.begin()) return false;
-    const size_t r = (size_t)(it - first.begin()) - 1;
+    size_t r = last;
+    if (r >= first.size() || d < first[r] || d >= first[r] + count[r]) {
+      auto it = std::upper_bound(first.begin(), first.end(), d);
+      if (it == first.begin()) return false;
+      r = (size_t)(it - first.begin()) - 1;
+      last = r;
+    }
     if (d >= first[r] + count[r]) return false;
     const int64_t k = base[r] + (d - first[r]);
     corr = corr_se[2 * k];
@@ -114,10 +119,15 @@ struct Receiver {
     const double min_e = 0.001;
     double best = 0;
     int64_t best_pos = -1;
+    // p^2 < 0.49 ra rb (rounded products, relative error ~1e-16) proves the rounded
+    // quotient is below 0.5: the division is only evaluated where it can matter
     while (st.ac_pos <= scan_end) {
       if (st.ac_ra > min_e && st.ac_rb > min_e) {
-        const double metric = (st.ac_p * st.ac_p) / (st.ac_ra * st.ac_rb);
-        if (metric > 0.5 && metric > best) { best = metric; best_pos = st.ac_pos; }
+        const double pp = st.ac_p * st.ac_p, rr = st.ac_ra * st.ac_rb;
+        if (pp >= 0.49 * rr) {
+          const double metric = pp / rr;
+          if (metric > 0.5 && metric > best) { best = metric; best_pos = st.ac_pos; }
+        }
       }
       if (st.ac_pos < scan_end) {
         const double a_out = S(st.ac_pos), mid = S(st.ac_pos + half), b_in = S(st.ac_pos + 2 * half);
@@ -194,7 +204,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
   amod_stream_stats stt{};
   // ---- GPU: DC removal (exact), screening, fine sums
-  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot;
+  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot, d_ze;
   const int64_t nchunks = std::max<int64_t>(1, (npad + kEmaChunk - 1) / kEmaChunk);
   S_TRY(d_x.alloc(sizeof(float) * (size_t)npad + 64));
   S_TRY(d_y.alloc(sizeof(float) * (size_t)npad + 64));
@@ -202,6 +212,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   S_TRY(d_end.alloc(sizeof(double) * nchunks));
   S_TRY(d_fixed.alloc(8));
   S_TRY(d_hot.alloc((size_t)(npad / 32 + 1)));
+  S_TRY(d_ze.alloc(sizeof(double2) * (size_t)(npad / 32 + 1)));
   if (npad) {
     S_TRY(hipMemsetAsync(d_x.p, 0, sizeof(float) * (size_t)npad, s));
     if (n) S_TRY(hipMemcpyAsync(d_x.p, samples, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
@@ -212,7 +223,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   S_TRY(amod_launch_ema(d_x.as<float>(), npad, kEmaChunk, kEmaWarm, d_y.as<float>(), d_warm.as<double>(),
                         d_end.as<double>(), d_fixed.as<unsigned long long>(), s));
   S_TRY(hipEventRecord(ev[1], s));
-  S_TRY(amod_launch_sc_screen(d_y.as<float>(), npad, 0.25f, d_hot.as<uint8_t>(), s));
+  S_TRY(amod_launch_sc_screen(d_y.as<float>(), npad, 0.25f, d_ze.as<double2>(), d_hot.as<uint8_t>(), s));
   std::vector<uint8_t> hot((size_t)(npad / 32));
   if (!hot.empty()) S_TRY(hipMemcpyAsync(hot.data(), d_hot.p, hot.size(), hipMemcpyDeviceToHost, s));
   S_TRY(hipStreamSynchronize(s));
@@ -263,8 +274,12 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   }
   S_TRY(hipEventRecord(ev[2], s));
   // the state machine reads the cleaned stream on the host
-  std::vector<float> yh((size_t)npad);
-  if (npad) S_TRY(hipMemcpyAsync(yh.data(), d_y.p, sizeof(float) * (size_t)npad, hipMemcpyDeviceToHost, s));
+  struct Pinned {
+    float *p = nullptr;
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+  } yh;
+  S_TRY(hipHostMalloc((void **)&yh.p, sizeof(float) * (size_t)std::max<int64_t>(npad, 1), hipHostMallocDefault));
+  if (npad) S_TRY(hipMemcpyAsync(yh.p, d_y.p, sizeof(float) * (size_t)npad, hipMemcpyDeviceToHost, s));
   S_TRY(hipStreamSynchronize(s));
   {
     float a = 0, b = 0;
@@ -284,7 +299,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
   Receiver rx;
   rx.cfg = cfg;
-  rx.n = n; rx.npad = npad; rx.y = yh.data(); rx.fine = &ft;
+  rx.n = n; rx.npad = npad; rx.y = yh.p; rx.fine = &ft;
   rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
   rx.pre1.resize(cfg->symbol_len);
   amod_preamble1(cfg, rx.pre1.data());

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--config", choices=["c2", "c3"], default="c2",
                     help="c2: 10k QPSK 1 KB frames per GPU (the metric's config); c3: 100k 16-QAM 1 KB frames")
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0: the config's, C2 10,000 / C3 100,000)")
+    ap.add_argument("--stream-chunks", type=int, default=2000,
+                    help="C4-shaped stream for the streaming-receiver leg (0 = skip)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="CPU-baseline sample (0 = auto, -1 = skip)")
     args = ap.parse_args()
 
@@ -123,6 +125,7 @@ def main():
         assert r.get("data") == amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), PAYLOAD), (i, r.get("error"))
 
     lib = L.load()
+    stream_res = stream_leg(amodem, L, local, args.stream_chunks) if (args.stream_chunks > 0 and rank == 0) else None
     # correlation-scan phase alone (k_corr_scan), measured before the timed region
     scan = scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, spf)
     lib.amod_set_profiling(dm.ctx, 1)
@@ -210,6 +213,7 @@ def main():
                    "roofline": {"bound": "hbm", "achieved": tx_bytes / (tx_avg_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": tx_bytes / (tx_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
                    "cpu_baseline": tx_cpu},
+            "stream": stream_res,
         }
         print(json.dumps(out), flush=True)
     dm.close()
@@ -240,6 +244,34 @@ def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, st
         return fm.value / max(1, fn.value)
     finally:
         del os.environ["AMOD_STOP_AFTER"]
+
+
+def stream_leg(amodem, L, device, nchunks=2000, chunk=2048):
+    """StreamingReceiver over a C4-shaped stream (metadata + nchunks 2 KB QPSK chunk
+    frames back to back, built by k_tx): whole-call time from host samples to the
+    assembled file, with the receiver's own phase split."""
+    cfg = amodem.preset("standard", "QPSK", 1)
+    data = amodem.synth_payload(0xC4000001, nchunks * chunk - 123)
+    pk = [amodem.packet_meta(nchunks, len(data), chunk, "c4.bin")]
+    pk += [amodem.packet_chunk(data[i * chunk:(i + 1) * chunk], i) for i in range(nchunks)]
+    dm = amodem.Demodulator(device)
+    sig, _, _ = dm.transmit_batch(cfg, pk, [L.TX_META] + [L.TX_CHUNK] * nchunks)
+    total = -(-(len(sig) + 8192) // 4096) * 4096
+    x = np.concatenate([sig, np.zeros(total - len(sig), np.float32)])
+    asm = amodem.ChunkAssembler()
+    dm.stream_receive(cfg, x[: 64 * 4096], amodem.ChunkAssembler())  # warm-up (tables, kernels)
+    t0 = time.perf_counter()
+    frames, _, st = dm.stream_receive(cfg, x, asm)
+    t = time.perf_counter() - t0
+    ok = asm.is_complete() and asm.assemble_file() == data
+    dm.close()
+    return {"what": "app.js StreamingReceiver restated (amod_stream_receive): host samples in, frames + assembled file out",
+            "workload": f"C4-shaped stream, metadata + {nchunks} x 2 KB QPSK chunk frames ({len(x)} samples)",
+            "samples_per_s": len(x) / t, "payload_MB_per_s": len(data) / t / 1e6, "seconds": t,
+            "frames": int(len(frames)), "file_ok": bool(ok),
+            "phases_ms": {"ema_gpu": st["t_ema_ms"], "screen_fine_gpu": st["t_fine_ms"], "decode_gpu": st["t_decode_ms"],
+                          "state_machine_host": st["t_host_ms"], "total": st["t_total_ms"]},
+            "reference_rate_note": "reference StreamingReceiver: 2.0e6 samples/s per core (SURVEY.md section 3.2)"}
 
 
 def cpu_baseline(x, offs, lens, mod, name):
