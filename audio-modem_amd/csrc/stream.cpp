@@ -27,7 +27,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "amodem_internal.h"
@@ -71,8 +73,8 @@ struct RxState {
 struct FineTable {
   std::vector<int64_t> first, base, count;
   std::vector<double> corr_se; // pairs
-  mutable size_t last = 0; // refine walks consecutive positions: try the last range first
-  bool lookup(int64_t d, double &corr, double &se) const {
+  // refine walks consecutive positions: `last` (the caller's cursor) is tried first
+  bool lookup(int64_t d, double &corr, double &se, size_t &last) const {
     size_t r = last;
     if (r >= first.size() || d < first[r] || d >= first[r] + count[r]) {
       auto it = std::upper_bound(first.begin(), first.end(), d);
@@ -96,8 +98,9 @@ struct Receiver {
   double pre1_energy = 0;
   const FineTable *fine = nullptr;
   RxState st;
-  std::vector<int64_t> refine_fail;
+  std::vector<std::pair<int64_t, int64_t>> *fails = nullptr; // (block, preambleGlobalPos) of failed refinements
   int64_t fine_host = 0; // positions the host had to correlate itself
+  size_t cursor = 0;     // FineTable lookup cursor
 
   double S(int64_t i) const { return (i >= 0 && i < npad) ? (double)y[i] : 0.0; }
   int64_t tw() const { return (st.block + 1) * kBlock; } // totalWritten after this block's write
@@ -153,7 +156,7 @@ struct Receiver {
     int64_t best_pos = st.pre_pos;
     for (int64_t d = fs; d <= fe; ++d) {
       double corr = 0, se = 0;
-      if (!fine || !fine->lookup(d, corr, se)) {
+      if (!fine || !fine->lookup(d, corr, se, cursor)) {
         for (int64_t i = 0; i < plen; ++i) {
           const double s = S(d + i);
           corr += s * (double)pre1[i];
@@ -168,7 +171,7 @@ struct Receiver {
       }
     }
     if (best < 0.1) {
-      refine_fail.push_back(st.pre_pos);
+      if (fails) fails->push_back({st.block, st.pre_pos});
       st.state = IDLE;
       st.ac_init = false;
       return;
@@ -188,6 +191,121 @@ struct Receiver {
     st.state = IDLE;
   }
 };
+
+// one demodulated window of the trajectory and the receiver state right after it
+// (_resetToIdle done, positioned at the next block)
+struct FrameEv {
+  int64_t pos, end;
+  bool lost; // getRange() returned null: counted as a frame error, nothing decoded
+  RxState after;
+};
+struct Traj {
+  std::vector<FrameEv> frames;
+  std::vector<std::pair<int64_t, int64_t>> fails;
+  RxState end;
+};
+
+// two runs that demodulated the same window and stand in the same post-reset state
+// continue identically (the next scan re-initialises its sums)
+bool same_after(const RxState &a, const RxState &b) {
+  return a.block == b.block && a.state == b.state && a.ac_init == b.ac_init && a.ac_pos == b.ac_pos &&
+         a.pre_pos == b.pre_pos && a.frame_end == b.frame_end && a.meta_received == b.meta_received &&
+         a.chunk_size == b.chunk_size && !a.ac_init;
+}
+
+// processAudioBlock (app.js:749-773) for blocks [st.block, stop): the state step of each
+// block. first_only: return after the first demodulated window. sync: return at the
+// first window that `sync` also demodulated from the same state (*sync_idx = its index).
+void run_blocks(Receiver &rx, const RxState &start, int64_t stop, bool first_only, const Traj *sync, Traj &out,
+                int64_t *sync_idx) {
+  rx.st = start;
+  rx.fails = &out.fails;
+  if (sync_idx) *sync_idx = -1;
+  while (rx.st.block < stop) {
+    switch (rx.st.state) {
+    case IDLE: rx.scan(); break;
+    case DETECTED: rx.refine(); break;
+    case COLLECTING:
+      if (rx.tw() >= rx.st.frame_end) { // _checkFrameComplete -> _demodulateFrame (app.js:900-972)
+        FrameEv ev{rx.st.pre_pos, rx.st.frame_end, rx.st.pre_pos < rx.tw() - rx.cap, RxState{}};
+        rx.reset();
+        ev.after = rx.st;
+        ev.after.block = rx.st.block + 1;
+        out.frames.push_back(ev);
+        if (sync) {
+          auto it = std::lower_bound(sync->frames.begin(), sync->frames.end(), ev.pos,
+                                     [](const FrameEv &f, int64_t p) { return f.pos < p; });
+          for (; it != sync->frames.end() && it->pos == ev.pos; ++it)
+            if (it->end == ev.end && same_after(it->after, ev.after)) {
+              *sync_idx = it - sync->frames.begin();
+              out.end = ev.after;
+              return;
+            }
+        }
+        if (first_only) {
+          out.end = ev.after;
+          return;
+        }
+      }
+      break;
+    }
+    ++rx.st.block;
+  }
+  out.end = rx.st;
+}
+
+// The receiver from `start` to the last block on up to `nthreads` host threads. Segment k
+// starts speculatively (IDLE, scan resuming at its first block, the same metadata state);
+// the true run is carried across each boundary until it demodulates a window that the
+// speculative segment demodulated from the identical post-reset state, and adopts the
+// segment's trajectory from there (or covers the whole segment itself).
+Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, int nthreads, int64_t &fine_host) {
+  const int64_t span = nblocks - start.block;
+  const char *ms = getenv("AMOD_STREAM_MINSEG"); // tests: force short speculative segments
+  const int64_t minseg = ms ? std::max(1, atoi(ms)) : 64;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, span / minseg));
+  std::vector<int64_t> bnd(T + 1);
+  for (int k = 0; k <= T; ++k) bnd[k] = start.block + span * k / T;
+  std::vector<Traj> seg(T);
+  std::vector<Receiver> rxs(T, proto);
+  std::vector<std::thread> th;
+  for (int k = 0; k < T; ++k) {
+    th.emplace_back([&, k] {
+      RxState st = start;
+      if (k > 0) {
+        st = RxState{};
+        st.block = bnd[k];
+        st.state = IDLE;
+        st.ac_pos = bnd[k] * kBlock - 511; // where a continuous scan stands at this block
+        st.meta_received = start.meta_received;
+        st.chunk_size = start.chunk_size;
+      }
+      run_blocks(rxs[k], st, bnd[k + 1], false, nullptr, seg[k], nullptr);
+    });
+  }
+  for (auto &t : th) t.join();
+  Traj total = std::move(seg[0]);
+  Receiver rx = proto;
+  for (int k = 1; k < T; ++k) {
+    Traj cont;
+    int64_t j = -1;
+    run_blocks(rx, total.end, bnd[k + 1], false, &seg[k], cont, &j);
+    total.frames.insert(total.frames.end(), cont.frames.begin(), cont.frames.end());
+    total.fails.insert(total.fails.end(), cont.fails.begin(), cont.fails.end());
+    if (j >= 0) {
+      const int64_t after_block = seg[k].frames[j].after.block;
+      total.frames.insert(total.frames.end(), seg[k].frames.begin() + j + 1, seg[k].frames.end());
+      for (auto &f : seg[k].fails)
+        if (f.first >= after_block) total.fails.push_back(f);
+      total.end = seg[k].end;
+    } else {
+      total.end = cont.end;
+    }
+  }
+  fine_host += rx.fine_host;
+  for (auto &r : rxs) fine_host += r.fine_host;
+  return total;
+}
 
 } // namespace
 
@@ -297,181 +415,163 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
     assembler = own;
   }
   struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
-  Receiver rx;
-  rx.cfg = cfg;
-  rx.n = n; rx.npad = npad; rx.y = yh.p; rx.fine = &ft;
-  rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
-  rx.pre1.resize(cfg->symbol_len);
-  amod_preamble1(cfg, rx.pre1.data());
-  for (float v : rx.pre1) rx.pre1_energy += (double)v * (double)v;
+  Receiver proto;
+  proto.cfg = cfg;
+  proto.n = n; proto.npad = npad; proto.y = yh.p; proto.fine = &ft;
+  proto.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
+  proto.pre1.resize(cfg->symbol_len);
+  amod_preamble1(cfg, proto.pre1.data());
+  for (float v : proto.pre1) proto.pre1_energy += (double)v * (double)v;
+  const char *tenv = getenv("AMOD_STREAM_THREADS"); // tests: 1 = the plain sequential receiver
+  const int nthreads = tenv ? std::max(1, atoi(tenv))
+                            : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 
-  struct Pending {
-    int64_t pos, end, window_len;
-    RxState after; // receiver state right after this frame was demodulated (reset included)
-  };
-  std::vector<Pending> pend;
-  int64_t nfr = 0, frames_decoded = 0, frame_errors = 0;
+  int64_t nfr = 0, frames_decoded = 0, frame_errors = 0, fine_host = 0;
+  std::vector<int64_t> fails_out;
   double t_decode = 0;
-  DBuf d_pos, d_len, d_woff, d_win, d_off, d_res, d_pay;
+  DBuf d_pos, d_len, d_woff, d_win, d_res, d_pay;
   std::vector<amod_result> hres;
   std::vector<uint8_t> hpay;
 
-  // decode the pending windows on the GPU, dispatch results in order; returns the
-  // index of a frame after which the window length changed (rollback), or -1
-  auto flush = [&](int64_t &rollback) -> int {
-    rollback = -1;
-    if (pend.empty()) return AMOD_SUCCESS;
-    const auto t0 = clk::now();
-    const int nw = (int)pend.size();
-    std::vector<int64_t> pos(nw), woff(nw);
-    std::vector<int32_t> len(nw);
-    int64_t tot = 0, maxlen = 0;
-    for (int i = 0; i < nw; ++i) {
-      pos[i] = pend[i].pos; len[i] = (int32_t)pend[i].window_len; woff[i] = tot;
-      tot += (pend[i].window_len + 3) & ~int64_t(3);
-      maxlen = std::max<int64_t>(maxlen, pend[i].window_len);
-    }
-    const int64_t stride = amod_payload_stride(cfg, maxlen);
-    S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
-    S_TRY(d_len.alloc(sizeof(int32_t) * nw));
-    S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
-    S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
-    S_TRY(d_res.alloc(sizeof(amod_result) * nw));
-    S_TRY(d_pay.alloc((size_t)stride * nw));
-    S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-    S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
-    S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-    S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
-    S_TRY(amod_launch_window(d_y.as<float>(), npad, d_pos.as<int64_t>(), d_len.as<int32_t>(), d_woff.as<int64_t>(),
-                             nw, d_win.as<float>(), s));
-    int rc = amod_reserve(ctx, cfg, nw, maxlen);
-    if (rc) return rc;
-    rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
-                            nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
-    if (rc) return rc;
-    hres.resize(nw);
-    hpay.resize((size_t)stride * nw);
-    S_TRY(hipMemcpyAsync(hres.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
-    S_TRY(hipMemcpyAsync(hpay.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
-    S_TRY(hipStreamSynchronize(s));
-    // _demodulateFrame's dispatch (app.js:926-961), in order
-    int i = 0;
-    for (; i < nw; ++i) {
-      const amod_result &r = hres[i];
-      if (nfr < max_frames) {
-        amod_stream_frame &f = frames[nfr];
-        f.pos = pend[i].pos; f.end = pend[i].end; f.window_len = (int32_t)pend[i].window_len; f.reserved = 0;
-        f.result = r;
+  // decode frames[a, b) (windows on the GPU) and dispatch them in order
+  // (_demodulateFrame, app.js:907-972); returns the index of the first frame whose
+  // metadata result changed the window length of what follows (its `after` updated),
+  // or -1
+  auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
+    changed = -1;
+    for (size_t c0 = a; c0 < b; c0 += kBatch) {
+      const size_t c1 = std::min(b, c0 + (size_t)kBatch);
+      const auto t0 = clk::now();
+      std::vector<int64_t> pos, woff;
+      std::vector<int32_t> len;
+      std::vector<int> slot(c1 - c0, -1);
+      int64_t tot = 0, maxlen = 0;
+      for (size_t i = c0; i < c1; ++i) {
+        if (fr[i].lost) continue;
+        slot[i - c0] = (int)pos.size();
+        const int64_t L = fr[i].end - fr[i].pos;
+        pos.push_back(fr[i].pos); len.push_back((int32_t)L); woff.push_back(tot);
+        tot += (L + 3) & ~int64_t(3);
+        maxlen = std::max(maxlen, L);
       }
-      ++nfr;
-      RxState &after = pend[i].after;
-      if (r.status != AMOD_OK) { ++frame_errors; continue; }
-      ++frames_decoded;
-      if (r.frame_type == 0xFE) {
-        if (r.crc_valid) {
-          const uint8_t *slot = hpay.data() + (size_t)stride * i;
-          const int m = amod_asm_metadata(assembler, r.total_chunks, r.total_size, r.chunk_size, slot + r.name_off,
+      const int nw = (int)pos.size();
+      int64_t stride = 16;
+      if (nw) {
+        stride = amod_payload_stride(cfg, maxlen);
+        S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
+        S_TRY(d_len.alloc(sizeof(int32_t) * nw));
+        S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
+        S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
+        S_TRY(d_res.alloc(sizeof(amod_result) * nw));
+        S_TRY(d_pay.alloc((size_t)stride * nw));
+        S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+        S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
+        S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+        S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
+        S_TRY(amod_launch_window(d_y.as<float>(), npad, d_pos.as<int64_t>(), d_len.as<int32_t>(),
+                                 d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
+        int rc = amod_reserve(ctx, cfg, nw, maxlen);
+        if (rc) return rc;
+        rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(),
+                                d_len.as<int32_t>(), nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
+        if (rc) return rc;
+        hres.resize(nw);
+        hpay.resize((size_t)stride * nw);
+        S_TRY(hipMemcpyAsync(hres.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
+        S_TRY(hipMemcpyAsync(hpay.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
+        S_TRY(hipStreamSynchronize(s));
+      }
+      for (size_t i = c0; i < c1; ++i) {
+        FrameEv &ev = fr[i];
+        amod_result r{};
+        if (ev.lost) {
+          r.status = AMOD_E_STREAM_LOST; r.preamble_idx = -1; r.coarse_idx = -1; r.frame_type = -1;
+        } else {
+          r = hres[slot[i - c0]];
+        }
+        if (nfr < max_frames) {
+          amod_stream_frame &f = frames[nfr];
+          f.pos = ev.pos; f.end = ev.end; f.window_len = ev.lost ? 0 : (int32_t)(ev.end - ev.pos); f.reserved = 0;
+          f.result = r;
+        }
+        ++nfr;
+        if (r.status != AMOD_OK) { ++frame_errors; continue; }
+        ++frames_decoded;
+        const uint8_t *sl = ev.lost ? nullptr : hpay.data() + (size_t)stride * slot[i - c0];
+        if (r.frame_type == 0xFE) {
+          if (!r.crc_valid) { ++frame_errors; continue; }
+          const int m = amod_asm_metadata(assembler, r.total_chunks, r.total_size, r.chunk_size, sl + r.name_off,
                                           r.name_len);
-          // the header fields are assigned even when the bitmap allocation throws
-          amod_asm_info inf;
+          amod_asm_info inf; // the header fields are assigned even when the bitmap allocation throws
           amod_asm_state(assembler, &inf);
-          bool meta = after.meta_received;
+          bool meta = ev.after.meta_received;
           if (m == AMOD_ASM_RANGE_ERROR) ++frame_errors; // caught by the receiver; metaReceived unchanged
           else meta = true;
-          const bool changed = meta != after.meta_received || (meta && inf.chunk_size != after.chunk_size);
-          after.meta_received = meta;
-          after.chunk_size = inf.chunk_size;
-          if (changed) {
-            rollback = i;
-            if (i + 1 < nw) { ++i; break; }
+          const bool chg = meta != ev.after.meta_received || (meta && inf.chunk_size != ev.after.chunk_size);
+          ev.after.meta_received = meta;
+          ev.after.chunk_size = inf.chunk_size;
+          if (chg) {
+            changed = (int64_t)i;
+            t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+            return AMOD_SUCCESS;
           }
-        } else {
-          ++frame_errors;
+        } else if (r.frame_type == 0xFF) {
+          const int c = amod_asm_chunk(assembler, r.seq_num, sl + r.data_off, r.data_len, r.crc_valid);
+          if (c < 0) return amod_ctx_fail(ctx, "assembler store", c);
         }
-      } else if (r.frame_type == 0xFF) {
-        const uint8_t *slot = hpay.data() + (size_t)stride * i;
-        const int c = amod_asm_chunk(assembler, r.seq_num, slot + r.data_off, r.data_len, r.crc_valid);
-        if (c < 0) return amod_ctx_fail(ctx, "assembler store", c);
       }
+      t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     }
-    (void)i;
-    t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     return AMOD_SUCCESS;
   };
 
-  rx.st.block = 0;
+  RxState st{};
   {
     amod_asm_info inf;
     amod_asm_state(assembler, &inf);
-    rx.st.chunk_size = inf.chunk_size; // this.assembler.chunkSize as the receiver starts
+    st.chunk_size = inf.chunk_size; // this.assembler.chunkSize as the receiver starts
   }
-  while (rx.st.block < nblocks) {
-    // processAudioBlock (app.js:749-773): the block is written, then one state step
-    switch (rx.st.state) {
-    case IDLE: rx.scan(); break;
-    case DETECTED: rx.refine(); break;
-    case COLLECTING:
-      if (rx.tw() >= rx.st.frame_end) {
-        // _demodulateFrame (app.js:907-972)
-        const int64_t len = rx.st.frame_end - rx.st.pre_pos;
-        const bool lost = rx.st.pre_pos < rx.tw() - rx.cap; // getRange: already overwritten
-        if (lost) {
-          if (nfr < max_frames) {
-            amod_stream_frame &f = frames[nfr];
-            std::memset(&f, 0, sizeof f);
-            f.pos = rx.st.pre_pos; f.end = rx.st.frame_end; f.window_len = 0;
-            f.result.status = AMOD_E_STREAM_LOST;
-            f.result.preamble_idx = -1; f.result.coarse_idx = -1; f.result.frame_type = -1;
-          }
-          ++nfr;
-          ++frame_errors;
-          rx.reset();
-        } else {
-          Pending p{rx.st.pre_pos, rx.st.frame_end, len, RxState{}};
-          rx.reset();
-          p.after = rx.st;
-          p.after.block = rx.st.block + 1;
-          pend.push_back(p);
-          // before the metadata frame every frame is decoded at once: its result decides
-          // the window length of the next one
-          if (!rx.st.meta_received || (int)pend.size() >= kBatch) {
-            int64_t rb;
-            const int rc = flush(rb);
-            if (rc) return rc;
-            const RxState resume = rb >= 0 ? pend[rb].after : pend.back().after;
-            pend.clear();
-            rx.st = resume;
-            continue;
-          }
-        }
-      }
-      break;
+  RxState final_state = st;
+  for (;;) {
+    Traj tr;
+    if (!st.meta_received) {
+      // before the metadata frame each window decides the next one's length: one at a time
+      Receiver rx = proto;
+      run_blocks(rx, st, nblocks, true, nullptr, tr, nullptr);
+      fine_host += rx.fine_host;
+    } else {
+      tr = run_parallel(proto, st, nblocks, nthreads, fine_host);
     }
-    ++rx.st.block;
-    if (rx.st.block >= nblocks && !pend.empty()) {
-      int64_t rb;
-      const int rc = flush(rb);
-      if (rc) return rc;
-      if (rb >= 0) { // the window length changed after frame rb: redo what followed it
-        const RxState resume = pend[rb].after;
-        pend.clear();
-        rx.st = resume;
-      } else {
-        pend.clear();
-      }
+    int64_t chg = -1;
+    const int rc = decode_dispatch(tr.frames, 0, tr.frames.size(), chg);
+    if (rc) return rc;
+    if (chg >= 0) {
+      // keep what happened up to that frame; re-run the rest with the new window length
+      const RxState after = tr.frames[chg].after;
+      for (auto &f : tr.fails)
+        if (f.first < after.block) fails_out.push_back(f.second);
+      st = after;
+      continue;
     }
+    for (auto &f : tr.fails) fails_out.push_back(f.second);
+    if (!tr.frames.empty() && tr.end.block < nblocks) { // first_only stop: continue from there
+      st = tr.end;
+      continue;
+    }
+    final_state = tr.end;
+    break;
   }
+  for (size_t i = 0; i < fails_out.size() && (int64_t)i < max_refine_fail; ++i) refine_fail[i] = fails_out[i];
   *nframes_out = nfr;
-  for (size_t i = 0; i < rx.refine_fail.size() && (int64_t)i < max_refine_fail; ++i) refine_fail[i] = rx.refine_fail[i];
   for (auto &e : ev) (void)hipEventDestroy(e);
   if (stats) {
     stt.nframes = nfr;
-    stt.nrefine_fail = (int64_t)rx.refine_fail.size();
+    stt.nrefine_fail = (int64_t)fails_out.size();
     stt.frames_decoded = frames_decoded;
     stt.frame_errors = frame_errors;
-    stt.final_state = rx.st.state;
-    stt.final_scan_pos = rx.st.ac_pos;
-    stt.fine_host_positions = rx.fine_host;
+    stt.final_state = final_state.state;
+    stt.final_scan_pos = final_state.ac_pos;
+    stt.fine_host_positions = fine_host;
     stt.t_decode_ms = t_decode;
     stt.t_total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
     stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - t_decode;

@@ -133,3 +133,59 @@ def test_c4_shaped_stream_round_trip():
     assert frames["result"]["seq_num"][1:].tolist() == list(range(n))
     assert stats["frames_decoded"] == n + 1 and stats["frame_errors"] == 0 and stats["ema_chunks_fixed"] == 0
     assert asm.is_complete() and asm.assemble_file() == data
+
+
+def _run(cfg, x, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        dm = amodem.Demodulator(0)
+        asm = amodem.ChunkAssembler()
+        fr, rf, st = dm.stream_receive(cfg, x, asm)
+        dm.close()
+        return fr, rf, st, asm.state(), (asm.assemble_file() if asm.is_complete() else None)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("sp", [s for s in streams() if s["name"] in ("qpsk_dc_gain_lead", "qam16_noise20",
+                                                                         "qpsk_corrupt_retransmit")],
+                         ids=lambda s: s["name"])
+def test_speculative_segments_match_sequential(sp):
+    """The host receiver's speculative segments (boundaries every 2 blocks, 16 threads)
+    reproduce the plain sequential receiver exactly on the golden streams, whose
+    reference outcomes test_stream_matches_reference pins."""
+    cfg, x, _ = build_stream(sp)
+    seq = _run(cfg, x, {"AMOD_STREAM_THREADS": "1"})
+    par = _run(cfg, x, {"AMOD_STREAM_THREADS": "16", "AMOD_STREAM_MINSEG": "2"})
+    assert np.array_equal(seq[0], par[0]) and seq[1] == par[1]
+    keys = ("nframes", "nrefine_fail", "frames_decoded", "frame_errors", "final_state", "final_scan_pos")
+    assert [seq[2][k] for k in keys] == [par[2][k] for k in keys]
+    assert seq[3] == par[3] and seq[4] == par[4]
+
+
+def test_speculative_long_noisy_stream():
+    """A 120-chunk stream with gaps, a DC step, AWGN and two corrupted chunks: sequential
+    and speculative-parallel receivers agree frame for frame."""
+    cfg = amodem.preset("standard", "QPSK", 1)
+    data = amodem.synth_payload(0x77, 120 * 1024)
+    parts = [np.zeros(5000, np.float32), amodem.build_metadata_frame(120, len(data), 1024, "long.bin", cfg=cfg)]
+    for i in range(120):
+        f = amodem.build_data_chunk_frame(data[i * 1024:(i + 1) * 1024], i, cfg=cfg)
+        if i in (17, 88):
+            f = f.copy()
+            f[5000:5300] = np.float32(0.7)
+        parts.append(f)
+        parts.append(np.zeros((i * 977) % 6000, np.float32))
+    x = np.concatenate(parts + [np.zeros(20000, np.float32)])
+    x = np.concatenate([x, np.zeros(-len(x) % 4096, np.float32)])
+    x[len(x) // 2:] = (x[len(x) // 2:].astype(np.float64) + 0.05).astype(np.float32)
+    x = O.apply_post(x, [{"op": "noise", "snr": 30, "seed": 0x1234}])
+    seq = _run(cfg, x, {"AMOD_STREAM_THREADS": "1"})
+    par = _run(cfg, x, {"AMOD_STREAM_THREADS": "16", "AMOD_STREAM_MINSEG": "3"})
+    assert len(seq[0]) >= 100
+    assert np.array_equal(seq[0], par[0]) and seq[1] == par[1] and seq[3] == par[3] and seq[4] == par[4]
