@@ -73,6 +73,16 @@ class StreamFrame(C.Structure):
                 ("result", Result)]
 
 
+class StreamState(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("block", "ac_pos", "pre_pos", "frame_end")] + \
+               [(n, C.c_double) for n in ("ac_p", "ac_ra", "ac_rb")] + \
+               [(n, C.c_int32) for n in ("state", "ac_init", "meta_received", "chunk_size")]
+
+
+class StreamEvent(C.Structure):
+    _fields_ = [("frame", StreamFrame), ("after", StreamState)]
+
+
 class StreamStats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in ("nframes", "nrefine_fail", "frames_decoded", "frame_errors", "final_state",
                                           "final_scan_pos", "ema_chunks_fixed", "fine_host_positions")] + \
@@ -128,6 +138,10 @@ SIGNATURES = {
     "amod_asm_file": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_stream_receive": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, C.c_int64, C.POINTER(C.c_int64),
                                       _P, C.c_int64, C.POINTER(StreamStats)]),
+    "amod_stream_shard": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                    C.POINTER(StreamState), C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64,
+                                    C.POINTER(C.c_int64), _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_int64), _P,
+                                    C.POINTER(StreamState)]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),

@@ -228,6 +228,33 @@ class Demodulator:
         stats = {k: getattr(st, k) for k, _ in L.StreamStats._fields_}
         return frames[:min(n.value, max_frames)], rf[:min(st.nrefine_fail, len(rf))].tolist(), stats
 
+    def stream_shard(self, cfg: L.Cfg, samples: np.ndarray, lo: int, hi: int, own_lo: int, own_hi: int,
+                     start: "L.StreamState | None" = None, meta_received: bool = False, chunk_size: int = 0,
+                     until_meta: bool = False, stride: int = 0, max_events: int = 1 << 18):
+        """One shard of a sharded stream receive (amod_stream_shard): samples = stream
+        samples [lo, hi). Returns (events: list of (StreamEvent copy), payload uint8
+        [n, stride], fails: list of (block, pos), ema: (state before own_lo, state at
+        own_hi - 1), end: StreamState)."""
+        x = np.ascontiguousarray(samples, np.float32)
+        assert len(x) == hi - lo
+        stride = stride or payload_stride(cfg, 1 << 20)
+        ev = (L.StreamEvent * max_events)()
+        pay = np.zeros((max_events, stride), np.uint8)
+        nev, nf = C.c_int64(), C.c_int64()
+        fails = np.zeros(2 * 4096, np.int64)
+        ema = np.zeros(2, np.float64)
+        end = L.StreamState()
+        with self._lock:
+            L.check(self._L.amod_stream_shard(self.ctx, C.byref(cfg), x.ctypes.data, lo, hi, own_lo, own_hi,
+                                              C.byref(start) if start is not None else None, int(meta_received),
+                                              int(chunk_size), int(until_meta), ev, max_events, C.byref(nev),
+                                              pay.ctypes.data, stride, fails.ctypes.data, 4096, C.byref(nf),
+                                              ema.ctypes.data, C.byref(end)), self.ctx)
+        n = min(nev.value, max_events)
+        events = [L.StreamEvent.from_buffer_copy(ev[i]) for i in range(n)]
+        fl = [(int(fails[2 * i]), int(fails[2 * i + 1])) for i in range(min(nf.value, 4096))]
+        return events, pay[:n], fl, (float(ema[0]), float(ema[1])), end
+
     # ------------------------------------------------------------ transmitter
     def transmit_device(self, cfg: L.Cfg, packets_ptr: int, pkt_off_ptr: int, pkt_len_ptr: int, pre_ptr: int,
                         post_ptr: int, nframes: int, out_ptr: int, out_off_ptr: int, stream: int = 0):

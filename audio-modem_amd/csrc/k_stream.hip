@@ -74,7 +74,7 @@ __global__ __launch_bounds__(64) void k_ema(const float *__restrict__ x, int64_t
 }
 
 __global__ void k_ema_fix(const float *__restrict__ x, int64_t n, int64_t L, float *__restrict__ y,
-                          const double *__restrict__ warm, const double *__restrict__ end, int64_t nchunks,
+                          const double *__restrict__ warm, double *__restrict__ end, int64_t nchunks,
                           unsigned long long *__restrict__ fixed) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double prev = end[0];
@@ -91,6 +91,7 @@ __global__ void k_ema_fix(const float *__restrict__ x, int64_t n, int64_t L, flo
       y[i] = (float)((double)x[i] - m);
     }
     prev = m;
+    end[t] = m; // the chunk's true end state (read back by sharded receivers)
     ++nf;
   }
   *fixed = nf;

@@ -92,7 +92,7 @@ struct FineTable {
 
 struct Receiver {
   const amod_cfg *cfg;
-  int64_t n = 0, npad = 0, cap = 0;
+  int64_t lo = 0, nloc = 0, cap = 0; // y[i] is stream sample lo + i, i < nloc
   const float *y = nullptr; // cleaned stream (host)
   std::vector<float> pre1;
   double pre1_energy = 0;
@@ -102,7 +102,7 @@ struct Receiver {
   int64_t fine_host = 0; // positions the host had to correlate itself
   size_t cursor = 0;     // FineTable lookup cursor
 
-  double S(int64_t i) const { return (i >= 0 && i < npad) ? (double)y[i] : 0.0; }
+  double S(int64_t i) const { return (i >= lo && i < lo + nloc) ? (double)y[i - lo] : 0.0; }
   int64_t tw() const { return (st.block + 1) * kBlock; } // totalWritten after this block's write
 
   // _scanForPreamble (app.js:775-847)
@@ -307,6 +307,209 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
   return total;
 }
 
+struct Pinned {
+  float *p = nullptr;
+  ~Pinned() { if (p) (void)hipHostFree(p); }
+};
+
+// The GPU part before the state machine, over stream samples [lo, lo + n) given on the
+// host (n a multiple of kBlock; lo a multiple of kEmaChunk): exact DC removal (EMA
+// started at lo), screening, fine sums, pinned host copy of the cleaned samples.
+struct Prepass {
+  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot, d_ze;
+  Pinned yh;
+  FineTable ft;
+  int64_t lo = 0, n = 0, fixed = 0;
+  std::vector<double> ema_end; // EMA state after each k_ema chunk (true states)
+  double t_ema = 0, t_fine = 0;
+
+  int run(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t nvalid, int64_t lo_, int64_t n_,
+          hipStream_t s) {
+    lo = lo_; n = n_;
+    const int64_t nchunks = std::max<int64_t>(1, (n + kEmaChunk - 1) / kEmaChunk);
+    S_TRY(d_x.alloc(sizeof(float) * (size_t)n + 64));
+    S_TRY(d_y.alloc(sizeof(float) * (size_t)n + 64));
+    S_TRY(d_warm.alloc(sizeof(double) * nchunks));
+    S_TRY(d_end.alloc(sizeof(double) * nchunks));
+    S_TRY(d_fixed.alloc(8));
+    S_TRY(d_hot.alloc((size_t)(n / 32 + 1)));
+    S_TRY(d_ze.alloc(sizeof(double2) * (size_t)(n / 32 + 1)));
+    if (n) {
+      S_TRY(hipMemsetAsync(d_x.p, 0, sizeof(float) * (size_t)n, s));
+      if (nvalid) S_TRY(hipMemcpyAsync(d_x.p, samples, sizeof(float) * (size_t)nvalid, hipMemcpyHostToDevice, s));
+    }
+    hipEvent_t ev[3];
+    for (auto &e : ev) S_TRY(hipEventCreate(&e));
+    S_TRY(hipEventRecord(ev[0], s));
+    S_TRY(amod_launch_ema(d_x.as<float>(), n, kEmaChunk, kEmaWarm, d_y.as<float>(), d_warm.as<double>(),
+                          d_end.as<double>(), d_fixed.as<unsigned long long>(), s));
+    S_TRY(hipEventRecord(ev[1], s));
+    S_TRY(amod_launch_sc_screen(d_y.as<float>(), n, 0.25f, d_ze.as<double2>(), d_hot.as<uint8_t>(), s));
+    std::vector<uint8_t> hot((size_t)(n / 32));
+    if (!hot.empty()) S_TRY(hipMemcpyAsync(hot.data(), d_hot.p, hot.size(), hipMemcpyDeviceToHost, s));
+    ema_end.resize(nchunks);
+    S_TRY(hipStreamSynchronize(s));
+    unsigned long long fx = 0;
+    S_TRY(hipMemcpy(&fx, d_fixed.p, 8, hipMemcpyDeviceToHost));
+    S_TRY(hipMemcpy(ema_end.data(), d_end.p, sizeof(double) * nchunks, hipMemcpyDeviceToHost));
+    fixed = (int64_t)fx;
+    // fine ranges (local positions): every position within 448 samples of a hot block
+    const int64_t pad = 448;
+    int64_t rlo = -1, rhi = -1, total = 0;
+    std::vector<int64_t> first_loc;
+    auto flush = [&]() {
+      first_loc.push_back(rlo); ft.first.push_back(lo + rlo); ft.count.push_back(rhi - rlo + 1);
+      ft.base.push_back(total);
+      total += rhi - rlo + 1;
+    };
+    bool open = false;
+    for (int64_t b = 0; b < (int64_t)hot.size(); ++b) {
+      if (!hot[b]) continue;
+      const int64_t za = 32 * b - pad, zb = 32 * b + 31 + pad;
+      if (open && za <= rhi + 1) rhi = std::max(rhi, zb);
+      else { if (open) flush(); rlo = za; rhi = zb; open = true; }
+    }
+    if (open) flush();
+    ft.corr_se.assign(2 * (size_t)total, 0.0);
+    if (total) {
+      DBuf d_pre1, d_first, d_base, d_count, d_out;
+      std::vector<float> p1(cfg->symbol_len);
+      amod_preamble1(cfg, p1.data());
+      const int nr = (int)first_loc.size();
+      S_TRY(d_pre1.alloc(sizeof(float) * p1.size()));
+      S_TRY(d_first.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_base.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_count.alloc(sizeof(int64_t) * nr));
+      S_TRY(d_out.alloc(sizeof(double) * 2 * (size_t)total));
+      S_TRY(hipMemcpyAsync(d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_first.p, first_loc.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
+      for (int r0 = 0; r0 < nr; r0 += 65535) {
+        const int k = std::min(65535, nr - r0);
+        S_TRY(amod_launch_fine(d_y.as<float>(), n, d_pre1.as<float>(), cfg->symbol_len, d_first.as<int64_t>() + r0,
+                               d_base.as<int64_t>() + r0, d_count.as<int64_t>() + r0, k, maxc, d_out.as<double2>(), s));
+      }
+      S_TRY(hipMemcpyAsync(ft.corr_se.data(), d_out.p, sizeof(double) * 2 * (size_t)total, hipMemcpyDeviceToHost, s));
+    }
+    S_TRY(hipEventRecord(ev[2], s));
+    S_TRY(hipHostMalloc((void **)&yh.p, sizeof(float) * (size_t)std::max<int64_t>(n, 1), hipHostMallocDefault));
+    if (n) S_TRY(hipMemcpyAsync(yh.p, d_y.p, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s));
+    S_TRY(hipStreamSynchronize(s));
+    float ta = 0, tb = 0;
+    S_TRY(hipEventElapsedTime(&ta, ev[0], ev[1]));
+    S_TRY(hipEventElapsedTime(&tb, ev[1], ev[2]));
+    t_ema = ta; t_fine = tb;
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    return AMOD_SUCCESS;
+  }
+
+  Receiver receiver(const amod_cfg *cfg) const {
+    Receiver rx;
+    rx.cfg = cfg;
+    rx.lo = lo; rx.nloc = n; rx.y = yh.p; rx.fine = &ft;
+    rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
+    rx.pre1.resize(cfg->symbol_len);
+    amod_preamble1(cfg, rx.pre1.data());
+    for (float v : rx.pre1) rx.pre1_energy += (double)v * (double)v;
+    return rx;
+  }
+};
+
+// Decodes frames' windows on the GPU (k_window peak normalisation + chunk-mode decode);
+// res[i] / payload row i for frame i (lost frames get AMOD_E_STREAM_LOST).
+struct WindowDecoder {
+  DBuf d_pos, d_len, d_woff, d_win, d_res, d_pay;
+  std::vector<amod_result> res;
+  std::vector<uint8_t> pay;
+  int64_t stride = 16;
+  double t_ms = 0;
+
+  int run(amod_ctx *ctx, const amod_cfg *cfg, const Prepass &pp, const std::vector<FrameEv> &fr, size_t a, size_t b,
+          hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<int64_t> pos, woff;
+    std::vector<int32_t> len;
+    std::vector<int> slot(b - a, -1);
+    int64_t tot = 0, maxlen = 0;
+    for (size_t i = a; i < b; ++i) {
+      if (fr[i].lost) continue;
+      slot[i - a] = (int)pos.size();
+      const int64_t L = fr[i].end - fr[i].pos;
+      pos.push_back(fr[i].pos - pp.lo); len.push_back((int32_t)L); woff.push_back(tot);
+      tot += (L + 3) & ~int64_t(3);
+      maxlen = std::max(maxlen, L);
+    }
+    const int nw = (int)pos.size();
+    stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
+    std::vector<amod_result> r(nw);
+    std::vector<uint8_t> py((size_t)stride * nw);
+    if (nw) {
+      S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
+      S_TRY(d_len.alloc(sizeof(int32_t) * nw));
+      S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
+      S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
+      S_TRY(d_res.alloc(sizeof(amod_result) * nw));
+      S_TRY(d_pay.alloc((size_t)stride * nw));
+      S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
+      S_TRY(amod_launch_window(pp.d_y.as<float>(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
+                               d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
+      int rc = amod_reserve(ctx, cfg, nw, maxlen);
+      if (rc) return rc;
+      rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
+                              nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
+      if (rc) return rc;
+      S_TRY(hipMemcpyAsync(r.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
+      S_TRY(hipMemcpyAsync(py.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
+      S_TRY(hipStreamSynchronize(s));
+    }
+    res.assign(b - a, amod_result{});
+    pay.assign((size_t)stride * (b - a), 0);
+    for (size_t i = a; i < b; ++i) {
+      amod_result &o = res[i - a];
+      if (slot[i - a] < 0) {
+        o.status = AMOD_E_STREAM_LOST; o.preamble_idx = -1; o.coarse_idx = -1; o.frame_type = -1;
+      } else {
+        o = r[slot[i - a]];
+        std::memcpy(pay.data() + (size_t)stride * (i - a), py.data() + (size_t)stride * slot[i - a], (size_t)stride);
+      }
+    }
+    t_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return AMOD_SUCCESS;
+  }
+};
+
+// What a decoded metadata result does to the receiver's window length
+// (_demodulateFrame -> handleMetadataFrame, app.js:926-940): chunkSize is assigned even
+// when the bitmap allocation throws (totalChunks <= -8), metaReceived only without it.
+void apply_meta(const amod_result &r, RxState &after) {
+  if (r.status != AMOD_OK || r.frame_type != 0xFE || !r.crc_valid) return;
+  after.chunk_size = r.chunk_size;
+  if (r.total_chunks > -8) after.meta_received = true;
+}
+
+int receiver_threads() {
+  const char *tenv = getenv("AMOD_STREAM_THREADS"); // tests: 1 = the plain sequential receiver
+  return tenv ? std::max(1, atoi(tenv)) : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+void to_state(const RxState &a, amod_stream_state &o) {
+  o.block = a.block; o.ac_pos = a.ac_pos; o.pre_pos = a.pre_pos; o.frame_end = a.frame_end;
+  o.ac_p = a.ac_p; o.ac_ra = a.ac_ra; o.ac_rb = a.ac_rb;
+  o.state = a.state; o.ac_init = a.ac_init; o.meta_received = a.meta_received; o.chunk_size = a.chunk_size;
+}
+RxState from_state(const amod_stream_state &o) {
+  RxState a;
+  a.block = o.block; a.ac_pos = o.ac_pos; a.pre_pos = o.pre_pos; a.frame_end = o.frame_end;
+  a.ac_p = o.ac_p; a.ac_ra = o.ac_ra; a.ac_rb = o.ac_rb;
+  a.state = o.state; a.ac_init = o.ac_init != 0; a.meta_received = o.meta_received != 0; a.chunk_size = o.chunk_size;
+  return a;
+}
+
 } // namespace
 
 extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
@@ -321,91 +524,14 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   hipStream_t s = amod_ctx_stream(ctx);
   const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
   amod_stream_stats stt{};
-  // ---- GPU: DC removal (exact), screening, fine sums
-  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot, d_ze;
-  const int64_t nchunks = std::max<int64_t>(1, (npad + kEmaChunk - 1) / kEmaChunk);
-  S_TRY(d_x.alloc(sizeof(float) * (size_t)npad + 64));
-  S_TRY(d_y.alloc(sizeof(float) * (size_t)npad + 64));
-  S_TRY(d_warm.alloc(sizeof(double) * nchunks));
-  S_TRY(d_end.alloc(sizeof(double) * nchunks));
-  S_TRY(d_fixed.alloc(8));
-  S_TRY(d_hot.alloc((size_t)(npad / 32 + 1)));
-  S_TRY(d_ze.alloc(sizeof(double2) * (size_t)(npad / 32 + 1)));
-  if (npad) {
-    S_TRY(hipMemsetAsync(d_x.p, 0, sizeof(float) * (size_t)npad, s));
-    if (n) S_TRY(hipMemcpyAsync(d_x.p, samples, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
-  }
-  hipEvent_t ev[4];
-  for (auto &e : ev) S_TRY(hipEventCreate(&e));
-  S_TRY(hipEventRecord(ev[0], s));
-  S_TRY(amod_launch_ema(d_x.as<float>(), npad, kEmaChunk, kEmaWarm, d_y.as<float>(), d_warm.as<double>(),
-                        d_end.as<double>(), d_fixed.as<unsigned long long>(), s));
-  S_TRY(hipEventRecord(ev[1], s));
-  S_TRY(amod_launch_sc_screen(d_y.as<float>(), npad, 0.25f, d_ze.as<double2>(), d_hot.as<uint8_t>(), s));
-  std::vector<uint8_t> hot((size_t)(npad / 32));
-  if (!hot.empty()) S_TRY(hipMemcpyAsync(hot.data(), d_hot.p, hot.size(), hipMemcpyDeviceToHost, s));
-  S_TRY(hipStreamSynchronize(s));
-  unsigned long long fixed = 0;
-  S_TRY(hipMemcpy(&fixed, d_fixed.p, 8, hipMemcpyDeviceToHost));
-  stt.ema_chunks_fixed = (int64_t)fixed;
-  // fine ranges: every position within 448 samples of a hot block
-  FineTable ft;
+  Prepass pp;
   {
-    const int64_t pad = 448;
-    int64_t lo = -1, hi = -1, total = 0;
-    auto flush = [&]() {
-      if (lo < 0 && hi < 0) return;
-      ft.first.push_back(lo); ft.count.push_back(hi - lo + 1); ft.base.push_back(total);
-      total += hi - lo + 1;
-    };
-    bool open = false;
-    for (int64_t b = 0; b < (int64_t)hot.size(); ++b) {
-      if (!hot[b]) continue;
-      const int64_t a = 32 * b - pad, z = 32 * b + 31 + pad;
-      if (open && a <= hi + 1) hi = std::max(hi, z);
-      else { if (open) flush(); lo = a; hi = z; open = true; }
-    }
-    if (open) flush();
-    ft.corr_se.assign(2 * (size_t)total, 0.0);
-    if (total) {
-      DBuf d_pre1, d_first, d_base, d_count, d_out;
-      std::vector<float> p1(cfg->symbol_len);
-      amod_preamble1(cfg, p1.data());
-      const int nr = (int)ft.first.size();
-      S_TRY(d_pre1.alloc(sizeof(float) * p1.size()));
-      S_TRY(d_first.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_base.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_count.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_out.alloc(sizeof(double) * 2 * (size_t)total));
-      S_TRY(hipMemcpyAsync(d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_first.p, ft.first.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
-      for (int r0 = 0; r0 < nr; r0 += 65535) {
-        const int k = std::min(65535, nr - r0);
-        S_TRY(amod_launch_fine(d_y.as<float>(), npad, d_pre1.as<float>(), cfg->symbol_len, d_first.as<int64_t>() + r0,
-                               d_base.as<int64_t>() + r0, d_count.as<int64_t>() + r0, k, maxc, d_out.as<double2>(), s));
-      }
-      S_TRY(hipMemcpyAsync(ft.corr_se.data(), d_out.p, sizeof(double) * 2 * (size_t)total, hipMemcpyDeviceToHost, s));
-    }
+    const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s);
+    if (rc) return rc;
   }
-  S_TRY(hipEventRecord(ev[2], s));
-  // the state machine reads the cleaned stream on the host
-  struct Pinned {
-    float *p = nullptr;
-    ~Pinned() { if (p) (void)hipHostFree(p); }
-  } yh;
-  S_TRY(hipHostMalloc((void **)&yh.p, sizeof(float) * (size_t)std::max<int64_t>(npad, 1), hipHostMallocDefault));
-  if (npad) S_TRY(hipMemcpyAsync(yh.p, d_y.p, sizeof(float) * (size_t)npad, hipMemcpyDeviceToHost, s));
-  S_TRY(hipStreamSynchronize(s));
-  {
-    float a = 0, b = 0;
-    S_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-    S_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
-    stt.t_ema_ms = a;
-    stt.t_fine_ms = b;
-  }
+  stt.ema_chunks_fixed = pp.fixed;
+  stt.t_ema_ms = pp.t_ema;
+  stt.t_fine_ms = pp.t_fine;
   const auto t_gpu_pre = clk::now();
 
   // ---- host: the receiver
@@ -415,80 +541,24 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
     assembler = own;
   }
   struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
-  Receiver proto;
-  proto.cfg = cfg;
-  proto.n = n; proto.npad = npad; proto.y = yh.p; proto.fine = &ft;
-  proto.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
-  proto.pre1.resize(cfg->symbol_len);
-  amod_preamble1(cfg, proto.pre1.data());
-  for (float v : proto.pre1) proto.pre1_energy += (double)v * (double)v;
-  const char *tenv = getenv("AMOD_STREAM_THREADS"); // tests: 1 = the plain sequential receiver
-  const int nthreads = tenv ? std::max(1, atoi(tenv))
-                            : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-
+  const Receiver proto = pp.receiver(cfg);
+  const int nthreads = receiver_threads();
   int64_t nfr = 0, frames_decoded = 0, frame_errors = 0, fine_host = 0;
   std::vector<int64_t> fails_out;
-  double t_decode = 0;
-  DBuf d_pos, d_len, d_woff, d_win, d_res, d_pay;
-  std::vector<amod_result> hres;
-  std::vector<uint8_t> hpay;
+  WindowDecoder wd;
 
-  // decode frames[a, b) (windows on the GPU) and dispatch them in order
-  // (_demodulateFrame, app.js:907-972); returns the index of the first frame whose
-  // metadata result changed the window length of what follows (its `after` updated),
-  // or -1
+  // decode frames[a, b) and dispatch them in order (_demodulateFrame, app.js:907-972);
+  // `changed`: the first frame whose metadata result changed the window length of what
+  // follows (its `after` updated), or -1
   auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
     changed = -1;
     for (size_t c0 = a; c0 < b; c0 += kBatch) {
       const size_t c1 = std::min(b, c0 + (size_t)kBatch);
-      const auto t0 = clk::now();
-      std::vector<int64_t> pos, woff;
-      std::vector<int32_t> len;
-      std::vector<int> slot(c1 - c0, -1);
-      int64_t tot = 0, maxlen = 0;
-      for (size_t i = c0; i < c1; ++i) {
-        if (fr[i].lost) continue;
-        slot[i - c0] = (int)pos.size();
-        const int64_t L = fr[i].end - fr[i].pos;
-        pos.push_back(fr[i].pos); len.push_back((int32_t)L); woff.push_back(tot);
-        tot += (L + 3) & ~int64_t(3);
-        maxlen = std::max(maxlen, L);
-      }
-      const int nw = (int)pos.size();
-      int64_t stride = 16;
-      if (nw) {
-        stride = amod_payload_stride(cfg, maxlen);
-        S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
-        S_TRY(d_len.alloc(sizeof(int32_t) * nw));
-        S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
-        S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
-        S_TRY(d_res.alloc(sizeof(amod_result) * nw));
-        S_TRY(d_pay.alloc((size_t)stride * nw));
-        S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-        S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
-        S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-        S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
-        S_TRY(amod_launch_window(d_y.as<float>(), npad, d_pos.as<int64_t>(), d_len.as<int32_t>(),
-                                 d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
-        int rc = amod_reserve(ctx, cfg, nw, maxlen);
-        if (rc) return rc;
-        rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(),
-                                d_len.as<int32_t>(), nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
-        if (rc) return rc;
-        hres.resize(nw);
-        hpay.resize((size_t)stride * nw);
-        S_TRY(hipMemcpyAsync(hres.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
-        S_TRY(hipMemcpyAsync(hpay.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
-        S_TRY(hipStreamSynchronize(s));
-      }
+      const int rc = wd.run(ctx, cfg, pp, fr, c0, c1, s);
+      if (rc) return rc;
       for (size_t i = c0; i < c1; ++i) {
         FrameEv &ev = fr[i];
-        amod_result r{};
-        if (ev.lost) {
-          r.status = AMOD_E_STREAM_LOST; r.preamble_idx = -1; r.coarse_idx = -1; r.frame_type = -1;
-        } else {
-          r = hres[slot[i - c0]];
-        }
+        const amod_result &r = wd.res[i - c0];
         if (nfr < max_frames) {
           amod_stream_frame &f = frames[nfr];
           f.pos = ev.pos; f.end = ev.end; f.window_len = ev.lost ? 0 : (int32_t)(ev.end - ev.pos); f.reserved = 0;
@@ -497,30 +567,23 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
         ++nfr;
         if (r.status != AMOD_OK) { ++frame_errors; continue; }
         ++frames_decoded;
-        const uint8_t *sl = ev.lost ? nullptr : hpay.data() + (size_t)stride * slot[i - c0];
+        const uint8_t *sl = wd.pay.data() + (size_t)wd.stride * (i - c0);
         if (r.frame_type == 0xFE) {
           if (!r.crc_valid) { ++frame_errors; continue; }
           const int m = amod_asm_metadata(assembler, r.total_chunks, r.total_size, r.chunk_size, sl + r.name_off,
                                           r.name_len);
-          amod_asm_info inf; // the header fields are assigned even when the bitmap allocation throws
-          amod_asm_state(assembler, &inf);
-          bool meta = ev.after.meta_received;
           if (m == AMOD_ASM_RANGE_ERROR) ++frame_errors; // caught by the receiver; metaReceived unchanged
-          else meta = true;
-          const bool chg = meta != ev.after.meta_received || (meta && inf.chunk_size != ev.after.chunk_size);
-          ev.after.meta_received = meta;
-          ev.after.chunk_size = inf.chunk_size;
-          if (chg) {
-            changed = (int64_t)i;
-            t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-            return AMOD_SUCCESS;
-          }
+          RxState upd = ev.after;
+          apply_meta(r, upd);
+          const bool chg = upd.meta_received != ev.after.meta_received ||
+                           (upd.meta_received && upd.chunk_size != ev.after.chunk_size);
+          ev.after = upd;
+          if (chg) { changed = (int64_t)i; return AMOD_SUCCESS; }
         } else if (r.frame_type == 0xFF) {
           const int c = amod_asm_chunk(assembler, r.seq_num, sl + r.data_off, r.data_len, r.crc_valid);
           if (c < 0) return amod_ctx_fail(ctx, "assembler store", c);
         }
       }
-      t_decode += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     }
     return AMOD_SUCCESS;
   };
@@ -563,7 +626,6 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   }
   for (size_t i = 0; i < fails_out.size() && (int64_t)i < max_refine_fail; ++i) refine_fail[i] = fails_out[i];
   *nframes_out = nfr;
-  for (auto &e : ev) (void)hipEventDestroy(e);
   if (stats) {
     stt.nframes = nfr;
     stt.nrefine_fail = (int64_t)fails_out.size();
@@ -572,10 +634,111 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
     stt.final_state = final_state.state;
     stt.final_scan_pos = final_state.ac_pos;
     stt.fine_host_positions = fine_host;
-    stt.t_decode_ms = t_decode;
+    stt.t_decode_ms = wd.t_ms;
     stt.t_total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
-    stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - t_decode;
+    stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - wd.t_ms;
     *stats = stt;
   }
+  return AMOD_SUCCESS;
+}
+
+extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t lo, int64_t hi,
+                                 int64_t own_lo, int64_t own_hi, const amod_stream_state *start, int32_t meta_received,
+                                 int32_t chunk_size, int32_t until_meta, amod_stream_event *events,
+                                 int64_t max_events, int64_t *nevents, uint8_t *payload, int64_t stride, int64_t *fails,
+                                 int64_t max_fails, int64_t *nfails, double *ema, amod_stream_state *end) {
+  if (!ctx || !cfg || lo < 0 || hi < lo || own_lo < lo || own_lo > hi || lo % kEmaChunk || hi % kBlock ||
+      own_lo % kBlock || (hi > lo && !samples) || !nevents || !nfails || (max_events > 0 && !events) ||
+      (max_events > 0 && payload && stride <= 0))
+    return amod_ctx_fail(ctx, "invalid shard arguments", AMOD_ERR_ARG);
+  S_TRY(hipSetDevice(amod_ctx_device(ctx)));
+  hipStream_t s = amod_ctx_stream(ctx);
+  Prepass pp;
+  {
+    const int rc = pp.run(ctx, cfg, samples, hi - lo, lo, hi - lo, s);
+    if (rc) return rc;
+  }
+  if (ema) {
+    auto state_after = [&](int64_t g) -> double { // EMA state after stream sample g (a chunk end)
+      const int64_t k = (g + 1 - lo) / kEmaChunk - 1;
+      return (k >= 0 && k < (int64_t)pp.ema_end.size() && (g + 1 - lo) % kEmaChunk == 0) ? pp.ema_end[k] : NAN;
+    };
+    ema[0] = own_lo > lo ? state_after(own_lo - 1) : NAN;
+    ema[1] = own_hi > lo ? state_after(own_hi - 1) : NAN;
+  }
+  RxState st;
+  if (start) {
+    st = from_state(*start);
+  } else {
+    st.block = own_lo / kBlock;
+    st.state = IDLE;
+    st.ac_pos = std::max<int64_t>(0, own_lo - 511); // where a continuous scan stands at this block
+  }
+  if (!start) { st.meta_received = meta_received != 0; st.chunk_size = chunk_size; }
+  const int64_t stop = hi / kBlock;
+  Traj tr;
+  int64_t fine_host = 0;
+  WindowDecoder wd;
+  std::vector<amod_result> res;
+  std::vector<uint8_t> pay;
+  if (until_meta) {
+    // one window at a time until a result makes the metadata state known
+    for (;;) {
+      Traj t1;
+      Receiver rx = pp.receiver(cfg);
+      run_blocks(rx, st, stop, true, nullptr, t1, nullptr);
+      tr.fails.insert(tr.fails.end(), t1.fails.begin(), t1.fails.end());
+      if (t1.frames.empty()) { tr.end = t1.end; break; }
+      const int rc = wd.run(ctx, cfg, pp, t1.frames, 0, 1, s);
+      if (rc) return rc;
+      apply_meta(wd.res[0], t1.frames[0].after);
+      tr.frames.push_back(t1.frames[0]);
+      res.push_back(wd.res[0]);
+      pay.insert(pay.end(), wd.pay.begin(), wd.pay.begin() + std::min<int64_t>(wd.stride, stride));
+      if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
+      st = t1.frames[0].after;
+      tr.end = st;
+      if (st.meta_received || st.block >= stop) break;
+    }
+  } else {
+    tr = run_parallel(pp.receiver(cfg), st, stop, receiver_threads(), fine_host);
+  }
+  *nevents = 0;
+  size_t first = 0;
+  while (first < tr.frames.size() && tr.frames[first].pos < own_lo) ++first; // owned by the previous shard
+  std::vector<FrameEv> fr(tr.frames.begin() + first, tr.frames.end());
+  if (until_meta) {
+    res.erase(res.begin(), res.begin() + first);
+    pay.erase(pay.begin(), pay.begin() + (size_t)stride * first);
+  } else {
+    for (size_t c0 = 0; c0 < fr.size(); c0 += kBatch) {
+      const size_t c1 = std::min(fr.size(), c0 + (size_t)kBatch);
+      const int rc = wd.run(ctx, cfg, pp, fr, c0, c1, s);
+      if (rc) return rc;
+      res.insert(res.end(), wd.res.begin(), wd.res.end());
+      for (size_t i = c0; i < c1; ++i) { // rows at the caller's stride
+        const uint8_t *row = wd.pay.data() + (size_t)wd.stride * (i - c0);
+        pay.insert(pay.end(), row, row + std::min<int64_t>(wd.stride, stride));
+        if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
+      }
+    }
+  }
+  for (size_t i = 0; i < fr.size(); ++i) {
+    if ((int64_t)i >= max_events) break;
+    amod_stream_event &e = events[i];
+    std::memset(&e, 0, sizeof e);
+    e.frame.pos = fr[i].pos; e.frame.end = fr[i].end;
+    e.frame.window_len = fr[i].lost ? 0 : (int32_t)(fr[i].end - fr[i].pos);
+    e.frame.result = res[i];
+    to_state(fr[i].after, e.after);
+    if (payload) std::memcpy(payload + (size_t)stride * i, pay.data() + (size_t)stride * i, (size_t)stride);
+  }
+  *nevents = (int64_t)fr.size();
+  *nfails = (int64_t)tr.fails.size();
+  for (size_t i = 0; i < tr.fails.size() && (int64_t)i < max_fails; ++i) {
+    fails[2 * i] = tr.fails[i].first;
+    fails[2 * i + 1] = tr.fails[i].second;
+  }
+  if (end) to_state(tr.end, *end);
   return AMOD_SUCCESS;
 }

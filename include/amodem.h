@@ -289,6 +289,36 @@ int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples
                         amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
                         int64_t *nframes, int64_t *refine_fail, int64_t max_refine_fail, amod_stream_stats *stats);
 
+/* ---- sharded streaming receive (one process per GPU, SURVEY §8e raw single stream) ----
+ * The receiver's state between blocks (StreamingReceiver fields): */
+typedef struct amod_stream_state {
+  int64_t block;                 /* next block to process                               */
+  int64_t ac_pos, pre_pos, frame_end;
+  double ac_p, ac_ra, ac_rb;
+  int32_t state, ac_init, meta_received, chunk_size;
+} amod_stream_state;
+/* one demodulated window of a shard's trajectory and the state right after it */
+typedef struct amod_stream_event {
+  amod_stream_frame frame;       /* pos, end, window_len, decodeChunkFrame result       */
+  amod_stream_state after;       /* after _resetToIdle, positioned at the next block     */
+} amod_stream_event;
+/* A shard holds stream samples [lo, hi) (host; lo a multiple of 8192, hi of 4096) and
+ * owns blocks from own_lo (a multiple of 4096). start == NULL: it starts speculatively
+ * at own_lo (IDLE, the scan resuming there) with the given metadata state; otherwise at
+ * *start (the true state, e.g. rank 0). until_meta: stop after the first window whose
+ * result makes the metadata state known (every window decoded as it comes). The run
+ * covers blocks up to hi, every window it demodulates at pos >= own_lo is decoded
+ * (payload rows of `stride` bytes), failed refinements go to fails as (block, pos)
+ * pairs. ema[0] / ema[1]: the DC-removal state after sample own_lo - 1 / own_hi - 1
+ * (own_hi a multiple of 8192; the neighbours' exactness check); *end: the state after the last block. Windows whose
+ * runs agree on a post-reset state continue identically; amodem/shard.py merges the
+ * shards' trajectories at such a window.                             */
+int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t lo, int64_t hi,
+                      int64_t own_lo, int64_t own_hi, const amod_stream_state *start, int32_t meta_received, int32_t chunk_size,
+                      int32_t until_meta, amod_stream_event *events, int64_t max_events, int64_t *nevents,
+                      uint8_t *payload, int64_t stride, int64_t *fails, int64_t max_fails, int64_t *nfails,
+                      double *ema, amod_stream_state *end);
+
 /* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
 void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
 /* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),

@@ -75,3 +75,56 @@ def test_gather_records_gloo_world2():
         assert status == list(range(n))            # rank order = frame order
         assert pidx == owner                       # each frame decoded by its owner
         assert p0 == [i & 0xFF for i in range(n)]  # payload rows follow their records
+
+
+def _ev(pos, end, block, ac_pos, status=0):
+    from amodem import _lib as L
+    e = L.StreamEvent()
+    e.frame.pos, e.frame.end, e.frame.window_len = pos, end, end - pos
+    e.frame.result.status = status
+    e.after.block, e.after.ac_pos, e.after.pre_pos, e.after.frame_end = block, ac_pos, -1, -1
+    e.after.meta_received, e.after.chunk_size = 1, 2048
+    return e
+
+
+def test_merge_trajectories_syncs_at_first_common_window():
+    """Shard 1 starts mid-frame (its first window is garbage) and meets the true run of
+    shard 0 at the window both demodulated from the same post-reset state."""
+    import numpy as np
+    from amodem import shard
+    row = lambda v: np.full(16, v, np.uint8)
+    s0 = {"own_lo": 0, "ema": (float("nan"), 1.5),
+          "events": [_ev(100, 900, 1, 900), _ev(1000, 1800, 2, 1800), _ev(2100, 2900, 3, 2900)],
+          "payload": [row(1), row(2), row(3)], "fails": [(0, 50), (2, 1950)]}
+    s1 = {"own_lo": 2000, "ema": (1.5, 2.5),
+          "events": [_ev(2050, 2850, 3, 2850), _ev(2100, 2900, 3, 2900), _ev(3100, 3900, 4, 3900)],
+          "payload": [row(9), row(33), row(4)], "fails": [(2, 2001), (3, 3050)]}
+    traj, fails, warn = shard.merge_trajectories([s0, s1])
+    assert [e.frame.pos for e, _ in traj] == [100, 1000, 2100, 3100]
+    assert [int(p[0]) for _, p in traj] == [1, 2, 3, 4]  # the sync window keeps shard 0's decode
+    assert fails == [(0, 50), (2, 1950), (3, 3050)] and warn == []
+
+
+def test_merge_trajectories_without_common_window_fails_loudly():
+    import numpy as np
+    import pytest as _pytest
+    from amodem import shard
+    s0 = {"own_lo": 0, "ema": (float("nan"), 1.0), "events": [_ev(100, 900, 1, 900)], "payload": [np.zeros(4)],
+          "fails": []}
+    s1 = {"own_lo": 2000, "ema": (2.0, 3.0), "events": [_ev(2100, 2900, 3, 2900)], "payload": [np.zeros(4)],
+          "fails": []}
+    with _pytest.raises(RuntimeError):
+        shard.merge_trajectories([s0, s1])
+
+
+def test_stream_bounds_cover_and_align():
+    from amodem import shard
+    for n, world in [(1, 1), (4096 * 7 + 5, 2), (10_000_000, 8), (123_456_789, 3)]:
+        b = shard.stream_bounds(n, world, 300_000)
+        npad = -(-n // 4096) * 4096
+        assert b[0][2] == 0 and b[-1][3] == npad
+        for r, (lo, hi, own_lo, own_hi) in enumerate(b):
+            assert lo % 8192 == 0 and own_lo % 8192 == 0 and hi % 4096 == 0
+            assert lo <= own_lo <= own_hi <= hi <= npad
+            if r:
+                assert own_lo == b[r - 1][3]
