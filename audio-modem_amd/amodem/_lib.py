@@ -19,6 +19,7 @@ MODS = {"BPSK": BPSK, "QPSK": QPSK, "QAM16": QAM16}
 MODE_RECEIVED, MODE_CHUNK, MODE_LOOPBACK = 0, 1, 2
 TX_LEGACY, TX_META, TX_CHUNK = 0, 1, 2
 OPT_FORCE_EXACT = 1
+OPT_SOFT_COMBINE = 2  # not reference behaviour: soft repetition combining (opt-in)
 
 OK = 0
 E_CAPACITY = 100

@@ -91,7 +91,16 @@ struct DevWork {
   int32_t nb_cap;     // fast kernel: Schmidl-Cox moment blocks per frame (dynamic LDS)
   int32_t bits_cap;   // fast kernel: packed bit-stream words per frame (dynamic LDS)
   int32_t rows_cap;   // fast kernel: symbol-row words per frame (dynamic LDS)
+  float *soft;        // exact kernel, AMOD_OPT_SOFT_COMBINE: per-slot soft bit values
+  int64_t soft_stride;// floats per slot
 };
+
+// AMOD_OPT_SOFT_COMBINE applies to repeated BPSK / QPSK frames
+__host__ __device__ inline bool soft_combine_applies(uint32_t options, int rep, int mod) {
+  return (options & AMOD_OPT_SOFT_COMBINE) && rep > 1 && (mod == AMOD_BPSK || mod == AMOD_QPSK);
+}
+
+
 
 // ---------------------------------------------------------------- helpers --
 // Lane id through an opaque copy: inside persistent frame loops this keeps the
@@ -291,6 +300,25 @@ __device__ inline uint32_t block_crc32(const uint32_t *v, int L, const DevTables
 // Majority vote (modem.js:487-495) of the bit stream `bits` (nbits) into `voted`
 // (words), returns the voted bit count. rep == 1 is a pass-through handled by
 // the caller. Whole workgroup.
+// soft vote: bit j = sign of the sum (in order, double) of its group's soft values
+// (a value < 0 stands for bit 1)
+__device__ inline int soft_vote(const float *sv, int nbits, int rep, uint32_t *voted) {
+  const int nv = nbits / rep;
+  const int nw = (nv + 31) >> 5;
+  for (int w = ltid(); w < nw; w += blockDim.x) {
+    uint32_t word = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int j = w * 32 + b;
+      if (j >= nv) break;
+      double sum = 0.0;
+      for (int u = 0; u < rep; ++u) sum += (double)sv[j * rep + u];
+      word |= (uint32_t)(sum < 0.0) << (31 - b);
+    }
+    voted[w] = word;
+  }
+  return nv;
+}
+
 __device__ inline int block_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
   const int nv = nbits / rep;
   const int nw = (nv + 31) >> 5;

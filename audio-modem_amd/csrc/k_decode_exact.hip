@@ -316,6 +316,13 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     for (int i = tid; i < nwords + 8; i += XT) bits[i] = 0u;
     wg_global_sync();
     const int npts = cfg.mod == AMOD_BPSK ? 2 : (cfg.mod == AMOD_QPSK ? 4 : 16);
+    // opt-in soft combining (AMOD_OPT_SOFT_COMBINE, not reference behaviour): per-bit soft
+    // values, < 0 for bit 1 (BPSK: cr; QPSK MSB: ci, LSB: max-log min(|cr|, |ci|) signed
+    // by whether the signs differ, the Gray map of initConstellation)
+    float *const sv = (soft_combine_applies(w.options, cfg.rep, cfg.mod) && w.soft &&
+                       (int64_t)nbits <= w.soft_stride)
+                          ? w.soft + (int64_t)blockIdx.x * w.soft_stride
+                          : nullptr;
     for (int s = 0; s < M; ++s) {
       __syncthreads();
       fft_exact(sig + data0 + s * SYM + CP, sm, cfg.t.tw_exact);
@@ -364,6 +371,18 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
           if (dist < md) { md = dist; mi = i; }
         }
         const int pos = (s * cfg.ndata + di) * cfg.bps;
+        if (sv) {
+          // weighted by |H|^2: the equaliser's division amplifies noise where the channel
+          // estimate is weak, so each bit counts in proportion to its channel power (MRC)
+          const double wgt = sm.hr[k] * sm.hr[k] + sm.hi[k] * sm.hi[k];
+          if (cfg.mod == AMOD_BPSK) {
+            sv[pos] = (float)(cr * wgt);
+          } else {
+            const double m = fmin(fabs(cr), fabs(ci)) * wgt;
+            sv[pos] = (float)(ci * wgt);
+            sv[pos + 1] = (float)(((cr < 0.0) != (ci < 0.0)) ? -m : m);
+          }
+        }
         const uint32_t val = (uint32_t)mi << (32 - cfg.bps - (pos & 31));
         if (val) atomicOr(&bits[pos >> 5], val);
       }
@@ -375,7 +394,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     int nv = nbits;
     if (cfg.rep > 1) {
       uint32_t *voted = bits + ((nwords + 3) & ~3);
-      nv = block_vote(bits, nbits, cfg.rep, voted);
+      nv = sv ? soft_vote(sv, nbits, cfg.rep, voted) : block_vote(bits, nbits, cfg.rep, voted);
       wg_global_sync();
       v = voted;
     }

@@ -282,8 +282,9 @@ __device__ __forceinline__ float dpp_sum8(float v) {
   return v;
 }
 
-__device__ __forceinline__ int frame_route(const DevWork &w, int N) {
+__device__ __forceinline__ int frame_route(const DevCfg &cfg, const DevWork &w, int N) {
   if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
+  if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) return AMOD_FLAG_FORCED; // opt-in soft vote
   if (8 * ((N + 3 + 255) >> 8) > w.nb_cap) return AMOD_FLAG_BIG; // moment arrays of this launch
   return 0;
 }
@@ -353,7 +354,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
   amod_debug *D = dbg ? w.dbg + f : nullptr;
   STAMP(0);
   {
-    const int route = frame_route(w, N);
+    const int route = frame_route(cfg, w, N);
     if (route) {
       if (tid == 0) {
         const int i = atomicAdd(w.fb_count, 1);

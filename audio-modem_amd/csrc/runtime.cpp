@@ -232,6 +232,9 @@ struct amod_ctx {
   DevBuf crc;          // shared CRC tables
   DevBuf fb;           // fb_count + list + flags
   DevBuf xs, bits;     // exact-kernel scratch
+  DevBuf soft;         // exact-kernel soft bit values (AMOD_OPT_SOFT_COMBINE only)
+  int64_t soft_stride = 0;
+  int soft_slots = 0;
   int64_t xs_stride = 0, bits_stride = 0;
   int nslots = 0;
   int64_t max_len = 0; // longest frame any reservation was sized for
@@ -443,6 +446,16 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
+  if (amod::soft_combine_applies(options, cfg->repetition, cfg->modulation)) {
+    const int64_t per = ((max_bits_for(cfg, std::max<int64_t>(ctx->max_len, max_len)) + 64) + 63) & ~int64_t(63);
+    if (ctx->soft_stride < per || ctx->soft_slots < ctx->nslots) {
+      HIP_TRY(ctx->soft.ensure(sizeof(float) * (size_t)(per * std::max(1, ctx->nslots))));
+      ctx->soft_stride = per;
+      ctx->soft_slots = ctx->nslots;
+    }
+    w.soft = (float *)ctx->soft.p;
+    w.soft_stride = ctx->soft_stride;
+  }
   { // fast-kernel LDS sized for the longest frame of this launch (host path) or reservation
     const int64_t flen = max_len >= 0 ? max_len : ctx->max_len;
     w.nb_cap = 8 * (int)((flen + 3 + 255) / 256) + 8;

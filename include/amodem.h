@@ -53,6 +53,11 @@ extern "C" {
 
 /* ---- decode option bits ---- */
 #define AMOD_OPT_FORCE_EXACT 1u /* run every frame through the exact-replica kernel */
+/* NOT reference behaviour, opt-in (BASELINE C5's noisy-channel path): with repetition > 1
+   and BPSK / QPSK, each group of `rep` repeated bits is decided by the sign of its summed
+   soft values (BPSK: the phase-corrected real part; QPSK: max-log per bit) instead of
+   majorityVote's hard vote (modem.js:487-495). Such frames run on the exact kernel. */
+#define AMOD_OPT_SOFT_COMBINE 2u
 
 /* ---- per-frame status (the reference's error strings, modem.js) ---- */
 #define AMOD_OK 0

@@ -1,0 +1,76 @@
+"""Opt-in soft combining of repeated bits (AMOD_OPT_SOFT_COMBINE) — NOT reference
+behaviour, so it is judged by error rate, not parity (majorityVote row;
+BASELINE C5: BPSK repetition under AWGN). Acoustic BPSK rep3 data-chunk frames with
+AWGN (noise divisor 1.5, ~1.8 dB): the reference's hard majority vote decodes 27 of 64
+frames with a valid CRC, the |H|^2-weighted soft vote 35 (measured, tools/soft_sweep.py;
+the reference's pilot-ratio phase estimate, not the vote, limits both below that). At
+20 dB, and for repetition 1, the option changes nothing."""
+import numpy as np
+import pytest
+
+import amodem
+from amodem import _lib as L
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(n, div, seed0, rep=3, mod="BPSK", config="acoustic", length=128):
+    out = []
+    pre = 2205  # buildChunkOFDMFrame's 0.05 s lead-in: windows start at pre1
+    for i in range(n):
+        case = {"config": config, "tx": {"kind": "chunk", "seq": i, "seed": 0xC5000000 + i, "len": length,
+                                          "mod": mod, "rep": rep},
+                "post": [{"op": "slice", "start": pre}, {"op": "noise", "snr": 0, "seed": seed0 + 7 * i, "div": div}]}
+        out.append(O.build_case(case))
+    lens = np.array([len(f) for f in out], np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return np.concatenate(out), offs, lens
+
+
+def _decode(dm, cfg, x, offs, lens, options):
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg, mode=L.MODE_CHUNK, options=options)
+    return rec, pay
+
+
+def test_soft_combining_beats_hard_vote_at_low_snr():
+    cfg = amodem.preset("acoustic", "BPSK", 3)
+    dm = amodem.Demodulator(0)
+    for div, strict in ((1.5, True), (2.0, False)):
+        x, offs, lens = _frames(64, div, 0x50F7)
+        hard, _ = _decode(dm, cfg, x, offs, lens, 0)
+        soft, sp = _decode(dm, cfg, x, offs, lens, L.OPT_SOFT_COMBINE)
+        ok_h = int(((hard["status"] == 0) & (hard["crc_valid"] == 1)).sum())
+        ok_s = int(((soft["status"] == 0) & (soft["crc_valid"] == 1)).sum())
+        assert ok_s >= ok_h and (ok_s > ok_h or not strict), (div, ok_h, ok_s)
+    dm.close()
+    for i in np.nonzero((soft["status"] == 0) & (soft["crc_valid"] == 1))[0][:8]:
+        d = amodem.to_reference(soft[i], sp[i].tobytes(), False)
+        assert d["data"] == amodem.synth_payload(0xC5000000 + int(i), 128)
+
+
+@pytest.mark.parametrize("rep,div", [(3, 100.0), (1, 3.0)])
+def test_soft_option_is_neutral_when_clean_or_unrepeated(rep, div):
+    cfg = amodem.preset("acoustic", "BPSK", rep)
+    x, offs, lens = _frames(16, div, 0x1111, rep=rep)
+    dm = amodem.Demodulator(0)
+    hard, hp = _decode(dm, cfg, x, offs, lens, 0)
+    soft, sp = _decode(dm, cfg, x, offs, lens, L.OPT_SOFT_COMBINE)
+    dm.close()
+    keys = ["status", "crc_valid", "seq_num", "data_len", "expected_crc", "actual_crc"]
+    assert all(np.array_equal(hard[k], soft[k]) for k in keys)
+    for i in range(len(hard)):
+        assert amodem.to_reference(hard[i], hp[i].tobytes(), False) == amodem.to_reference(soft[i], sp[i].tobytes(),
+                                                                                            False)
+
+
+def test_soft_combining_qpsk_rep3():
+    cfg = amodem.preset("standard", "QPSK", 3)
+    x, offs, lens = _frames(64, 8.0, 0x50F7, rep=3, mod="QPSK", config="standard", length=256)
+    dm = amodem.Demodulator(0)
+    hard, _ = _decode(dm, cfg, x, offs, lens, 0)
+    soft, _ = _decode(dm, cfg, x, offs, lens, L.OPT_SOFT_COMBINE)
+    dm.close()
+    ok_h = int(((hard["status"] == 0) & (hard["crc_valid"] == 1)).sum())
+    ok_s = int(((soft["status"] == 0) & (soft["crc_valid"] == 1)).sum())
+    assert ok_s >= ok_h, (ok_h, ok_s)
