@@ -56,9 +56,13 @@ __device__ __forceinline__ int rev6(int g) {
   return ((g & 1) << 5) | ((g & 2) << 3) | ((g & 4) << 1) | ((g & 8) >> 1) | ((g & 16) >> 3) | ((g & 32) >> 5);
 }
 
+constexpr int TX_PKT_LDS = 8192; // packet bytes staged in LDS (longer packets read from global)
+
 __global__ __launch_bounds__(TX_WG) void k_tx(const DevCfg cfg, const DevTxWork w) {
   __shared__ double2 xch[TX_NWAVE][kFft];
   __shared__ float wmaxv[TX_NWAVE];
+  __shared__ uint32_t pk_s[TX_PKT_LDS / 4];
+  __shared__ int16_t di_s[kMaxBand];
   const int f = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint8_t *const pkt = w.pkt + w.pkt_off[f];
@@ -73,13 +77,26 @@ __global__ __launch_bounds__(TX_WG) void k_tx(const DevCfg cfg, const DevTxWork 
   // silence before and after (Float32Array zeros; 0 * s stays +0)
   for (int i = tid; i < pre; i += TX_WG) out[i] = 0.f;
   for (int i = tid; i < post; i += TX_WG) out[total - post + i] = 0.f;
+  // the packet and the band -> data-index table in LDS: the spectrum build reads them
+  // per bit, so their latency must not be a global round trip each
+  const bool pk_lds = plen <= TX_PKT_LDS;
+  if (pk_lds)
+    for (int i = tid; i < (plen + 3) / 4; i += TX_WG) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; ++b)
+        if (4 * i + b < plen) v |= (uint32_t)pkt[4 * i + b] << (8 * b);
+      pk_s[i] = v;
+    }
+  for (int b = tid; b < cfg.nband; b += TX_WG) di_s[b] = cfg.t.band_di[b];
+  __syncthreads();
+  const uint8_t *const pk8 = reinterpret_cast<const uint8_t *>(pk_s);
 
   const double2 *const tw = cfg.t.tw_inv;
   // spectrum value V(k), 1 <= k <= 255: pilot 1 + 0i, data point, 0 elsewhere
   auto value = [&](int s, int k) -> double2 {
     const int b = k - cfg.sub_start;
     if (b < 0 || k > cfg.sub_end) return make_double2(0.0, 0.0);
-    const int di = cfg.t.band_di[b];
+    const int di = di_s[b];
     if (di < 0) return make_double2(1.0, 0.0);
     int idx = 0;
     for (int q = 0; q < bps; ++q) {
@@ -87,7 +104,7 @@ __global__ __launch_bounds__(TX_WG) void k_tx(const DevCfg cfg, const DevTxWork 
       int bit = 0;
       if (p < nbits) {
         const int64_t o = p / rep; // original bit (repeatBits: each bit rep times in a row)
-        bit = (pkt[o >> 3] >> (7 - (int)(o & 7))) & 1;
+        bit = ((pk_lds ? pk8[o >> 3] : pkt[o >> 3]) >> (7 - (int)(o & 7))) & 1;
       }
       idx = (idx << 1) | bit;
     }
