@@ -534,6 +534,204 @@ static napi_value js_abi(napi_env env, napi_callback_info info) {
   return out;
 }
 
+
+/* ----------------------------------------------- chunk assembler / stream receive */
+static void asm_finalize(napi_env env, void *data, void *hint) {
+  (void)env; (void)hint;
+  amod_asm_close((amod_assembler *)data);
+}
+
+static amod_assembler *get_asm(napi_env env, napi_value v) {
+  void *p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "expected an assembler handle");
+    return NULL;
+  }
+  return (amod_assembler *)p;
+}
+
+static napi_value make_i32(napi_env env, int32_t v) {
+  napi_value out;
+  NAPI_TRY(env, napi_create_int32(env, v, &out));
+  return out;
+}
+
+/* asmOpen(dir | null) -> handle (closed when collected) */
+static napi_value js_asm_open(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return NULL;
+  char dir[4096] = {0};
+  if (!is_nullish(env, argv[0])) {
+    size_t n;
+    if (napi_get_value_string_utf8(env, argv[0], dir, sizeof dir, &n) != napi_ok) return throw_msg(env, "bad dir");
+  }
+  amod_assembler *a;
+  if (amod_asm_open(dir[0] ? dir : NULL, &a) != AMOD_SUCCESS) return throw_msg(env, "assembler");
+  napi_value out;
+  NAPI_TRY(env, napi_create_external(env, a, asm_finalize, NULL, &out));
+  return out;
+}
+
+/* asmMetadata(h, totalChunks, totalFileSize, chunkSize, nameBytes) -> status */
+static napi_value js_asm_metadata(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return NULL;
+  amod_assembler *a = get_asm(env, argv[0]);
+  if (!a) return NULL;
+  int32_t tc, ts, cs;
+  const uint8_t *nm;
+  int32_t nn;
+  if (napi_get_value_int32(env, argv[1], &tc) != napi_ok || napi_get_value_int32(env, argv[2], &ts) != napi_ok ||
+      napi_get_value_int32(env, argv[3], &cs) != napi_ok || !get_u8(env, argv[4], &nm, &nn))
+    return NULL;
+  return make_i32(env, amod_asm_metadata(a, tc, ts, cs, nm, nn));
+}
+
+/* asmChunk(h, seq, data, crcValid) -> 1 stored / 0 ignored */
+static napi_value js_asm_chunk(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return NULL;
+  amod_assembler *a = get_asm(env, argv[0]);
+  if (!a) return NULL;
+  int32_t seq;
+  bool crc;
+  const uint8_t *d;
+  int32_t n;
+  if (napi_get_value_int32(env, argv[1], &seq) != napi_ok || !get_u8(env, argv[2], &d, &n) ||
+      napi_get_value_bool(env, argv[3], &crc) != napi_ok)
+    return NULL;
+  return make_i32(env, amod_asm_chunk(a, seq, d, n, crc ? 1 : 0));
+}
+
+static napi_value bytes_from(napi_env env, const uint8_t *p, int64_t n) {
+  napi_value ab, ta;
+  void *q;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)(n > 0 ? n : 0), &q, &ab));
+  if (n > 0) memcpy(q, p, (size_t)n);
+  NAPI_TRY(env, napi_create_typedarray(env, napi_uint8_array, (size_t)(n > 0 ? n : 0), ab, 0, &ta));
+  return ta;
+}
+
+/* asmState(h) -> {totalChunks, totalFileSize, chunkSize, receivedCount, crcErrors, complete,
+   framesDecoded, frameErrors, bitmap: Uint8Array | null, fileName: Uint8Array} */
+static napi_value js_asm_state(napi_env env, napi_callback_info info) {
+  napi_value argv[1], out, v;
+  if (!get_args(env, info, 1, argv)) return NULL;
+  amod_assembler *a = get_asm(env, argv[0]);
+  if (!a) return NULL;
+  amod_asm_info st;
+  amod_asm_state(a, &st);
+  NAPI_TRY(env, napi_create_object(env, &out));
+  const struct { const char *k; int32_t v; } f[] = {
+      {"totalChunks", st.total_chunks}, {"totalFileSize", st.total_size}, {"chunkSize", st.chunk_size},
+      {"receivedCount", st.received}, {"crcErrors", st.crc_errors}, {"framesDecoded", st.frames_decoded},
+      {"frameErrors", st.frame_errors}};
+  for (size_t i = 0; i < sizeof f / sizeof f[0]; ++i) {
+    NAPI_TRY(env, napi_create_int32(env, f[i].v, &v));
+    NAPI_TRY(env, napi_set_named_property(env, out, f[i].k, v));
+  }
+  NAPI_TRY(env, napi_get_boolean(env, st.complete != 0, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "complete", v));
+  if (st.has_bitmap) {
+    const int64_t n = amod_asm_bitmap(a, NULL, 0);
+    uint8_t *b = (uint8_t *)malloc((size_t)(n > 0 ? n : 1));
+    amod_asm_bitmap(a, b, n);
+    v = bytes_from(env, b, n);
+    free(b);
+    if (!v) return NULL;
+  } else {
+    NAPI_TRY(env, napi_get_null(env, &v));
+  }
+  NAPI_TRY(env, napi_set_named_property(env, out, "bitmap", v));
+  const int64_t nn = amod_asm_name(a, NULL, 0);
+  uint8_t *nm = (uint8_t *)malloc((size_t)(nn > 0 ? nn : 1));
+  amod_asm_name(a, nm, nn);
+  v = bytes_from(env, nm, nn);
+  free(nm);
+  if (!v) return NULL;
+  NAPI_TRY(env, napi_set_named_property(env, out, "fileName", v));
+  return out;
+}
+
+/* asmMissing(h) -> Int32Array */
+static napi_value js_asm_missing(napi_env env, napi_callback_info info) {
+  napi_value argv[1], ab, ta;
+  if (!get_args(env, info, 1, argv)) return NULL;
+  amod_assembler *a = get_asm(env, argv[0]);
+  if (!a) return NULL;
+  const int64_t n = amod_asm_missing(a, NULL, 0);
+  void *p;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)n * 4, &p, &ab));
+  amod_asm_missing(a, (int32_t *)p, n);
+  NAPI_TRY(env, napi_create_typedarray(env, napi_int32_array, (size_t)n, ab, 0, &ta));
+  return ta;
+}
+
+/* asmFile(h) -> Uint8Array, or a negative status (RangeError / TypeError in JS) */
+static napi_value js_asm_file(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return NULL;
+  amod_assembler *a = get_asm(env, argv[0]);
+  if (!a) return NULL;
+  const int64_t n = amod_asm_file(a, NULL, 0);
+  if (n < 0) return make_i32(env, (int32_t)n);
+  napi_value ab, ta;
+  void *p;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)n, &p, &ab));
+  const int64_t m = amod_asm_file(a, (uint8_t *)p, n);
+  if (m < 0) return make_i32(env, (int32_t)m);
+  NAPI_TRY(env, napi_create_typedarray(env, napi_uint8_array, (size_t)n, ab, 0, &ta));
+  return ta;
+}
+
+/* receiveStream(samples, cfg, asmHandle, device) -> {frames: ArrayBuffer of amod_stream_frame,
+   nframes, refineFail: Float64Array, framesDecoded, frameErrors} */
+static napi_value js_receive_stream(napi_env env, napi_callback_info info) {
+  napi_value argv[4], out, v, ab;
+  if (!get_args(env, info, 4, argv)) return NULL;
+  float *x;
+  size_t n;
+  if (!typed(env, argv[0], napi_float32_array, (void **)&x, &n)) return throw_msg(env, "expected a Float32Array");
+  amod_cfg c;
+  if (!to_cfg(env, argv[1], &c)) return NULL;
+  amod_assembler *a = get_asm(env, argv[2]);
+  if (!a) return NULL;
+  int32_t dev = 0;
+  napi_get_value_int32(env, argv[3], &dev);
+  amod_ctx *ctx = get_ctx(env, dev);
+  if (!ctx) return NULL;
+  const int64_t cap = (int64_t)(n / 4096) + 64;
+  amod_stream_frame *fr = (amod_stream_frame *)calloc((size_t)cap, sizeof(amod_stream_frame));
+  int64_t *rf = (int64_t *)calloc(4096, sizeof(int64_t));
+  int64_t nf = 0;
+  amod_stream_stats st;
+  const int rc = amod_stream_receive(ctx, &c, x, (int64_t)n, a, fr, cap, &nf, rf, 4096, &st);
+  if (rc != AMOD_SUCCESS) {
+    free(fr); free(rf);
+    return throw_msg(env, amod_last_error(ctx));
+  }
+  const int64_t k = nf < cap ? nf : cap;
+  void *p;
+  NAPI_TRY(env, napi_create_object(env, &out));
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)k * sizeof(amod_stream_frame), &p, &ab));
+  memcpy(p, fr, (size_t)k * sizeof(amod_stream_frame));
+  NAPI_TRY(env, napi_set_named_property(env, out, "frames", ab));
+  NAPI_TRY(env, napi_create_int64(env, k, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "nframes", v));
+  const int64_t nr = st.nrefine_fail < 4096 ? st.nrefine_fail : 4096;
+  NAPI_TRY(env, napi_create_arraybuffer(env, (size_t)nr * 8, &p, &ab));
+  for (int64_t i = 0; i < nr; ++i) ((double *)p)[i] = (double)rf[i];
+  NAPI_TRY(env, napi_create_typedarray(env, napi_float64_array, (size_t)nr, ab, 0, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "refineFail", v));
+  NAPI_TRY(env, napi_create_int64(env, st.frames_decoded, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "framesDecoded", v));
+  NAPI_TRY(env, napi_create_int64(env, st.frame_errors, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "frameErrors", v));
+  free(fr);
+  free(rf);
+  return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -549,6 +747,13 @@ static napi_value init(napi_env env, napi_value exports) {
       {"numDataSubs", NULL, js_num_data_subs, NULL, NULL, NULL, napi_enumerable, NULL},
       {"payloadStride", NULL, js_payload_stride, NULL, NULL, NULL, napi_enumerable, NULL},
       {"abiVersion", NULL, js_abi, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmOpen", NULL, js_asm_open, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmMetadata", NULL, js_asm_metadata, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmChunk", NULL, js_asm_chunk, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmState", NULL, js_asm_state, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmMissing", NULL, js_asm_missing, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmFile", NULL, js_asm_file, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"receiveStream", NULL, js_receive_stream, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof props / sizeof props[0], props) != napi_ok) return NULL;
   return exports;

@@ -382,11 +382,100 @@ function analyzeLoopback(recorded, modName, repetition, testData) {
   return { detected: true, correlation, ber, channelMagnitude, snrEstimate, quality };
 }
 
+
+// ------------------------------------------- chunk assembly / streaming receive --
+// app.js ChunkAssembler (597-704) over libamodem's host assembler (assembler.cpp): same
+// methods, getters and thrown errors; chunks live in memory, or as files under
+// opts.directory (the IndexedDB store's stand-in). The async methods resolve at once.
+const ASM_RANGE_ERROR = -10, ASM_TYPE_ERROR = -11;
+function asmThrow(st) {
+  if (st === ASM_RANGE_ERROR) throw new RangeError('Invalid typed array length');
+  if (st === ASM_TYPE_ERROR) throw new TypeError("Cannot read properties of null (reading 'transaction')");
+  if (typeof st === 'number' && st < 0) throw new Error(`assembler error ${st}`);
+  return st;
+}
+
+class ChunkAssembler {
+  constructor(opts) {
+    this._h = native.asmOpen((opts && opts.directory) || null);
+  }
+  _st() { return native.asmState(this._h); }
+  get totalChunks() { return this._st().totalChunks; }
+  get totalFileSize() { return this._st().totalFileSize; }
+  get chunkSize() { return this._st().chunkSize; }
+  get fileName() { return utf8(this._st().fileName); }
+  get receivedBitmap() { return this._st().bitmap; }
+  get receivedCount() { return this._st().receivedCount; }
+  get crcErrors() { return this._st().crcErrors; }
+  async handleMetadataFrame(meta) {
+    asmThrow(native.asmMetadata(this._h, meta.totalChunks | 0, meta.totalFileSize | 0, meta.chunkSize | 0,
+      new TE().encode(String(meta.fileName))));
+  }
+  async handleDataChunk(seqNum, data, crcValid) {
+    asmThrow(native.asmChunk(this._h, seqNum | 0, toBytes(data), !!crcValid));
+  }
+  isReceived(seqNum) {
+    const b = this._st().bitmap;
+    if (!b) return false;
+    return !!(b[seqNum >> 3] & (1 << (seqNum & 7)));
+  }
+  isComplete() { return this._st().complete; }
+  getMissingChunks() { return Array.from(native.asmMissing(this._h)); }
+  async assembleFile() {
+    const r = native.asmFile(this._h);
+    asmThrow(typeof r === 'number' ? r : 0);
+    return r;
+  }
+  cleanup() {}
+}
+
+const E_STREAM_LOST = 101;
+const STREAM_REC = 24 + REC; // sizeof(amod_stream_frame)
+
+// receiveStream(samples, modName, repetition, {assembler, device}) -> Promise<{frames,
+// refineFail, framesDecoded, frameErrors, assembler}>: app.js StreamingReceiver
+// (706-998) over a recorded stream fed in 4096-sample blocks (GPU pre-pass + decode,
+// host state machine); every demodulated window with decodeChunkFrame's outcome
+// (payload bytes go to the assembler, as _demodulateFrame does). Additive API.
+async function receiveStream(samples, modName, repetition, opts) {
+  const o = opts || {};
+  const asm = o.assembler || new ChunkAssembler();
+  const r = native.receiveStream(asFloat32(samples), nativeCfg(modName, repetition), asm._h, o.device | 0);
+  const view = new DataView(r.frames);
+  const frames = [];
+  for (let i = 0; i < r.nframes; i++) {
+    const b = i * STREAM_REC, g = (k) => view.getInt32(b + 24 + 4 * k, true);
+    const status = g(0), frameType = g(3), aux = g(4);
+    let result;
+    if (status === 0 && frameType === FRAME_META) {
+      result = { frameType, totalChunks: g(11), totalFileSize: g(12), chunkSize: g(13), crcValid: g(16) !== 0 };
+    } else if (status === 0) {
+      result = { frameType, seqNum: g(10), dataLen: g(9), crcValid: g(16) !== 0 };
+    } else if (status === E_STREAM_LOST) {
+      result = { error: 'window left the ring buffer' };
+    } else if (status === E_INVALID_LEN) {
+      result = { error: `Invalid data length: ${aux}` };
+    } else if (status === E_UNKNOWN_TYPE) {
+      result = { error: `Unknown frame type: 0x${aux.toString(16)}`, frameType: aux };
+    } else {
+      result = { error: ERR[status] };
+    }
+    frames.push({
+      preambleGlobalPos: Number(view.getBigInt64(b, true)), expectedFrameEnd: Number(view.getBigInt64(b + 8, true)),
+      length: view.getInt32(b + 16, true), result,
+    });
+  }
+  return {
+    frames, refineFail: Array.from(r.refineFail), framesDecoded: Number(r.framesDecoded),
+    frameErrors: Number(r.frameErrors), assembler: asm,
+  };
+}
+
 const api = {
   fft, OFDM_CONFIGS, OFDM, setOFDMConfig, Constellations, generatePreambleSymbol1, buildTransmitSignal,
   decodeReceivedSignal, FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame, decodeChunkFrame,
   estimateFrameSamples, generateSweepTone, generateTestSignal, analyzeLoopback,
-  decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native,
+  decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native, ChunkAssembler, receiveStream,
 };
 
 module.exports = api;

@@ -49,6 +49,40 @@ async function main() {
         case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
         case 'loopback': r = M.analyzeLoopback(f32(j.file), j.mod, j.rep, Uint8Array.from(j.testData)); break;
         case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { mode: j.mode }); break;
+        case 'asm': {
+          // one ChunkAssembler scenario (tests/golden/assembler.json ops); state after each op
+          const a = new M.ChunkAssembler(j.directory ? { directory: j.directory } : undefined);
+          r = [];
+          for (const op of j.ops) {
+            let error = null, file = null;
+            try {
+              if (op.op === 'meta') await a.handleMetadataFrame(op);
+              else if (op.op === 'chunk') await a.handleDataChunk(op.seq, Buffer.from(op.hex, 'hex'), op.crc);
+              else file = Buffer.from(await a.assembleFile()).toString('hex');
+            } catch (e) {
+              error = e.constructor.name;
+            }
+            const bm = a.receivedBitmap;
+            r.push({
+              error, file, totalChunks: a.totalChunks, totalFileSize: a.totalFileSize, chunkSize: a.chunkSize,
+              fileName: a.fileName, receivedCount: a.receivedCount, crcErrors: a.crcErrors, complete: a.isComplete(),
+              bitmap: bm ? Array.from(bm) : null, missing: bm ? a.getMissingChunks() : null,
+              received: bm ? Array.from({ length: Math.max(0, a.totalChunks) }, (_, i) => a.isReceived(i)) : null,
+            });
+          }
+          break;
+        }
+        case 'stream': {
+          const s = await M.receiveStream(f32(j.file), j.mod, j.rep);
+          const a = s.assembler;
+          r = {
+            frames: s.frames, refineFail: s.refineFail, framesDecoded: s.framesDecoded, frameErrors: s.frameErrors,
+            asm: { totalChunks: a.totalChunks, totalFileSize: a.totalFileSize, chunkSize: a.chunkSize,
+              fileName: a.fileName, receivedCount: a.receivedCount, crcErrors: a.crcErrors, complete: a.isComplete() },
+            file: a.totalChunks > 0 ? sha(await a.assembleFile()) : null,
+          };
+          break;
+        }
         default: throw new Error('unknown op ' + j.op);
       }
       out[j.id] = { ok: enc(r) };

@@ -224,3 +224,85 @@ def test_analyze_loopback_golden(tmp_path):
         got = [_lb_num(v) for v in r["channelMagnitude"]]
         exp = [_gold_num(v) for v in g["channelMagnitude"]]
         assert got == pytest.approx(exp, rel=1e-12, abs=1e-12), c["name"]
+
+
+def _asm_scenarios():
+    from helpers import GOLDEN
+    with open(os.path.join(GOLDEN, "assembler.json")) as f:
+        return json.load(f)["scenarios"]
+
+
+@pytest.mark.parametrize("store", ["memory", "files"])
+def test_chunk_assembler_through_js(store, tmp_path):
+    """app.js ChunkAssembler's methods, getters and thrown errors through the JS class,
+    on every golden scenario the reference produced (tests/golden/assembler.json)."""
+    import amodem
+    scen = _asm_scenarios()
+    jobs = []
+    for name, sc in sorted(scen.items()):
+        ops = []
+        for op in sc["ops"]:
+            op = dict(op)
+            if op["op"] == "chunk":
+                op["hex"] = amodem.synth_payload(op["seed"], op["len"]).hex()
+            ops.append(op)
+        d = tmp_path / name
+        if store == "files":
+            d.mkdir()
+        jobs.append({"op": "asm", "ops": ops, "id": name, **({"directory": str(d)} if store == "files" else {})})
+    res = run(jobs, tmp_path)
+    for name, sc in scen.items():
+        got = ok(res, name)
+        assert len(got) == len(sc["steps"]), name
+        for g, step in zip(got, sc["steps"]):
+            w = step["state"]
+            assert g["error"] == step["error"], (name, g)
+            assert g["file"] == step["file"], name
+            for k in ("totalChunks", "totalFileSize", "chunkSize", "receivedCount", "crcErrors", "complete"):
+                assert g[k] == w[k], (name, k)
+            assert g["fileName"] == (w["fileName"] or ""), name
+            if w["bitmap"] is not None:
+                assert g["bitmap"][:64] == w["bitmap"], name
+                assert len(g["bitmap"]) == w["bitmapLen"], name
+            else:
+                assert g["bitmap"] is None, name
+            if w["missing"] is not None:
+                assert g["missing"] == w["missing"], name
+                miss = set(w["missing"])
+                assert g["received"] == [i not in miss for i in range(w["totalChunks"])], name
+
+
+@pytest.mark.gpu
+def test_receive_stream_through_js(tmp_path):
+    """receiveStream (StreamingReceiver over a recorded stream) from JS on the golden
+    streams: every window, its decode outcome, the failed refinements, the counters and
+    the assembled file equal what the reference receiver did (tests/golden/stream.json)."""
+    from test_gpu_stream import build_stream, streams
+    jobs, want = [], {}
+    for sp in streams():
+        _, x, _ = build_stream(sp)
+        p = tmp_path / f"{sp['name']}.f32"
+        x.astype(np.float32).tofile(p)
+        jobs.append({"op": "stream", "file": str(p), "mod": sp["mod"], "rep": sp["rep"], "config": sp["config"],
+                     "id": sp["name"]})
+        want[sp["name"]] = sp
+    res = run(jobs, tmp_path)
+    for name, sp in want.items():
+        g = ok(res, name)
+        got = [{"pos": f["preambleGlobalPos"], "end": f["expectedFrameEnd"], "len": f["length"],
+                **({"error": f["result"]["error"]} if "error" in f["result"] else
+                   {k: v for k, v in f["result"].items() if k in ("frameType", "crcValid", "seqNum", "dataLen",
+                                                                   "totalChunks", "chunkSize")})}
+               for f in g["frames"]]
+        exp = [{k: v for k, v in w.items() if k != "fileName"} for w in sp["frames"]]
+        assert got == exp, name
+        assert g["refineFail"] == sp["refineFail"], name
+        assert (g["framesDecoded"], g["frameErrors"]) == (sp["framesDecoded"], sp["frameErrors"]), name
+        a = sp["assembler"]
+        assert [g["asm"][k] for k in ("totalChunks", "totalFileSize", "chunkSize", "receivedCount", "crcErrors",
+                                      "complete", "fileName")] == [a[k] for k in ("totalChunks", "totalFileSize",
+                                                                                 "chunkSize", "receivedCount",
+                                                                                 "crcErrors", "complete",
+                                                                                 "fileName")], name
+        if sp["offered"] is not None:
+            assert g["file"] == sp["offered"]["sha256"], name
