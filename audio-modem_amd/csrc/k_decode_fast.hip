@@ -202,6 +202,13 @@ __device__ __forceinline__ int decide(int mod, float cr, float ci, float &margin
   return 4 * row + col;
 }
 
+// v_rcp_f32 / v_sqrt_f32 / v_rsq_f32 without the IEEE scaling and fix-up sequences
+// (<= 1 ulp). Used only for bounds and metrics whose guards carry a relative slack of
+// >= 1e-4 (caps, brackets) or an absolute one of >= 1e-3 (metric guards).
+__device__ __forceinline__ float rcp_a(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sqrt_a(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float rsq_a(float x) { return __builtin_amdgcn_rsqf(x); }
+
 // min/max of three without the NaN canonicalisation fminf/fmaxf add (a NaN sample
 // is caught through the sum instead)
 __device__ __forceinline__ float min3_raw(float a, float b, float c) {
@@ -532,7 +539,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         if (b < bz_edge && (b > 0 || ph == 0)) {
           const float s1b = LDS_F[b], s1p = LDS_F[b + 8], s2p = fmaxf(LDS_F[nbc + b + 8], 0.f);
           LDS_F[2 * nbc + b] = fmaf(AA, LDS_F[2 * nbc + b], fmaf(AB, s1b + s1p, 32.f * BB));
-          tmax = fmaxf(tmax, AA * sqrtf(s2b * s2p) + aAB * (sqrtf(32.f * s2b) + sqrtf(32.f * s2p)) + 32.f * BB);
+          tmax = fmaxf(tmax, AA * sqrt_a(s2b * s2p) + aAB * (sqrt_a(32.f * s2b) + sqrt_a(32.f * s2p)) + 32.f * BB);
         }
       }
       __syncthreads();
@@ -540,7 +547,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         const float s1b = LDS_F[b], s2b = fmaxf(LDS_F[nbc + b], 0.f);
         const int nv = min(BLK * b + BLK, K) - max(BLK * b, ph);
         LDS_F[nbc + b] = fmaf(AA, s2b, fmaf(2.f * AB, s1b, (float)nv * BB));
-        tmax = fmaxf(tmax, AA * s2b + 2.f * aAB * sqrtf(32.f * s2b) + 32.f * BB);
+        tmax = fmaxf(tmax, AA * s2b + 2.f * aAB * sqrt_a(32.f * s2b) + 32.f * BB);
       }
       // blocks whose pairs leave the frame (and block 0 when the frame starts mid-float4):
       // summed directly from the samples, one 32-lane group per block
@@ -564,7 +571,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         float T = 0.f;
         for (int i = 0; i < NWAVE; ++i) T = fmaxf(T, sm.rf[i]);
         // a block sum carries <= ~13 roundings of terms bounded by T; a window adds 8 blocks
-        sm.errw = 8.f * 16.f * 5.9604645e-8f * T + 1e-30f;
+        sm.errw = 8.f * 16.f * 5.9604645e-8f * (1.0001f * T) + 1e-30f;
       }
       __syncthreads();
     }
@@ -597,7 +604,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         for (int q = 0; q < 8; ++q) { p += Zb[c + q]; ra += Eb[c + q]; rb += Eb[c + 8 + q]; }
         if (BLK * c - ph >= 0 && ra - errw > gate_hi && rb - errw > gate_hi) {
           const float pl = fmaxf(fabsf(p) - errw, 0.f);
-          lmax = fmaxf(lmax, (pl * pl) / ((ra + errw) * (rb + errw)) * 0.9999f);
+          lmax = fmaxf(lmax, (pl * pl) * rcp_a((ra + errw) * (rb + errw)) * 0.9999f);
         }
         const float e0 = fmaxf(Eb[c], 0.f) + errw, e8 = fmaxf(Eb[c + 8], 0.f) + errw;
         const float e16 = (c + 16 < NB ? fmaxf(Eb[c + 16], 0.f) : 0.f) + errw;
@@ -606,8 +613,8 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         if (!(ra + e8 + errw > gate_lo && rb + e16 + errw > gate_lo)) cv = -2.f; // gated out throughout
         else if (ra_lo > 0.f && rb_lo > 0.f) {
           // |p(d) - p_c| <= sum|z| over blocks c and c+8 <= sqrt(E_c E_c+8) + sqrt(E_c+8 E_c+16)
-          const float pm = fabsf(p) + errw + sqrtf(e0 * e8) + sqrtf(e8 * e16);
-          cv = (pm * pm) / (ra_lo * rb_lo) * 1.0001f;
+          const float pm = fabsf(p) + errw + sqrt_a(e0 * e8) + sqrt_a(e8 * e16);
+          cv = (pm * pm) * rcp_a(ra_lo * rb_lo) * 1.0001f;
         } else cv = INFINITY;
         cap[c] = cv;
       }
@@ -670,10 +677,10 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         // exclusive prefix (inclusive scan minus own term) over the 32-lane group
         p += scan32(vp) - vp; ra += scan32(va) - va; rb += scan32(vb) - vb;
         const bool ok = d >= 0 && d <= E && ra > gate_lo && rb > gate_lo;
-        m = ok ? (p * p) / (ra * rb) : -1.f;
+        m = ok ? (p * p) * rcp_a(ra * rb) : -1.f;
         const float pl = fmaxf(fabsf(p) - errw, 0.f), ph2 = fabsf(p) + errw;
-        mlo = ok ? (pl * pl) / ((ra + errw) * (rb + errw)) * 0.9999f : -1.f;
-        mhi = ok ? ((ra > errw && rb > errw) ? (ph2 * ph2) / ((ra - errw) * (rb - errw)) * 1.0001f : INFINITY) : -1.f;
+        mlo = ok ? (pl * pl) * rcp_a((ra + errw) * (rb + errw)) * 0.9999f : -1.f;
+        mhi = ok ? ((ra > errw && rb > errw) ? (ph2 * ph2) * rcp_a((ra - errw) * (rb - errw)) * 1.0001f : INFINITY) : -1.f;
         return ok;
       };
       float best = -1.f, blo = -1.f, bhi = -1.f;
@@ -932,11 +939,13 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
             en = 0.f;
             for (int i = 0; i < SYM; ++i) en = fmaf(yw[d + i], yw[d + i], en);
           }
-          const float den = sqrtf(fmaxf(en, 0.f) * te);
+          // den = sqrt(en te) against the 0.001 gate, compared as squares; m = cj / den
+          const float et = fmaxf(en, 0.f) * te;
+          const float g_hi = 0.001f * (1.f + eps_g), g_lo = 0.001f * (1.f - eps_g);
           float m;
-          if (den > 0.001f * (1.f + eps_g)) m = cj / den;
-          else if (den > 0.001f * (1.f - eps_g)) m = cj / den + 4.f; // uncertain gate: tagged
-          else m = -8.f;                                              // gated out
+          if (et > g_hi * g_hi) m = cj * rsq_a(et);
+          else if (et > g_lo * g_lo) m = cj * rsq_a(et) + 4.f; // uncertain gate: tagged
+          else m = -8.f;                                      // gated out
           LDS_F[FINE_M + j0 + sp] = m;
         }
       }
