@@ -36,7 +36,10 @@ namespace {
 constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
-constexpr int FINE_MAX = 1024;               // max fine-search positions (else exact)
+#ifndef AMOD_FINE_MAX
+#define AMOD_FINE_MAX 1024
+#endif
+constexpr int FINE_MAX = AMOD_FINE_MAX;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
 constexpr int SC_CACHE = 16;                 // candidate blocks whose per-position results stay in LDS
 constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT round (+ CE)
@@ -67,6 +70,13 @@ extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
 constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
 constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the window, span + 1 entries
+#ifndef AMOD_FINE_MFMA
+#define AMOD_FINE_MFMA 1 // folded fine correlation as Toeplitz tiles on the matrix cores
+#endif
+// zero-padded template table of the MFMA fine path for n taps: 16 zeros, n taps, zeros
+// up to the last K step (K = n + 15 rounded up to 4)
+__host__ __device__ constexpr int fine_tab_len(int n) { return 16 + 4 * ((n + 15 + 3) >> 2); }
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int FQ_G = NWAVE * 512;             // float2 index of g
 #ifndef AMOD_TW_LDS
 #define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
@@ -826,19 +836,43 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         const __amdgpu_buffer_rsrc_t rt =
             __builtin_amdgcn_make_buffer_rsrc((void *)cfg.t.pre1, (short)0, 4 * SYM, 0x00020000);
         float tv[TR], yv[YR];
+#if AMOD_FINE_MFMA
+        // folded: two zero-padded template tables (the MFMA A operand, fine_mfma)
+        const int la = fine_tab_len(256), lb = fine_tab_len(CP);
+        auto tab_src = [&](int j) { // template index feeding table entry j (-1: zero)
+          const int i = j < la ? j - 16 : j - la - 16, n = j < la ? 256 : CP;
+          return (i >= 0 && i < n && j < la + lb) ? i : -1;
+        };
+#endif
 #pragma unroll
-        for (int r = 0; r < TR; ++r)
-          tv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, 4 * (tid + r * WG), 0, 0));
+        for (int r = 0; r < TR; ++r) {
+          int src = tid + r * WG;
+#if AMOD_FINE_MFMA
+          if (cfg.fold) src = tab_src(src);
+#endif
+          tv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, 4 * src, 0, 0)); // src < 0: 0
+        }
 #pragma unroll
         for (int r = 0; r < YR; ++r)
           yv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, 4 * (tid + r * WG), 0, 0));
 #pragma unroll
-        for (int r = 0; r < TR; ++r)
-          if (tid + r * WG < SYM) LDS_F[FINE_TM + tid + r * WG] = tv[r];
+        for (int r = 0; r < TR; ++r) {
+          const int j = tid + r * WG;
+#if AMOD_FINE_MFMA
+          if (cfg.fold) { if (j < la + lb) LDS_F[FINE_TM + j] = tab_src(j) >= 0 ? tv[r] : 0.f; }
+          else
+#endif
+          if (j < SYM) LDS_F[FINE_TM + j] = tv[r];
+        }
 #pragma unroll
         for (int r = 0; r < YR; ++r) {
           const int j = tid + r * WG;
+#if AMOD_FINE_MFMA
+          // the tiles read past the window: zeros (finite) up to the region's end
+          if (j < FINE_MAX + 800) LDS_F[FINE_YW + j] = (j < span && w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
+#else
           if (j < span) LDS_F[FINE_YW + j] = (w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
+#endif
         }
       }
       __syncthreads();
@@ -850,7 +884,12 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       if (fold) {
         // corr(d) = sum_{i<256} t[i] (y[d+i] + fold y[d+i+256]) + sum_{i<CP} t[i] y[d+i+512]
         // (t[i+256] = fold t[i]): 256 + CP taps instead of SYM
-        for (int j = tid; j < 8 * noct + 264; j += WG) LDS_F[FINE_Q + j] = fmaf((float)fold, yw[j + 256], yw[j]);
+#if AMOD_FINE_MFMA
+        const int qn = 256 * ((P + 255) >> 8) + 256; // everything the tiles read
+#else
+        const int qn = 8 * noct + 264;
+#endif
+        for (int j = tid; j < qn; j += WG) LDS_F[FINE_Q + j] = fmaf((float)fold, yw[j + 256], yw[j]);
       }
       // window energies from a prefix of squares: E[j] = sum_{i<j} y[i]^2, en(d) = E[d+SYM] - E[d].
       // Each E[j] carries <= ~26 roundings of partial sums <= E[span]: |err en| <= en_err.
@@ -887,6 +926,62 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       }
       __syncthreads();
       const float *qw = LDS_F + FINE_Q;
+      // metric of window position d from its correlation cj; energies from the prefix E
+      auto fine_metric = [&](int d, float cj) {
+        float en = LDS_F[FINE_E + d + SYM] - LDS_F[FINE_E + d];
+        if (en < 1e4f * en_err) { // low-energy window: the difference is not accurate enough
+          en = 0.f;
+          for (int i = 0; i < SYM; ++i) en = fmaf(yw[d + i], yw[d + i], en);
+        }
+        // den = sqrt(en te) against the 0.001 gate, compared as squares; m = cj / den
+        const float et = fmaxf(en, 0.f) * te;
+        const float g_hi = 0.001f * (1.f + eps_g), g_lo = 0.001f * (1.f - eps_g);
+        float m;
+        if (et > g_hi * g_hi) m = cj * rsq_a(et);
+        else if (et > g_lo * g_lo) m = cj * rsq_a(et) + 4.f; // uncertain gate: tagged
+        else m = -8.f;                                      // gated out
+        LDS_F[FINE_M + d] = m;
+      };
+#if AMOD_FINE_MFMA
+      if (fold) {
+        // Toeplitz tiles of 256 positions on the matrix cores (v_mfma_f32_16x16x4_f32,
+        // f32 in, f32 accumulate), one tile per wave:
+        //   C[r][n] = corr(256 t + 16 n + r) = sum_k T[r][k] Y[k][n],
+        //   T[r][k] = tpad[16 + k - r]   (zero-padded template table),
+        //   Y[k][n] = q[256 t + 16 n + k] (folded window), then the CP tail taps on y at
+        //   offset 512 with their own table; K in steps of 4.
+        // Lane l supplies A = T[l % 16][4 s + l / 16] and B = Y[4 s + l / 16][l % 16] (one
+        // LDS word each, immediate offsets) and receives C[4 (l / 16) + i][l % 16], i < 4:
+        // four consecutive positions. Two accumulators alternate to halve the chain.
+        const int la = fine_tab_len(256);
+        const int r16 = lane & 15, kk = lane >> 4;
+        const int ntile = (P + 255) >> 8;
+        const int sb = (CP + 15 + 3) >> 2;
+        for (int t = wave; t < ntile; t += NWAVE) {
+          const float *ta = LDS_F + FINE_TM + 16 + kk - r16;
+          const float *tb = ta + la;
+          const float *ya = LDS_F + FINE_Q + 256 * t + 16 * r16 + kk;
+          const float *yb = LDS_F + FINE_YW + 512 + 256 * t + 16 * r16 + kk;
+          floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int st = 0; st < 68; st += 2) {
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * st], ya[4 * st], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * st + 4], ya[4 * st + 4], c1, 0, 0, 0);
+          }
+          int st = 0;
+          for (; st + 1 < sb; st += 2) {
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st], yb[4 * st], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st + 4], yb[4 * st + 4], c1, 0, 0, 0);
+          }
+          if (st < sb) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st], yb[4 * st], c0, 0, 0, 0);
+          const int d0 = 256 * t + 16 * r16 + 4 * kk;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (d0 + i < P) fine_metric(d0 + i, c0[i] + c1[i]);
+        }
+      } else
+#endif
+      {
       // lane = (octet of 8 positions, one of 8 tap ranges): per tap one window read,
       // one template read, 8 correlations. The 8 ranges of an octet are 8 aligned
       // lanes, combined by DPP; energies come from the prefix E.
@@ -933,21 +1028,9 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           float cj = c[0];
 #pragma unroll
           for (int r = 1; r < 8; ++r) cj = sp == r ? c[r] : cj;
-          const int d = j0 + sp;
-          float en = LDS_F[FINE_E + d + SYM] - LDS_F[FINE_E + d];
-          if (en < 1e4f * en_err) { // low-energy window: the difference is not accurate enough
-            en = 0.f;
-            for (int i = 0; i < SYM; ++i) en = fmaf(yw[d + i], yw[d + i], en);
-          }
-          // den = sqrt(en te) against the 0.001 gate, compared as squares; m = cj / den
-          const float et = fmaxf(en, 0.f) * te;
-          const float g_hi = 0.001f * (1.f + eps_g), g_lo = 0.001f * (1.f - eps_g);
-          float m;
-          if (et > g_hi * g_hi) m = cj * rsq_a(et);
-          else if (et > g_lo * g_lo) m = cj * rsq_a(et) + 4.f; // uncertain gate: tagged
-          else m = -8.f;                                      // gated out
-          LDS_F[FINE_M + j0 + sp] = m;
+          fine_metric(j0 + sp, cj);
         }
+      }
       }
       __syncthreads();
       // argmax (first index), second best, uncertain-gate candidates
