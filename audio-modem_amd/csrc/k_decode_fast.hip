@@ -1,8 +1,8 @@
 // k_decode_fast.hip — streaming fast path of the OFDM receive chain (gfx950).
 //
-// One 256-thread workgroup (4 waves) per frame, ~29 KB of LDS, so five frames are
-// in flight per CU: while one workgroup streams its frame from HBM, the others
-// compute. The frame is never held in LDS; it is read from HBM once, coalesced,
+// One 256-thread workgroup (4 waves) per frame, <= 26 KB of LDS and 80 registers on
+// C2-sized frames, so six frames are in flight per CU: while one workgroup streams its
+// frame from HBM, the others compute. The frame is never held in LDS; it is read from HBM once, coalesced,
 // and the few samples later stages need again come back from L2 / Infinity Cache.
 //
 //   stage 0  stream pass        preprocessSignal (modem.js:213-232) statistics and,
@@ -37,7 +37,7 @@ constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
 #ifndef AMOD_FINE_MAX
-#define AMOD_FINE_MAX 1024
+#define AMOD_FINE_MAX 896 // keeps the stage-2 LDS under the 6-workgroups-per-CU budget
 #endif
 constexpr int FINE_MAX = AMOD_FINE_MAX;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
@@ -51,7 +51,10 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #define AMOD_RING 1                          // stream pass: rolling ring of SB + 1 chunk loads
 #endif
 #ifndef AMOD_WPE
-#define AMOD_WPE 5                           // waves per SIMD the register budget is sized for
+#define AMOD_WPE 6                           // waves per SIMD the register budget is sized for
+#endif
+#ifndef AMOD_SCAN_WPE
+#define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone): 96 registers
 #endif
 
 // Dynamic LDS, sized per launch from the reserved frame length (amod_fast_lds_bytes):
@@ -60,8 +63,9 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 //               cmax[256], pass-1 cache[SC_CACHE][32] (float2: top metric, uncertainty bits)
 //   stage 2   : tmpl[768] m[FINE_MAX + 8] yw[FINE_MAX + 800] q[FINE_MAX + 280] (folded window)
 //               E[FINE_MAX + 800] (prefix of squares of yw)
-//   stage 3-4 : xch[4][512] float2 (FFT exchange; decision bytes after each FFT; voted bits
-//               at finish), g[256] float2, twiddles, bits[bitc] (packed stream),
+//   stage 3-4 : xch[4][512] float2 (FFT exchange; decision bytes after each FFT; between
+//               rounds and at finish the packed stream bits[bitc] in its last bitc words and
+//               the voted bits from its start), g[256] float2, twiddles (tw1 rows 1-7, tw2),
 //               rows[rows_cap + 1] (word-aligned bit row per data symbol)
 extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_F (reinterpret_cast<float *>(amod_dyn))
@@ -81,9 +85,10 @@ constexpr int FQ_G = NWAVE * 512;             // float2 index of g
 #ifndef AMOD_TW_LDS
 #define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
 #endif
-constexpr int FQ_TW = FQ_G + kMaxBand;        // float2 index of the twiddles (tw1[512], tw2[64])
-constexpr int TW_WORDS = AMOD_TW_LDS ? 2 * (8 * 64 + 8 * 8) : 0;
-constexpr int FQ_BITS = 2 * (FQ_G + kMaxBand) + TW_WORDS; // word index of bits
+constexpr int FQ_TW = FQ_G + kMaxBand;        // float2 index of the twiddles (tw1 rows 1-7, tw2[64])
+constexpr int TW_WORDS = AMOD_TW_LDS ? 2 * (7 * 64 + 8 * 8) : 0;
+constexpr int FQ_XCH_WORDS = 2 * NWAVE * 512; // words of the exchange buffers
+constexpr int FQ_ROWS = 2 * (FQ_G + kMaxBand) + TW_WORDS; // word index of the symbol rows
 
 struct Smem {  // fixed part (static LDS)
   float rf[4 * NWAVE];
@@ -1113,7 +1118,11 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     const int nbytes_total = (nbits / cfg.rep) >> 3;
     const int nband = cfg.nband;
     const int wsym = (per_sym + 31) >> 5;      // words per symbol row
-    const int fq_sa = FQ_BITS + bitc;          // word index of the symbol rows
+    const int fq_sa = FQ_ROWS;                 // word index of the symbol rows
+    // the packed stream lives in the exchange buffers (dead between rounds and at finish;
+    // rebuilt from the rows after every round); bitc <= 2048 words, so it never reaches
+    // the voted bits written from the start of the region
+    uint32_t *const fq_bits = LDS_U + FQ_XCH_WORDS - bitc;
     // Jobs are numbered over the whole frame: job 0 = (CE, symbol 0), job j = (2j-1, 2j);
     // wave w owns jobs w, w+4, ... and prefetches its next job's samples while it
     // transforms and demaps the current one (across the round boundary too: the
@@ -1140,12 +1149,12 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     if (wave == 0 || 2 * wave - 1 < M) { load_job(wave, M, pf1, pf2); pf_job = wave; }
     // tables: every load issued before the first LDS store
     {
-      const float2 t1a = cfg.t.tw1[tid], t1b = cfg.t.tw1[tid + WG], t2 = cfg.t.tw2[tid & 63];
+      const float2 t1a = cfg.t.tw1[64 + tid], t1b = cfg.t.tw1[64 + min(tid + WG, 447)], t2 = cfg.t.tw2[tid & 63];
       const float kn = cfg.t.known[min(tid, nband - 1)];
       if (AMOD_TW_LDS) {
-        LDS_F2[FQ_TW + tid] = t1a;
-        LDS_F2[FQ_TW + WG + tid] = t1b;
-        if (tid < 64) LDS_F2[FQ_TW + 8 * 64 + tid] = t2;
+        LDS_F2[FQ_TW + tid] = t1a; // tw1 row q at FQ_TW + 64 (q - 1): row 0 is never read
+        if (tid + WG < 7 * 64) LDS_F2[FQ_TW + WG + tid] = t1b;
+        if (tid < 64) LDS_F2[FQ_TW + 7 * 64 + tid] = t2;
       }
       // the CE signs ride in the G slots until the CE job overwrites them with G
       if (tid < nband) LDS_F[2 * (FQ_G + tid)] = kn;
@@ -1212,7 +1221,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           const2 = __ballot(ne2) == 0;
           if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
           if (r == 0) STAMP(first ? 8 : 16);
-          if (AMOD_TW_LDS) fft512_wave(v, xb, LDS_F2 + FQ_TW, LDS_F2 + FQ_TW + 8 * 64);
+          if (AMOD_TW_LDS) fft512_wave(v, xb, LDS_F2 + FQ_TW - 64, LDS_F2 + FQ_TW + 7 * 64);
           else fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
           if (r == 0) STAMP(first ? 9 : 17);
           if (j == 0) {
@@ -1395,12 +1404,12 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       done = target;
       jdone = jend;
       // rows [0, done) -> the MSB-first bit stream the parse, vote and CRC read
-      repack_rows(LDS_U + fq_sa, wsym, per_sym, min(done, M), LDS_U + FQ_BITS);
+      repack_rows(LDS_U + fq_sa, wsym, per_sym, min(done, M), fq_bits);
       __syncthreads();
       // how much of the voted stream the parse reads; decode more symbols if needed
       if (tid == 0) {
         const int avail = ((min(done * per_sym, nbits) / cfg.rep) >> 3);
-        need_bytes = parse_need((LDS_U + FQ_BITS), cfg.rep, avail, nbytes_total, cfg.mode);
+        need_bytes = parse_need(fq_bits, cfg.rep, avail, nbytes_total, cfg.mode);
         int t = done;
         if (need_bytes > avail) {
           const int64_t raw = (int64_t)need_bytes * 8 * cfg.rep;
@@ -1424,13 +1433,13 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     {
       FRESH_ARGS;
       if (dbg && tid == 0) D->nsym = M;
-      const uint32_t *v = (LDS_U + FQ_BITS);
+      const uint32_t *v = fq_bits;
       const int nv = nbits / cfg.rep;
       if (cfg.rep > 1) {
         // vote only the decoded prefix (the parse reads need_bytes bytes)
         uint32_t *voted = reinterpret_cast<uint32_t *>(LDS_F2);
         const int decoded = min(done * per_sym, nbits);
-        block_vote((LDS_U + FQ_BITS), min(decoded, need_bytes * 8 * cfg.rep), cfg.rep, voted);
+        block_vote(fq_bits, min(decoded, need_bytes * 8 * cfg.rep), cfg.rep, voted);
         __syncthreads();
         v = voted;
       }
@@ -1479,7 +1488,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
 }
 // stream pass + Schmidl-Cox only (diagnostics: AMOD_STOP_AFTER=1); launched with the same
 // dynamic LDS as k_decode_fast, so the same number of workgroups share a CU
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_SCAN_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
   decode_fast<true, false>();
@@ -1501,6 +1510,6 @@ extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap) {
   using namespace amod;
   const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND + 8 * 32 * SC_CACHE;
   const int fine = 4 * (FINE_E + FINE_MAX + 800);
-  const int fq = 4 * (FQ_BITS + bits_cap + rows_cap + 1);
+  const int fq = 4 * (FQ_ROWS + rows_cap + 1);
   return (std::max(mom, std::max(fine, fq)) + 15) & ~15;
 }
