@@ -47,9 +47,6 @@ constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT ro
 #define AMOD_SB 8
 #endif
 constexpr int SB = AMOD_SB;                  // stream pass: chunks per load batch
-#ifndef AMOD_RING
-#define AMOD_RING 1                          // stream pass: rolling ring of SB + 1 chunk loads
-#endif
 #ifndef AMOD_WPE
 #define AMOD_WPE 6                           // waves per SIMD the register budget is sized for
 #endif
@@ -81,6 +78,7 @@ constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the wind
 // up to the last K step (K = n + 15 rounded up to 4)
 __host__ __device__ constexpr int fine_tab_len(int n) { return 16 + 4 * ((n + 15 + 3) >> 2); }
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 constexpr int FQ_G = NWAVE * 512;             // float2 index of g
 #ifndef AMOD_TW_LDS
 #define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
@@ -297,6 +295,12 @@ __device__ __forceinline__ float scan32(float v) {
 
 // sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
+// three dpp_sum8 interleaved (each DPP read of a fresh VALU result needs wait states)
+__device__ __forceinline__ void dpp_sum8x3(float &a, float &b, float &c) {
+  a += AMOD_DPP_F(a, 0xB1); b += AMOD_DPP_F(b, 0xB1); c += AMOD_DPP_F(c, 0xB1);
+  a += AMOD_DPP_F(a, 0x4E); b += AMOD_DPP_F(b, 0x4E); c += AMOD_DPP_F(c, 0x4E);
+  a += AMOD_DPP_F(a, 0x141); b += AMOD_DPP_F(b, 0x141); c += AMOD_DPP_F(c, 0x141);
+}
 __device__ __forceinline__ float dpp_sum8(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
@@ -444,32 +448,43 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * q, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
       };
-      auto step = [&](int q, const float4 a, const float4 nb) {
+      // per-sample work on packed pairs (v_pk_add/mul/fma_f32): u = x - x[0] of a chunk is
+      // computed once, when the chunk is its predecessor's partner, and carried in
+      // registers to its own step
+      const f2v c0v = {c0, c0};
+      auto u_of = [&](const float4 v, f2v &lo, f2v &hi) {
+        lo = f2v{v.x, v.y} - c0v;
+        hi = f2v{v.z, v.w} - c0v;
+      };
+      // chunk q (raw a, u in u01/u23) with its partner chunk q + 1 (raw nb -> n01/n23);
+      // block moments stored through pb[0..2] (block 8 q + lane / 8 of each array)
+      auto step = [&](int q, const float4 a, f2v u01, f2v u23, const float4 nb, f2v &n01, f2v &n23,
+                      float *const pb0, float *const pb1, float *const pb2) {
         const int kq = 256 * q;
-        float ua[4] = {a.x - c0, a.y - c0, a.z - c0, a.w - c0};
-        const float ub[4] = {nb.x - c0, nb.y - c0, nb.z - c0, nb.w - c0};
+        u_of(nb, n01, n23);
         if (kq >= ph && kq + 256 <= kfull) { // whole chunk inside the frame (wave-uniform)
           mn = min3_raw(mn, min3_raw(a.x, a.y, a.z), a.w);
           mxv = max3_raw(mxv, max3_raw(a.x, a.y, a.z), a.w);
         } else {
           const int k0 = kq + 4 * lane;
           const float av[4] = {a.x, a.y, a.z, a.w};
+          float ua[4] = {u01.x, u01.y, u23.x, u23.y};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             if (k0 + j >= ph && k0 + j < kfull) { mn = fminf(mn, av[j]); mxv = fmaxf(mxv, av[j]); }
             else ua[j] = 0.f;
           }
+          u01 = f2v{ua[0], ua[1]};
+          u23 = f2v{ua[2], ua[3]};
         }
-        const float s1 = dpp_sum8((ua[0] + ua[1]) + (ua[2] + ua[3]));
-        const float s2 = dpp_sum8(fmaf(ua[3], ua[3], fmaf(ua[2], ua[2], fmaf(ua[1], ua[1], ua[0] * ua[0]))));
-        const float sx = dpp_sum8(fmaf(ua[3], ub[3], fmaf(ua[2], ub[2], fmaf(ua[1], ub[1], ua[0] * ub[0]))));
+        const f2v p1 = u01 + u23;
+        const f2v p2 = __builtin_elementwise_fma(u23, u23, u01 * u01);
+        const f2v px = __builtin_elementwise_fma(u23, n23, u01 * n01);
+        float s1 = p1.x + p1.y, s2 = p2.x + p2.y, sx = px.x + px.y;
+        dpp_sum8x3(s1, s2, sx);
         sacc += s1; // every lane of a group holds its block's sum: lane 0 of the group counts it
-        if ((lane & 7) == 0) {
-          const int b = 8 * q + (lane >> 3);
-          LDS_F[b] = s1; LDS_F[nbc + b] = s2; LDS_F[2 * nbc + b] = sx;
-        }
+        if ((lane & 7) == 0) { *pb0 = s1; *pb1 = s2; *pb2 = sx; }
       };
-#if AMOD_RING
       // a ring of R chunk registers kept full: chunk q is stepped with its partner q + 1
       // (next slot), then its slot is refilled with chunk q + R, so about R - 1 loads per
       // wave stay in flight through the whole pass (no drain between batches). The
@@ -483,30 +498,20 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         c[j] = LD(min(q0 + j, q1));
         __builtin_amdgcn_sched_barrier(0);
       }
+      f2v cu01, cu23; // u of the chunk stepped next
+      u_of(c[0], cu01, cu23);
       for (int qb = q0; qb < q1; qb += R) {
+        // one moment address per array and ring turn; the steps use immediate offsets
+        float *const pb = LDS_F + 8 * qb + (lane >> 3);
+        float *const pb1 = pb + nbc, *const pb2 = pb1 + nbc;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
           const int q = qb + j;
-          if (q < q1) step(q, c[j], c[(j + 1) % R]);
+          if (q < q1) step(q, c[j], cu01, cu23, c[(j + 1) % R], cu01, cu23, pb + 8 * j, pb1 + 8 * j, pb2 + 8 * j);
           c[j] = LD(min(q + R, q1));
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else
-      // batches of SB chunks (+ the partner chunk): SB + 1 loads in flight, then SB steps
-      // in straight-line code so each step waits only for its own two chunks
-      for (int qb = q0; qb < q1; qb += SB) {
-        float4 c[SB + 1];
-#pragma unroll
-        for (int j = 0; j < SB + 1; ++j) {
-          c[j] = LD(qb + j);
-          __builtin_amdgcn_sched_barrier(0); // keep the loads in chunk order (vmcnt is in-order)
-        }
-#pragma unroll
-        for (int j = 0; j < SB; ++j)
-          if (qb + j < q1) step(qb + j, c[j], c[j + 1]); // partner of chunk q is chunk q + 1 (k + 256)
-      }
-#endif
       double sacc_d = (lane & 7) == 0 ? (double)sacc : 0.0;
       sacc_d = wave_sum(sacc_d);
       mn = -wmax(-mn);
