@@ -37,7 +37,7 @@ constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
 #ifndef AMOD_FINE_MAX
-#define AMOD_FINE_MAX 896 // keeps the stage-2 LDS under the 6-workgroups-per-CU budget
+#define AMOD_FINE_MAX 1024
 #endif
 constexpr int FINE_MAX = AMOD_FINE_MAX;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
@@ -69,11 +69,16 @@ extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_F2 (reinterpret_cast<float2 *>(amod_dyn))
 #define LDS_U (reinterpret_cast<uint32_t *>(amod_dyn))
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
-constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
-constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the window, span + 1 entries
 #ifndef AMOD_FINE_MFMA
 #define AMOD_FINE_MFMA 1 // folded fine correlation as Toeplitz tiles on the matrix cores
 #endif
+#if AMOD_FINE_MFMA
+// the metrics m overwrite the folded window q once every tile has been read (barrier)
+constexpr int FINE_TM = 0, FINE_YW = 768, FINE_Q = FINE_YW + FINE_MAX + 800, FINE_M = FINE_Q;
+#else
+constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
+#endif
+constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the window, span + 1 entries
 // zero-padded template table of the MFMA fine path for n taps: 16 zeros, n taps, zeros
 // up to the last K step (K = n + 15 rounded up to 4)
 __host__ __device__ constexpr int fine_tab_len(int n) { return 16 + 4 * ((n + 15 + 3) >> 2); }
@@ -967,12 +972,14 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         const int r16 = lane & 15, kk = lane >> 4;
         const int ntile = (P + 255) >> 8;
         const int sb = (CP + 15 + 3) >> 2;
-        for (int t = wave; t < ntile; t += NWAVE) {
+        static_assert(FINE_MAX <= 256 * NWAVE, "one tile per wave");
+        const int t = wave;
+        floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+        if (t < ntile) {
           const float *ta = LDS_F + FINE_TM + 16 + kk - r16;
           const float *tb = ta + la;
           const float *ya = LDS_F + FINE_Q + 256 * t + 16 * r16 + kk;
           const float *yb = LDS_F + FINE_YW + 512 + 256 * t + 16 * r16 + kk;
-          floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int st = 0; st < 68; st += 2) {
             c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * st], ya[4 * st], c0, 0, 0, 0);
@@ -984,6 +991,9 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
             c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st + 4], yb[4 * st + 4], c1, 0, 0, 0);
           }
           if (st < sb) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st], yb[4 * st], c0, 0, 0, 0);
+        }
+        __syncthreads(); // every tile has read q: the metrics may overwrite it
+        if (t < ntile) {
           const int d0 = 256 * t + 16 * r16 + 4 * kk;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
