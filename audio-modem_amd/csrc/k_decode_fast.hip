@@ -298,6 +298,14 @@ __device__ __forceinline__ float scan32(float v) {
   return v;
 }
 
+// inclusive prefix sum over the whole wave: scan32, then row_bcast:31 carries lane 31
+// into rows 2 and 3. Whole wave active.
+__device__ __forceinline__ float scan64(float v) {
+  v = scan32(v);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  return v;
+}
+
 // sum over each aligned group of 8 lanes, result in every lane of the group (DPP:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror). Whole wave active.
 // three dpp_sum8 interleaved (each DPP read of a fresh VALU result needs wait states)
@@ -918,12 +926,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           sq[k] = v * v;
           s += sq[k];
         }
-        float inc = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const float t = __shfl_up(inc, o, 64);
-          if (lane >= o) inc += t;
-        }
+        const float inc = scan64(s);
         if (lane == 63) sm.rf[wave] = inc;
         __syncthreads();
         float run = -s + inc, tot = 0.f;
@@ -980,10 +983,18 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           const float *tb = ta + la;
           const float *ya = LDS_F + FINE_Q + 256 * t + 16 * r16 + kk;
           const float *yb = LDS_F + FINE_YW + 512 + 256 * t + 16 * r16 + kk;
+          // operands of the next step pair are requested before this pair's MFMAs issue
+          // (the LDS latency hides under the matrix pipe instead of stalling each pair)
+          float a0 = ta[0], y0 = ya[0], a1 = ta[4], y1 = ya[4];
 #pragma unroll
           for (int st = 0; st < 68; st += 2) {
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * st], ya[4 * st], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * st + 4], ya[4 * st + 4], c1, 0, 0, 0);
+            float na0 = 0.f, ny0 = 0.f, na1 = 0.f, ny1 = 0.f;
+            if (st + 2 < 68) { na0 = ta[4 * st + 8]; ny0 = ya[4 * st + 8]; na1 = ta[4 * st + 12]; ny1 = ya[4 * st + 12]; }
+            __builtin_amdgcn_sched_barrier(0);
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, y0, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, y1, c1, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            a0 = na0; y0 = ny0; a1 = na1; y1 = ny1;
           }
           int st = 0;
           for (; st + 1 < sb; st += 2) {
@@ -1053,46 +1064,42 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       }
       }
       __syncthreads();
-      // argmax (first index), second best, uncertain-gate candidates
-      float b1 = -8.f;
+      // argmax (first index), second best and the best uncertain-gate candidate in one
+      // pass: per lane its best (first index), the best of its other positions and its
+      // best tagged metric; per wave the same with the second best taken over everything
+      // but the wave's argmax; thread 0 combines the waves (the global argmax belongs to
+      // exactly one wave, whose second best then stands in for its best)
+      float b1 = -8.f, b2 = -8.f, mt = -INFINITY;
       int i1x = 0x7fffffff;
       for (int k = tid; k < P; k += WG) {
         float m = LDS_F[FINE_M + k];
-        if (m > 2.f) m -= 4.f;
-        if (m > b1) { b1 = m; i1x = k; }
+        const bool tagged = m > 2.f;
+        if (tagged) { m -= 4.f; mt = fmaxf(mt, m); }
+        if (m > b1) { b2 = b1; b1 = m; i1x = k; }
+        else b2 = fmaxf(b2, m);
       }
       {
         const float bw = wmax(b1);
         const int iw = wmin_i(b1 == bw ? i1x : 0x7fffffff);
-        if (lane == 0) { sm.rf[wave] = bw; sm.ri[wave] = iw; }
-        __syncthreads();
-        if (tid == 0) {
-          float BB = -8.f;
-          int II = 0x7fffffff;
-          for (int i = 0; i < NWAVE; ++i)
-            if (sm.rf[i] > BB || (sm.rf[i] == BB && sm.ri[i] < II)) { BB = sm.rf[i]; II = sm.ri[i]; }
-          sm.fbest = BB; sm.start = II;
+        const float sw = wmax(i1x == iw ? b2 : b1);
+        const float tw = wmax(mt);
+        if (lane == 0) {
+          sm.rf[wave] = bw; sm.ri[wave] = iw; sm.rf[NWAVE + wave] = sw; sm.rf[2 * NWAVE + wave] = tw;
         }
-        __syncthreads();
       }
-      const float FB = sm.fbest;
-      const int kst = sm.start;
-      float b2 = -8.f;
-      int unc = 0;
-      for (int k = tid; k < P; k += WG) {
-        float m = LDS_F[FINE_M + k];
-        const bool tagged = m > 2.f;
-        if (tagged) m -= 4.f;
-        if (k != kst) b2 = fmaxf(b2, m);
-        if (tagged && m >= FB - eps_f) unc = 1;
-      }
-      b2 = wmax(b2); unc = wor_i(unc);
-      if (lane == 0) { sm.rf[wave] = b2; sm.ri[wave] = unc; }
       __syncthreads();
       if (tid == 0) {
-        float B2 = -8.f;
-        int U = 0;
-        for (int i = 0; i < NWAVE; ++i) { B2 = fmaxf(B2, sm.rf[i]); U |= sm.ri[i]; }
+        float FB = -8.f;
+        int kst = 0x7fffffff;
+        for (int i = 0; i < NWAVE; ++i)
+          if (sm.rf[i] > FB || (sm.rf[i] == FB && sm.ri[i] < kst)) { FB = sm.rf[i]; kst = sm.ri[i]; }
+        float B2 = -8.f, MT = -INFINITY;
+        for (int i = 0; i < NWAVE; ++i) {
+          B2 = fmaxf(B2, sm.ri[i] == kst ? sm.rf[NWAVE + i] : sm.rf[i]);
+          MT = fmaxf(MT, sm.rf[2 * NWAVE + i]);
+        }
+        const int U = MT >= FB - eps_f; // a tagged (uncertain-gate) metric near the best
+        sm.fbest = FB;
         const int dstar = w0 + kst;
         int flags = sm.flags;
         if (FB <= -7.f) {
