@@ -8,7 +8,9 @@ CRC-32) over the whole resident batch: BASELINE config C2, 10,000 QPSK frames of
 transmitter. Inputs are in HBM before the timed region. Frames are independent,
 so ranks shard them (weak scaling, no data-path collective).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+  (c4: decodeChunkFrame over 2 KB data-chunk windows, 32,000 per GPU = the 500 MB
+  file of BASELINE C4 across 8 GPUs)
   (N > 1: torch.distributed.run, one process per GPU; RCCL only for barrier/max)
 """
 import argparse
@@ -29,6 +31,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 SAMPLES_PER_FRAME = 35874     # C2: QPSK 1 KB legacy frame
 SAMPLES_PER_FRAME_C3 = 30114  # C3: 16-QAM 1 KB legacy frame
 PAYLOAD = 1024
+CHUNK = 2048                  # C4: data bytes per chunk frame
 
 
 def main():
@@ -36,9 +39,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
-                    help="c2: 10k QPSK 1 KB frames per GPU (the metric's config); c3: 100k 16-QAM 1 KB frames")
-    ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0: the config's, C2 10,000 / C3 100,000)")
+    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
+                    help="c2: 10k QPSK 1 KB frames per GPU (the metric's config); c3: 100k 16-QAM 1 KB frames; "
+                         "c4: 32k QPSK 2 KB data-chunk windows (decodeChunkFrame)")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames per GPU (0: the config's, C2 10,000 / C3 100,000 / C4 32,000)")
     ap.add_argument("--stream-chunks", type=int, default=2000,
                     help="C4-shaped stream for the streaming-receiver leg (0 = skip)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="CPU-baseline sample (0 = auto, -1 = skip)")
@@ -63,25 +68,44 @@ def main():
         if world > 1:
             dist.barrier()
 
-    C3 = args.config == "c3"
+    C3, C4 = args.config == "c3", args.config == "c4"
     cfg = amodem.preset("standard", "QAM16" if C3 else "QPSK", 1)
-    F = args.frames if args.frames > 0 else (100000 if C3 else 10000)
-    spf = SAMPLES_PER_FRAME_C3 if C3 else SAMPLES_PER_FRAME
+    F = args.frames if args.frames > 0 else (100000 if C3 else (32000 if C4 else 10000))
     dm = amodem.Demodulator(local)
     # ---- synthetic input, built on the GPU by k_tx (the reference transmitter, bit-exact)
     # from the workload's packets; the timed region is device-resident
-    pk, po, pl = amodem.synth_legacy_packets(F, PAYLOAD, "f.bin", first=rank * F)
-    pre, post = amodem.tx_silence(cfg, L.TX_LEGACY)
+    if C4:
+        # the file's chunks this rank owns: chunk seq = rank * F + i, bytes from xorshift32
+        pre, post = amodem.tx_silence(cfg, L.TX_CHUNK)
+        win = amodem.estimate_frame_samples(CHUNK + 11, "QPSK", 1)  # the receiver's window (app.js:853)
+        spf = pre + win + post
+        chunks = [amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), CHUNK) for i in range(F)]
+        pkts = [amodem.packet_chunk(chunks[i], rank * F + i) for i in range(F)]
+        pl = np.array([len(p) for p in pkts], np.int32)
+        po = np.concatenate([[0], np.cumsum(pl)[:-1]]).astype(np.int64)
+        pk = np.frombuffer(b"".join(pkts), np.uint8).copy()
+    else:
+        spf = SAMPLES_PER_FRAME_C3 if C3 else SAMPLES_PER_FRAME
+        pk, po, pl = amodem.synth_legacy_packets(F, PAYLOAD, "f.bin", first=rank * F)
+        pre, post = amodem.tx_silence(cfg, L.TX_LEGACY)
     offs = (np.arange(F, dtype=np.int64) * spf)
     lens = np.full(F, spf, np.int32)
     nsamples = int(lens.sum())
+    # what one step decodes: whole legacy frames, or the C4 windows (pre1 .. end of the
+    # estimated frame, as StreamingReceiver cuts them) in decodeChunkFrame mode
+    mode = L.MODE_CHUNK if C4 else L.MODE_RECEIVED
+    doffs = offs + pre if C4 else offs
+    dlens = np.full(F, win, np.int32) if C4 else lens
+    ndecoded = int(dlens.sum())
+    payload_bytes = CHUNK if C4 else PAYLOAD
     xs = torch.empty(nsamples + 16, dtype=torch.float32, device=dev)
     d_pk = torch.from_numpy(pk).to(dev)
     d_po, d_pl = torch.from_numpy(po).to(dev), torch.from_numpy(pl).to(dev)
     d_pre = torch.full((F,), pre, dtype=torch.int32, device=dev)
     d_post = torch.full((F,), post, dtype=torch.int32, device=dev)
     d_off = torch.from_numpy(offs).to(dev)
-    d_len = torch.from_numpy(lens).to(dev)
+    d_doff = torch.from_numpy(doffs).to(dev)
+    d_dlen = torch.from_numpy(dlens).to(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     tx_stream = torch.cuda.Stream(dev)  # a real (non-null) stream, so events and kernel share it
 
@@ -102,14 +126,14 @@ def main():
         tx_ms.append(e0.elapsed_time(e1))
     torch.cuda.synchronize(dev)
     tx_avg_ms = sum(tx_ms) / len(tx_ms)
-    stride = amodem.payload_stride(cfg, spf)
+    stride = amodem.payload_stride(cfg, int(dlens.max()))
     d_res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
     d_pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
 
-    dm.reserve(cfg, F, spf)
+    dm.reserve(cfg, F, int(dlens.max()))
 
     def step():
-        dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
+        dm.decode_device(cfg, mode, xs.data_ptr(), d_doff.data_ptr(), d_dlen.data_ptr(), F,
                          d_res.data_ptr(), d_pay.data_ptr(), stride, stream=stream)
 
     for _ in range(args.warmup):
@@ -121,13 +145,17 @@ def main():
     fallback = int((rec["flags"] != 0).sum())
     pay = d_pay.view(F, stride).cpu().numpy()
     for i in range(0, F, max(1, F // 16)):
-        r = amodem.to_reference(rec[i], pay[i].tobytes(), True)
-        assert r.get("data") == amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), PAYLOAD), (i, r.get("error"))
+        r = amodem.to_reference(rec[i], pay[i].tobytes(), not C4)
+        assert r.get("data") == amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), payload_bytes), (i, r.get("error"))
+        if C4:
+            assert r.get("seqNum") == rank * F + i, (i, r.get("seqNum"))
 
     lib = L.load()
     stream_res = stream_leg(amodem, L, local, args.stream_chunks) if (args.stream_chunks > 0 and rank == 0) else None
     # correlation-scan phase alone (k_corr_scan), measured before the timed region
-    scan = scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, spf)
+    # (decodeChunkFrame has no scan: the window starts at pre1)
+    scan = None if C4 else scan_phase(amodem, L, lib, cfg, local, xs, d_doff, d_dlen, F, d_res, d_pay, stride,
+                                      stream, spf)
     lib.amod_set_profiling(dm.ctx, 1)
     barrier()
     torch.cuda.synchronize(dev)
@@ -151,11 +179,11 @@ def main():
         ok, fallback = int(tsum[0].item()), int(tsum[1].item())
 
     if rank == 0:
-        total_samples = nsamples * world * args.steps
+        total_samples = ndecoded * world * args.steps
         value = total_samples / elapsed
-        payload_mbps = PAYLOAD * F * world * args.steps / elapsed / 1e6
+        payload_mbps = payload_bytes * F * world * args.steps / elapsed / 1e6
         fast_avg_s = fast_ms.value / max(1, nfast.value) / 1e3
-        algo_bytes = 4.0 * nsamples  # each float32 sample read once
+        algo_bytes = 4.0 * ndecoded  # each float32 sample read once
         achieved = algo_bytes / fast_avg_s / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -165,6 +193,7 @@ def main():
             if tj.get("frames") == F and tj.get("samples_per_frame") == spf:
                 traffic = tj.get("hbm_bytes_per_launch")
         mod = "QAM16" if C3 else "QPSK"
+        name = "C3" if C3 else ("C4" if C4 else "C2")
         cpu, tx_cpu, d2h = None, None, None
         if args.cpu_frames >= 0:
             # the CPU legs need the samples on the host: copy back the sample's frames
@@ -172,8 +201,8 @@ def main():
             t0 = time.perf_counter()
             xh = xs[: ncpu * spf].cpu().numpy()
             d2h = 4.0 * ncpu * spf / (time.perf_counter() - t0) / 1e9
-            cpu = cpu_baseline(xh, offs[:ncpu], lens[:ncpu], mod, "C3" if C3 else "C2")
-            tx_cpu = tx_cpu_baseline(amodem, cfg, min(ncpu, 4000), spf)
+            cpu = cpu_baseline(xh, doffs[:ncpu], dlens[:ncpu], mod, name, chunk=C4, payload=payload_bytes)
+            tx_cpu = None if C4 else tx_cpu_baseline(amodem, cfg, min(ncpu, 4000), spf)
         tx_bytes = 4.0 * nsamples + float(pl.sum())  # samples written + packet bytes read
         out = {
             "metric": METRIC,
@@ -188,11 +217,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference-equivalent TX, xorshift32 payloads)",
-            "config": {"workload": ("C3: 100k-frame 16-QAM batch demod per GPU" if C3 else
-                                    "C2: 10k-frame QPSK batch demod per GPU") +
-                                   " (decodeReceivedSignal, legacy 1 KB frames)",
-                       "frames_per_gpu": F, "samples_per_frame": spf, "fft": 512,
-                       "modulation": mod, "payload_bytes": PAYLOAD, "parallelism": f"frame-sharded x{world}"},
+            "config": {"workload": ("C4: 32k QPSK 2 KB data-chunk windows per GPU (decodeChunkFrame; value counts "
+                                    "the window samples decoded, 25,344 of each 28,431-sample frame)" if C4 else
+                                    ("C3: 100k-frame 16-QAM batch demod per GPU" if C3 else
+                                     "C2: 10k-frame QPSK batch demod per GPU") +
+                                    " (decodeReceivedSignal, legacy 1 KB frames)"),
+                       "frames_per_gpu": F, "samples_per_frame": int(dlens[0]), "fft": 512,
+                       "modulation": mod, "payload_bytes": payload_bytes, "parallelism": f"frame-sharded x{world}"},
             "payload_MB_per_s": payload_mbps,
             "frames_ok": ok,
             "frames_exact_fallback": fallback,
@@ -202,11 +233,11 @@ def main():
                          "kernel": "k_decode_fast", "kernel_ms_avg": fast_avg_s * 1e3,
                          "exact_kernel_ms_avg": exact_ms.value / max(1, nexact.value)},
             "cpu_baseline": cpu,
-            "scan_roofline": {"phase": "stream pass + Schmidl-Cox coarse search ("
-                                       "k_corr_scan: the same code compiled to stop there, results not written; 20 launches)",
-                              "kernel": "k_corr_scan", "kernel_ms_avg": scan, "achieved": algo_bytes / (scan / 1e3) / 1e9,
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": algo_bytes / (scan / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "scan_roofline": None if scan is None else {
+                "phase": "stream pass + Schmidl-Cox coarse search ("
+                         "k_corr_scan: the same code compiled to stop there, results not written; 20 launches)",
+                "kernel": "k_corr_scan", "kernel_ms_avg": scan, "achieved": algo_bytes / (scan / 1e3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo_bytes / (scan / 1e3) / 1e9 / HBM_PEAK_GBS},
             "tx": {"kernel": "k_tx", "what": "GPU transmitter (modulateOFDM + buildTransmitSignal, bit-exact) "
                                              "building this run's input", "kernel_ms_avg": tx_avg_ms,
                    "samples_per_s": nsamples / (tx_avg_ms / 1e3),
@@ -274,7 +305,7 @@ def stream_leg(amodem, L, device, nchunks=2000, chunk=2048):
             "reference_rate_note": "reference StreamingReceiver: 2.0e6 samples/s per core (SURVEY.md section 3.2)"}
 
 
-def cpu_baseline(x, offs, lens, mod, name):
+def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
     """The C restatement of the reference RX (oracle/, kind 'port') on this host's
     cores over a bounded sample of the same frames, repeated to ~1 s of wall time
     (~16 s of CPU work on 16 threads)."""
@@ -283,15 +314,15 @@ def cpu_baseline(x, offs, lens, mod, name):
     c = O.cfg("standard")
     t, reps = 0.0, 0
     while t < 1.0 and reps < 8:
-        dt, st, _ = O.bench_decode(c, x, offs, lens, mod, 1, threads)
+        dt, st, _ = O.bench_decode(c, x, offs, lens, mod, 1, threads, chunk=chunk)
         assert (st == 0).all()
         t += dt
         reps += 1
     samples = float(lens.sum()) * reps
     return {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"{len(offs)} {name} frames x {reps} passes ({int(samples)} samples), "
-                      f"oracle/amodem_oracle.c, {threads} threads",
-            "payload_MB_per_s": PAYLOAD * len(offs) * reps / t / 1e6, "seconds": t}
+                      f"oracle/amodem_oracle.c{' (decodeChunkFrame)' if chunk else ''}, {threads} threads",
+            "payload_MB_per_s": payload * len(offs) * reps / t / 1e6, "seconds": t}
 
 
 def tx_cpu_baseline(amodem, cfg, nframes, spf):

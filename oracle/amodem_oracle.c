@@ -683,7 +683,7 @@ typedef struct {
   const float *x;
   const int64_t *off;
   const int32_t *len;
-  int nframes, mod, rep, tid, nthreads;
+  int nframes, mod, rep, tid, nthreads, chunk;
   int32_t *status;
   uint32_t *crc;
 } bench_job;
@@ -692,26 +692,38 @@ static void *bench_worker(void *arg) {
   bench_job *j = arg;
   for (int f = j->tid; f < j->nframes; f += j->nthreads) {
     orc_result r;
-    orc_decode_received(j->c, j->x + j->off[f], j->len[f], j->mod, j->rep, &r, NULL, 0);
+    if (j->chunk) orc_decode_chunk(j->c, j->x + j->off[f], j->len[f], j->mod, j->rep, &r, NULL, 0);
+    else orc_decode_received(j->c, j->x + j->off[f], j->len[f], j->mod, j->rep, &r, NULL, 0);
     if (j->status) j->status[f] = r.status;
     if (j->crc) j->crc[f] = r.actual_crc;
   }
   return NULL;
 }
 
-double orc_bench_decode(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
-                        int nframes, int mod, int rep, int threads, int32_t *status_out, uint32_t *crc_out) {
+static double bench_run(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len, int nframes,
+                        int mod, int rep, int threads, int32_t *status_out, uint32_t *crc_out, int chunk) {
   if (threads < 1) threads = 1;
   pthread_t *th = malloc(sizeof(pthread_t) * (size_t)threads);
   bench_job *jobs = malloc(sizeof(bench_job) * (size_t)threads);
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (int t = 0; t < threads; t++) {
-    jobs[t] = (bench_job){c, x, off, len, nframes, mod, rep, t, threads, status_out, crc_out};
+    jobs[t] = (bench_job){c, x, off, len, nframes, mod, rep, t, threads, chunk, status_out, crc_out};
     pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
   }
   for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   free(th); free(jobs);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+double orc_bench_decode(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
+                        int nframes, int mod, int rep, int threads, int32_t *status_out, uint32_t *crc_out) {
+  return bench_run(c, x, off, len, nframes, mod, rep, threads, status_out, crc_out, 0);
+}
+
+/* decodeChunkFrame over frames that start at pre1 (the C4 windows) */
+double orc_bench_decode_chunk(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
+                              int nframes, int mod, int rep, int threads, int32_t *status_out, uint32_t *crc_out) {
+  return bench_run(c, x, off, len, nframes, mod, rep, threads, status_out, crc_out, 1);
 }

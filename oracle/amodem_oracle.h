@@ -116,6 +116,9 @@ void orc_add_noise_div(const float *in, int n, double div, uint32_t seed, float 
 double orc_bench_decode(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
                         int nframes, int mod, int rep, int threads, int32_t *status_out,
                         uint32_t *crc_out);
+double orc_bench_decode_chunk(const orc_cfg *c, const float *x, const int64_t *off, const int32_t *len,
+                        int nframes, int mod, int rep, int threads, int32_t *status_out,
+                        uint32_t *crc_out);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,8 @@ def lib():
             "orc_add_noise_div": (None, [f32p, C.c_int, C.c_double, C.c_uint32, f32p]),
             "orc_bench_decode": (C.c_double, [cfgp, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                               C.c_int, C.c_void_p, C.c_void_p]),
+            "orc_bench_decode_chunk": (C.c_double, [cfgp, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                              C.c_int, C.c_void_p, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -241,11 +243,13 @@ def crc32(b: bytes) -> int:
     return lib().orc_crc32(b, len(b))
 
 
-def bench_decode(c: Cfg, x: np.ndarray, offs: np.ndarray, lens: np.ndarray, mod: str, rep: int, threads: int):
+def bench_decode(c: Cfg, x: np.ndarray, offs: np.ndarray, lens: np.ndarray, mod: str, rep: int, threads: int,
+                 chunk: bool = False):
     offs = np.ascontiguousarray(offs, np.int64)
     lens = np.ascontiguousarray(lens, np.int32)
     status = np.zeros(len(offs), np.int32)
     crc = np.zeros(len(offs), np.uint32)
-    t = lib().orc_bench_decode(C.byref(c), x.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(offs),
+    fn = lib().orc_bench_decode_chunk if chunk else lib().orc_bench_decode
+    t = fn(C.byref(c), x.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(offs),
                                MODS[mod], rep, threads, status.ctypes.data, crc.ctypes.data)
     return t, status, crc

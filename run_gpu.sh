@@ -8,6 +8,7 @@ for s in "$@"; do
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3;;
     benchc3) run bench_c3 600 python bench.py --config c3 --steps 10 --warmup 2;;
+    benchc4) run bench_c4 600 python bench.py --config c4 --steps 10 --warmup 2 --stream-chunks 0;;
     stamps) run stamps 300 python tools/stamps.py;;
     stages) run stages 600 env STAGES=${STAGES:-0,1,2,3,99} python tools/stage_profile.py;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv rocpd -- python bench.py --steps 20 --warmup 3 --cpu-frames -1;;
