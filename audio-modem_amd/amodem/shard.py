@@ -5,7 +5,8 @@ modem.js:557, 770), so a batch splits into contiguous frame ranges, one per rank
 balanced by sample count; each rank decodes its range on its own device with no
 data-path collective. Only the 96-byte result records (and, if wanted, the
 payload slots) travel back to rank 0, through one all-gather of fixed-size
-buffers (RCCL over xGMI with the nccl backend, gloo on CPU).
+buffers (RCCL over xGMI with the nccl backend, gloo on CPU), or — for the device-
+resident bench path — one gather into rank 0 (`gather_to_root`).
 """
 from __future__ import annotations
 
@@ -63,6 +64,37 @@ def gather_records(records: np.ndarray, payload: np.ndarray | None, counts: list
     if payload is not None:
         pay = allgather_rows(payload, payload.shape[1])
     return rec, pay
+
+
+def gather_to_root(rows, counts: list[int], dst: int = 0, group=None):
+    """Gather every rank's rows (a uint8 tensor [counts[rank], width], device-resident
+    under RCCL) to rank `dst`, in rank order, without leaving the device.
+
+    This is the C4 collective of SURVEY.md §8e: one gather (RCCL over xGMI, point to
+    point into the root) of the fixed-size result records and of the payload slots;
+    no all-reduce, no halo exchange. Rows are padded to the largest count so one
+    fixed-size collective suffices. Returns the [sum(counts), width] tensor on `dst`
+    and None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(counts) != world or rows.shape[0] != counts[rank] or rows.dtype != torch.uint8 or rows.dim() != 2:
+        raise ValueError(f"gather_to_root: rows {tuple(rows.shape)} {rows.dtype} vs counts {counts} at rank {rank}")
+    m = max(counts)
+    buf = rows
+    if rows.shape[0] != m:
+        buf = torch.zeros((m, rows.shape[1]), dtype=torch.uint8, device=rows.device)
+        buf[: rows.shape[0]] = rows
+    buf = buf.contiguous()
+    if dist.get_backend(group) == "gloo" and buf.is_cuda:  # gloo gathers host buffers only
+        buf = buf.cpu()
+    outs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, outs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([outs[r][: counts[r]] for r in range(world)])
 
 
 def decode_sharded(dm, samples: np.ndarray, offsets, lengths, cfg, mode, group=None):

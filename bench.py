@@ -11,7 +11,8 @@ so ranks shard them (weak scaling, no data-path collective).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
   (c4: decodeChunkFrame over 2 KB data-chunk windows, 32,000 per GPU = the 500 MB
   file of BASELINE C4 across 8 GPUs)
-  (N > 1: torch.distributed.run, one process per GPU; RCCL only for barrier/max)
+  (N > 1: torch.distributed.run, one process per GPU; RCCL for the barrier, the
+  max-over-ranks time and, after the timed region, the gather of results into rank 0)
 """
 import argparse
 import ctypes as C
@@ -58,9 +59,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AMOD_BENCH_BACKEND=gloo rehearses the N > 1 flow with several ranks on one GPU
+    # (RCCL refuses two ranks per device); the driver's runs use the default, RCCL
+    backend = os.environ.get("AMOD_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -169,6 +178,10 @@ def main():
     lib.amod_kernel_times(dm.ctx, C.byref(fast_ms), C.byref(nfast), C.byref(exact_ms), C.byref(nexact))
     lib.amod_set_profiling(dm.ctx, 0)
 
+    gather = None
+    if world > 1:
+        gather = gather_leg(amodem, dist, torch, dev, rank, world, F, stride, d_res, d_pay, C4, payload_bytes)
+
     t = torch.tensor([elapsed, float(ok), float(fallback)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t[:1].clone()
@@ -245,11 +258,52 @@ def main():
                                 "unit": "GB/s", "frac": tx_bytes / (tx_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
                    "cpu_baseline": tx_cpu},
             "stream": stream_res,
+            "gather": gather,
         }
         print(json.dumps(out), flush=True)
     dm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def gather_leg(amodem, dist, torch, dev, rank, world, F, stride, d_res, d_pay, chunk_mode, payload_bytes, reps=3):
+    """N > 1, after the timed region: the device-resident result records (96 B/frame)
+    and payload slots of every rank gathered into rank 0 over RCCL (SURVEY.md §8e,
+    BASELINE C4's "RCCL gather over xGMI"), timed with barrier + synchronize on both
+    sides, then every gathered record checked on rank 0 (status, CRC, and for C4 the
+    file's sequence numbers 0 .. world*F-1 in rank order)."""
+    from amodem.shard import gather_to_root
+
+    counts = [F] * world
+    res_rows = d_res.view(F, 96)
+    pay_rows = d_pay.view(F, stride)[:, : min(stride, payload_bytes + 64)].contiguous()  # data bytes + header slack
+    ms = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        g_res = gather_to_root(res_rows, counts, dst=0)
+        g_pay = gather_to_root(pay_rows, counts, dst=0)
+        torch.cuda.synchronize(dev)
+        ms.append((time.perf_counter() - t0) * 1e3)
+    tmax = torch.tensor([max(ms[1:]) if len(ms) > 1 else ms[0]], dtype=torch.float64, device=dev)
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    if rank != 0:
+        return None
+    rec = np.frombuffer(g_res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
+    pay = g_pay.cpu().numpy()
+    ok = bool(((rec["status"] == 0) & (rec["crc_valid"] == 1)).all()) and len(rec) == world * F
+    if chunk_mode:
+        ok = ok and bool((rec["seq_num"] == np.arange(world * F)).all())
+    for i in range(0, world * F, max(1, world * F // 64)):  # payload rows follow their records
+        r = amodem.to_reference(rec[i], pay[i].tobytes(), not chunk_mode)
+        ok = ok and r.get("data") == amodem.synth_payload(0x9E3779B9 ^ i, payload_bytes)
+    nbytes = (res_rows.numel() + pay_rows.numel()) * (world - 1)  # what crosses xGMI into rank 0
+    t = float(tmax.item())
+    return {"what": "result records + payload slots of every rank gathered into rank 0 (%s gather)"
+                    % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()),
+            "frames": world * F, "bytes_into_root": nbytes, "ms": t, "GBps": nbytes / (t / 1e3) / 1e9,
+            "records_ok": ok}
 
 
 def scan_phase(amodem, L, lib, cfg, local, xs, d_off, d_len, F, d_res, d_pay, stride, stream, spf, reps=20):

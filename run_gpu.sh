@@ -8,6 +8,8 @@ for s in "$@"; do
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3;;
     benchc3) run bench_c3 600 python bench.py --config c3 --steps 10 --warmup 2;;
+    bench2g) run bench2g 600 env AMOD_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0 &&
+            run bench2g_c4 600 env AMOD_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config c4 --frames 4000 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0;;
     benchc4) run bench_c4 600 python bench.py --config c4 --steps 10 --warmup 2 --stream-chunks 0;;
     stamps) run stamps 300 python tools/stamps.py;;
     stages) run stages 600 env STAGES=${STAGES:-0,1,2,3,99} python tools/stage_profile.py;;

@@ -77,6 +77,44 @@ def test_gather_records_gloo_world2():
         assert p0 == [i & 0xFF for i in range(n)]  # payload rows follow their records
 
 
+def _root_worker(rank, world, port, counts, q):
+    import torch
+    import torch.distributed as dist
+    from amodem.shard import gather_to_root
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first = sum(counts[:rank])
+        rows = torch.zeros((counts[rank], 96), dtype=torch.uint8)
+        rows[:, 0] = (torch.arange(first, first + counts[rank]) & 0xFF).to(torch.uint8)
+        rows[:, 1] = rank
+        out = gather_to_root(rows, counts, dst=0)
+        q.put((rank, None if out is None else out[:, :2].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("counts", [[5, 5], [7, 0], [3, 9]])
+def test_gather_to_root_gloo_world2(counts):
+    """The bench's C4 collective: records/payload rows gathered into rank 0 in rank
+    order, ragged and empty shards padded to one fixed-size gather."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_root_worker, args=(r, 2, port, counts, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert out[1] is None
+    owner = [r for r in range(2) for _ in range(counts[r])]
+    assert out[0] == [[i & 0xFF, owner[i]] for i in range(sum(counts))]
+
+
 def _ev(pos, end, block, ac_pos, status=0):
     from amodem import _lib as L
     e = L.StreamEvent()
