@@ -36,13 +36,17 @@ namespace {
 constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
+constexpr float ACTIVE_EB = 0.05f;           // normalised 32-sample block energy of "signal" (rms ~0.04 of peak)
 #ifndef AMOD_FINE_MAX
 #define AMOD_FINE_MAX 1024
 #endif
 constexpr int FINE_MAX = AMOD_FINE_MAX;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
 constexpr int SC_CACHE = 16;                 // candidate blocks whose per-position results stay in LDS
-constexpr int FIRST_SYMS = 7;                // data symbols of the first FFT round (+ CE)
+#ifndef AMOD_FIRST_SYMS
+#define AMOD_FIRST_SYMS 7
+#endif
+constexpr int FIRST_SYMS = AMOD_FIRST_SYMS;  // data symbols of the first FFT round (+ CE)
 #ifndef AMOD_SB
 #define AMOD_SB 8
 #endif
@@ -99,7 +103,7 @@ struct Smem {  // fixed part (static LDS)
   double rd[2 * NWAVE];
   uint32_t ru[16];
   // per-frame scalars (written by one thread, read after a barrier)
-  int status, flags, coarse, clo, chi, start, ncand, target;
+  int status, flags, coarse, clo, chi, start, ncand, target, last_blk;
   float A, B, Bu, errw, cbest, cblo, cbhi, fbest, gmax, zce;
   double mean, mx;
 };
@@ -555,7 +559,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           if (mx > 1e-6) { A = (float)(1.0 / mx); B = (float)(-mean / mx); Bu = (float)(((double)c0 - mean) / mx); }
           else { A = 1.f; B = (float)(-mean); Bu = (float)((double)c0 - mean); }
         }
-        sm.flags = flags; sm.A = A; sm.B = B; sm.Bu = Bu; sm.mean = mean; sm.mx = mx;
+        sm.flags = flags; sm.A = A; sm.B = B; sm.Bu = Bu; sm.mean = mean; sm.mx = mx; sm.last_blk = -1;
         if (dbg) { D->mean = mean; D->mx = mx; }
       }
       __syncthreads();
@@ -576,12 +580,17 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         }
       }
       __syncthreads();
+      int last = -1; // last block with signal energy (sizes the first FFT round only)
       for (int b = tid; b < NB; b += WG) {
         const float s1b = LDS_F[b], s2b = fmaxf(LDS_F[nbc + b], 0.f);
         const int nv = min(BLK * b + BLK, K) - max(BLK * b, ph);
-        LDS_F[nbc + b] = fmaf(AA, s2b, fmaf(2.f * AB, s1b, (float)nv * BB));
+        const float eb = fmaf(AA, s2b, fmaf(2.f * AB, s1b, (float)nv * BB));
+        LDS_F[nbc + b] = eb;
+        if (eb > ACTIVE_EB) last = b;
         tmax = fmaxf(tmax, AA * s2b + 2.f * aAB * sqrt_a(32.f * s2b) + 32.f * BB);
       }
+      last = wmax_i(last);
+      if (lane == 0 && last >= 0) atomicMax(&sm.last_blk, last);
       // blocks whose pairs leave the frame (and block 0 when the frame starts mid-float4):
       // summed directly from the samples, one 32-lane group per block
       const float Af = sm.A, Bf = sm.B;
@@ -1194,8 +1203,17 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     const bool pil_multi = __ballot(npl > 1) != 0;
     if (tid == 0) {
       sm.gmax = 0.f; sm.zce = 0.f;
-      sm.target = dbg ? M : min(M, FIRST_SYMS);
-      if (sm.target * per_sym > bitc * 32 || sm.target * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
+      int t = min(M, FIRST_SYMS);
+      if (t * per_sym > bitc * 32 || t * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
+      // the first round also covers every symbol up to the end of the frame's signal
+      // energy (the trailing silence is skipped as before): a transmitted frame's data
+      // then decodes in one round. Rounds stay header-driven, so this only sets the
+      // round size, never what the result holds.
+      const int act_end = BLK * (sm.last_blk + 1) - ph; // first sample after the last active block
+      const int tact = ((act_end - data0 + SYM - 1) / SYM) | 1;  // whole jobs
+      const int tcap = min(bitc * 32 / per_sym, w.rows_cap / wsym);
+      if (sm.last_blk >= 0) t = max(t, min(min(M, tact), tcap));
+      sm.target = dbg ? M : t;
     }
     __syncthreads();
     if (sm.flags) goto to_exact;
