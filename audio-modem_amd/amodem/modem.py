@@ -230,29 +230,39 @@ class Demodulator:
 
     def stream_shard(self, cfg: L.Cfg, samples: np.ndarray, lo: int, hi: int, own_lo: int, own_hi: int,
                      start: "L.StreamState | None" = None, meta_received: bool = False, chunk_size: int = 0,
-                     until_meta: bool = False, stride: int = 0, max_events: int = 1 << 18):
+                     until_meta: bool = False, stride: int = 0, max_events: int | None = None):
         """One shard of a sharded stream receive (amod_stream_shard): samples = stream
         samples [lo, hi). Returns (events: list of (StreamEvent copy), payload uint8
         [n, stride], fails: list of (block, pos), ema: (state before own_lo, state at
         own_hi - 1), end: StreamState)."""
         x = np.ascontiguousarray(samples, np.float32)
         assert len(x) == hi - lo
-        stride = stride or payload_stride(cfg, 1 << 20)
-        ev = (L.StreamEvent * max_events)()
-        pay = np.zeros((max_events, stride), np.uint8)
+        if not stride:  # rows wide enough for the longest window this shard can cut
+            win = int(self._L.amod_estimate_frame_samples(C.byref(cfg), (chunk_size or 4096) + 11))
+            stride = payload_stride(cfg, max(win, int(self._L.amod_estimate_frame_samples(C.byref(cfg), 4107))))
+        # the receiver demodulates at most one window and fails at most one refinement per
+        # 4096-sample block (app.js:749-773), so these bounds never truncate
+        nblk = (hi - lo) // 4096 + 1
+        max_events = nblk if max_events is None else max_events
+        ev = (L.StreamEvent * max(max_events, 1))()
+        pay = np.zeros((max(max_events, 1), stride), np.uint8)
         nev, nf = C.c_int64(), C.c_int64()
-        fails = np.zeros(2 * 4096, np.int64)
+        max_fails = nblk
+        fails = np.zeros(2 * max_fails, np.int64)
         ema = np.zeros(2, np.float64)
         end = L.StreamState()
         with self._lock:
             L.check(self._L.amod_stream_shard(self.ctx, C.byref(cfg), x.ctypes.data, lo, hi, own_lo, own_hi,
                                               C.byref(start) if start is not None else None, int(meta_received),
                                               int(chunk_size), int(until_meta), ev, max_events, C.byref(nev),
-                                              pay.ctypes.data, stride, fails.ctypes.data, 4096, C.byref(nf),
+                                              pay.ctypes.data, stride, fails.ctypes.data, max_fails, C.byref(nf),
                                               ema.ctypes.data, C.byref(end)), self.ctx)
-        n = min(nev.value, max_events)
+        if nev.value > max_events or nf.value > max_fails:
+            raise RuntimeError(f"stream_shard: {nev.value} windows / {nf.value} failed refinements exceed the "
+                               f"buffers ({max_events} / {max_fails})")
+        n = nev.value
         events = [L.StreamEvent.from_buffer_copy(ev[i]) for i in range(n)]
-        fl = [(int(fails[2 * i]), int(fails[2 * i + 1])) for i in range(min(nf.value, 4096))]
+        fl = [(int(fails[2 * i]), int(fails[2 * i + 1])) for i in range(nf.value)]
         return events, pay[:n], fl, (float(ema[0]), float(ema[1])), end
 
     # ------------------------------------------------------------ transmitter

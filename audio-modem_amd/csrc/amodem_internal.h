@@ -419,4 +419,5 @@ hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, con
 int amod_ctx_device(const amod_ctx *ctx);
 hipStream_t amod_ctx_stream(const amod_ctx *ctx);
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code);
+int amod_cfg_valid(const amod_cfg *cfg); // the decode entry points' configuration check
 }

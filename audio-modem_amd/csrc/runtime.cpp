@@ -401,18 +401,17 @@ int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) 
   const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
       std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
   HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 2 * (size_t)std::max(nframes, 1))));
-  const int64_t xs_stride = (max_len + 64) & ~int64_t(63);
+  // grow-only: a later, smaller reservation never shrinks a stride or the slot count that
+  // earlier (longer) frames were sized for
   const int64_t words = (max_bits_for(c, max_len) + 31) / 32;
-  const int64_t bits_stride = ((2 * words + 32) + 63) & ~int64_t(63);
-  if (ctx->nslots < nslots || ctx->xs_stride < xs_stride) {
-    HIP_TRY(ctx->xs.ensure(sizeof(float) * (size_t)(nslots * xs_stride)));
-    ctx->xs_stride = xs_stride;
-  }
-  if (ctx->nslots < nslots || ctx->bits_stride < bits_stride) {
-    HIP_TRY(ctx->bits.ensure(sizeof(uint32_t) * (size_t)(nslots * bits_stride)));
-    ctx->bits_stride = bits_stride;
-  }
-  ctx->nslots = std::max<int>(ctx->nslots, (int)nslots);
+  const int64_t xs_stride = std::max<int64_t>(ctx->xs_stride, (max_len + 64) & ~int64_t(63));
+  const int64_t bits_stride = std::max<int64_t>(ctx->bits_stride, ((2 * words + 32) + 63) & ~int64_t(63));
+  const int64_t slots = std::max<int64_t>(ctx->nslots, nslots);
+  HIP_TRY(ctx->xs.ensure(sizeof(float) * (size_t)(slots * xs_stride)));
+  HIP_TRY(ctx->bits.ensure(sizeof(uint32_t) * (size_t)(slots * bits_stride)));
+  ctx->xs_stride = xs_stride;
+  ctx->bits_stride = bits_stride;
+  ctx->nslots = (int)slots;
   ctx->max_len = std::max<int64_t>(ctx->max_len, max_len);
   return AMOD_SUCCESS;
 }
@@ -603,6 +602,7 @@ int amod_abi_version(void) { return AMOD_ABI_VERSION; }
 int amod_ctx_device(const amod_ctx *ctx) { return ctx ? ctx->device : 0; }
 hipStream_t amod_ctx_stream(const amod_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code) { return fail(ctx, msg, code); }
+int amod_cfg_valid(const amod_cfg *cfg) { return validate(cfg); }
 
 int amod_open(int device, amod_ctx **out) {
   if (!out) return fail(nullptr, "null out", AMOD_ERR_ARG);

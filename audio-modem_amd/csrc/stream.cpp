@@ -374,7 +374,7 @@ struct Prepass {
     if (total) {
       DBuf d_pre1, d_first, d_base, d_count, d_out;
       std::vector<float> p1(cfg->symbol_len);
-      amod_preamble1(cfg, p1.data());
+      if (amod_preamble1(cfg, p1.data()) != AMOD_SUCCESS) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
       const int nr = (int)first_loc.size();
       S_TRY(d_pre1.alloc(sizeof(float) * p1.size()));
       S_TRY(d_first.alloc(sizeof(int64_t) * nr));
@@ -520,6 +520,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   const auto t_start = clk::now();
   if (!ctx || !cfg || n < 0 || (n && !samples) || (max_frames > 0 && !frames) || !nframes_out)
     return amod_ctx_fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  if (!amod_cfg_valid(cfg)) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
   S_TRY(hipSetDevice(amod_ctx_device(ctx)));
   hipStream_t s = amod_ctx_stream(ctx);
   const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
@@ -651,6 +652,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       own_lo % kBlock || (hi > lo && !samples) || !nevents || !nfails || (max_events > 0 && !events) ||
       (max_events > 0 && payload && stride <= 0))
     return amod_ctx_fail(ctx, "invalid shard arguments", AMOD_ERR_ARG);
+  if (!amod_cfg_valid(cfg)) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
   S_TRY(hipSetDevice(amod_ctx_device(ctx)));
   hipStream_t s = amod_ctx_stream(ctx);
   Prepass pp;
