@@ -23,6 +23,7 @@ OPT_SOFT_COMBINE = 2  # not reference behaviour: soft repetition combining (opt-
 
 OK = 0
 E_CAPACITY = 100
+FLAG_SPAN = 1 << 9
 FLAG_EXACT = 1 << 15
 
 
@@ -107,6 +108,7 @@ SIGNATURES = {
                                    C.c_int64, C.c_uint32]),
     "amod_synchronize": (C.c_int, [_P]),
     "amod_set_profiling": (C.c_int, [_P, C.c_int]),
+    "amod_kernel_breakdown": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "amod_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int64)]),
     "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,

@@ -2,11 +2,12 @@
 //
 // Frame pipeline (per frame, mirrors modem.js decodeReceivedSignal 557-654 and
 // decodeChunkFrame 770-803):
-//   k_decode_fast  (k_decode_fast.hip)  one 256-thread workgroup per frame, the
-//                   frame streamed once from HBM, fp32 arithmetic with guard bands on
-//                   every discrete decision; a frame whose decision falls inside a
-//                   guard band (or that exceeds the launch's LDS capacities) is
-//                   appended to the exact list.
+//   fast path      (k_decode_fast.hip) k_detect (one workgroup per frame, the frame
+//                   streamed once from HBM) -> k_demod (persistent waves, one frame
+//                   at a time per wave); fp32 arithmetic with guard bands on every
+//                   discrete decision; a frame whose decision falls inside a guard band
+//                   (or that exceeds the launch's capacities) is appended to the exact
+//                   list.
 //   k_decode_exact (k_decode_exact.hip) replays the reference arithmetic in IEEE
 //                   double, operation for operation, for the listed frames.
 // Both end in finish_frame() below: majority vote, MSB-first byte packing, frame
@@ -26,6 +27,7 @@ constexpr int kMaxBand = 256;  // sub_end < fft/2
 constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
 constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
+constexpr int kCrcMats = 512;  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
 
 // Device-resident tables, built once per configuration by the runtime.
 struct DevTables {
@@ -39,6 +41,7 @@ struct DevTables {
   const uint32_t *crc_m1;  // [32][4][256] shift-by-(16*q) zero-byte operators, q<32
   const uint32_t *crc_m2;  // [32][4][256] shift-by-(512*q) operators, q<32
   const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
+  const uint32_t *crc_mat; // [kCrcMats][32] shift-by-(16*q) zero-byte operators as GF(2) matrices (column i = image of bit i)
   const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
   const double2 *tw_inv;   // [511] inverse-transform recurrence twiddles (fftIterative, ifft)
   const float *tmpl;       // [3][symbol_len] pre1, pre2, CE symbols (f32, before normalisation)
@@ -70,11 +73,26 @@ struct DevTxWork {
   int32_t nframes;
 };
 
+// k_detect / k_chunk_prep -> k_demod: one record per frame
+enum { ROUTE_DEMOD = 0, ROUTE_DONE = 1, ROUTE_EXACT = 2 };
+struct DetRec {
+  int32_t route;   // ROUTE_DEMOD: demodulate; ROUTE_DONE: result written; ROUTE_EXACT: listed
+  int32_t flags;   // reserved (0)
+  int32_t start;   // preambleIdx (fine timing); 0 in chunk mode
+  int32_t M, T;    // whole data symbols (demodulateOFDM numSym); symbols demodulated (prefix)
+  int32_t coarse;  // Schmidl-Cox index (in the plateau)
+  float A, B;      // normalisation y = A x + B (preprocessSignal)
+  float fbest;     // best fine metric
+  float pad[3];
+};
+static_assert(sizeof(DetRec) == 48, "DetRec layout");
+
 struct DevWork {
   const float *samples;
   const int64_t *off;
   const int32_t *len;
   int32_t nframes;
+  int32_t f0, f1;     // k_detect / k_chunk_prep / k_demod: the launch's frames [f0, f1)
   amod_result *res;
   uint8_t *payload;
   int64_t stride;
@@ -88,9 +106,13 @@ struct DevWork {
   int64_t bits_stride;// words per slot
   uint32_t options;
   unsigned long long *stamps; // diagnostics (AMOD_STAMPS=1): per-frame s_memtime marks, 32 per frame
-  int32_t nb_cap;     // fast kernel: Schmidl-Cox moment blocks per frame (dynamic LDS)
-  int32_t bits_cap;   // fast kernel: packed bit-stream words per frame (dynamic LDS)
-  int32_t rows_cap;   // fast kernel: symbol-row words per frame (dynamic LDS)
+  int32_t nb_cap;     // k_detect: Schmidl-Cox moment blocks per frame (dynamic LDS)
+  int32_t fine_cap;   // k_detect: fine-search positions (dynamic LDS), >= 12 CP + 1
+  int32_t mcap;       // data symbols a frame of fast_len samples can hold (k_demod stream LDS)
+  int32_t stream_words; // k_demod: LDS words per wave (bit stream, then the voted stream)
+  int32_t vote_off;   // k_demod: word offset of the voted stream
+  int64_t fast_len;   // frames longer than this go to the exact kernel (AMOD_FLAG_BIG)
+  DetRec *det;        // [nframes] detection records
   float *soft;        // exact kernel, AMOD_OPT_SOFT_COMBINE: per-slot soft bit values
   int64_t soft_stride;// floats per slot
 };
@@ -402,10 +424,13 @@ __device__ inline void init_result(amod_result &r) {
 
 // kernels (defined in k_decode_fast.hip / k_decode_exact.hip)
 extern "C" {
-hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s);
+hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s); // k_detect / k_chunk_prep
+hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s);
+int amod_demod_blocks_per_cu(int mod, int lds);
+void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_words, int *vote_off);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
-int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap); // dynamic LDS of one fast-kernel workgroup
+int amod_fast_lds_bytes(int nb_cap, int fine_cap); // dynamic LDS of one k_detect workgroup
 // streaming receiver pieces (k_stream.hip)
 hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, float *y, double *warm, double *end,
                            unsigned long long *fixed, hipStream_t s);

@@ -1,27 +1,27 @@
-// k_decode_fast.hip — streaming fast path of the OFDM receive chain (gfx950).
+// k_decode_fast.hip — fast path of the OFDM receive chain (gfx950).
 //
-// One 256-thread workgroup (4 waves) per frame, <= 26 KB of LDS and 80 registers on
-// C2-sized frames, so six frames are in flight per CU: while one workgroup streams its
-// frame from HBM, the others compute. The frame is never held in LDS; it is read from HBM once, coalesced,
-// and the few samples later stages need again come back from L2 / Infinity Cache.
+// Two launches per batch, each shaped for what it does (one HBM pass over the samples,
+// then short compute jobs over the few samples the demodulator needs):
 //
-//   stage 0  stream pass        preprocessSignal (modem.js:213-232) statistics and,
-//                               in the same pass, 32-sample block moments of
-//                               u = x - x[0] (sum u, sum u^2, sum u[k] u[k+256]);
-//                               normalised Schmidl-Cox block sums follow exactly
-//                               from them once mean and peak are known
-//   stage 1  Schmidl-Cox        detectPreamble (286-319): window sums at block
-//                               starts, rigorous per-block caps, candidate blocks
-//                               slid position by position (32-lane prefix scans)
-//   stage 2  fine timing        inline xcorr (567-588) over the plateau +- 3 CP
-//   stage 3  FFT jobs           estimateChannel (421-440) + demodulateOFDM (365-418):
-//                               one wave per pair of real symbols packed into one
-//                               512-pt complex FFT (radix-8 x 3, swizzled LDS
-//                               exchanges). Only the symbols that hold the bytes the
-//                               parse reads (header .. CRC) are demodulated: the
-//                               first round decodes the CE and 7 symbols, the
-//                               header then says how many more are needed.
-//   stage 4  finish             majorityVote / bitsToBytes / parse / CRC-32 (shared)
+//   k_detect   one 256-thread workgroup per frame (decodeReceivedSignal frames only):
+//              stage 0  stream pass   preprocessSignal (modem.js:213-232) statistics and,
+//                                     in the same pass, 32-sample block moments of
+//                                     u = x - x[0] (sum u, sum u^2, sum u[k] u[k+256]);
+//                                     normalised Schmidl-Cox block sums follow exactly
+//                                     from them once mean and peak are known
+//              stage 1  Schmidl-Cox   detectPreamble (286-319): window sums at block
+//                                     starts, rigorous per-block caps, candidate blocks
+//                                     slid position by position (32-lane prefix scans)
+//              stage 2  fine timing   inline xcorr (567-588) over the plateau +- 3 CP,
+//                                     VALU + DPP, folded on pre1's 256-sample period
+//              -> per-frame detection record (start, normalisation, symbols to decode)
+//   k_chunk_prep  the same record for decodeChunkFrame windows (modem.js:770-786)
+//   k_demod    persistent waves, one frame at a time per wave: CE + data symbols as FFT
+//              jobs (two real symbols per complex 512-pt FFT, radix-8 x 3, swizzled LDS
+//              exchanges), estimateChannel (421-440), equalise + pilot phase + demap
+//              (demodulateOFDM 365-418) into the frame's bit stream in LDS, then
+//              majorityVote / bitsToBytes / parse / CRC-32 and the stores; the next
+//              job's samples are in flight while the current one computes
 //
 // Arithmetic is fp32. Every discrete decision carries a guard band sized from an
 // error bound; a frame with a decision inside its band is listed
@@ -37,16 +37,12 @@ constexpr int WG = 256;                      // 4 waves
 constexpr int NWAVE = WG / 64;
 constexpr int BLK = 32;                      // Schmidl-Cox block length
 constexpr float ACTIVE_EB = 0.05f;           // normalised 32-sample block energy of "signal" (rms ~0.04 of peak)
-#ifndef AMOD_FINE_MAX
-#define AMOD_FINE_MAX 1024
-#endif
-constexpr int FINE_MAX = AMOD_FINE_MAX;               // max fine-search positions (else exact)
 constexpr int SC_MAXCAND = 256;              // candidate blocks slid per position (else exact)
 constexpr int SC_CACHE = 16;                 // candidate blocks whose per-position results stay in LDS
 #ifndef AMOD_FIRST_SYMS
 #define AMOD_FIRST_SYMS 7
 #endif
-constexpr int FIRST_SYMS = AMOD_FIRST_SYMS;  // data symbols of the first FFT round (+ CE)
+constexpr int FIRST_SYMS = AMOD_FIRST_SYMS;  // data symbols always decoded (the header's)
 #ifndef AMOD_SB
 #define AMOD_SB 8
 #endif
@@ -55,47 +51,29 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #define AMOD_WPE 6                           // waves per SIMD the register budget is sized for
 #endif
 #ifndef AMOD_SCAN_WPE
-#define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone): 96 registers
+#define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone)
+#endif
+#ifndef AMOD_DEMOD_WPE
+#define AMOD_DEMOD_WPE 4                     // k_demod: 109 registers, no spills
 #endif
 
-// Dynamic LDS, sized per launch from the reserved frame length (amod_fast_lds_bytes):
-// one region reused by the stages, addressed by float / float2 / word index.
+// Dynamic LDS of k_detect, sized per launch (amod_fast_lds_bytes): one region reused
+// by the stages, addressed by float / float2 / word index.
 //   stages 0-1: s1[nbc] s2[nbc] sx[nbc] (block moments -> caps / E_b / Z_b), cand[256] (int16),
 //               cmax[256], pass-1 cache[SC_CACHE][32] (float2: top metric, uncertainty bits)
-//   stage 2   : tmpl[768] m[FINE_MAX + 8] yw[FINE_MAX + 800] q[FINE_MAX + 280] (folded window)
-//               E[FINE_MAX + 800] (prefix of squares of yw)
-//   stage 3-4 : xch[4][512] float2 (FFT exchange; decision bytes after each FFT; between
-//               rounds and at finish the packed stream bits[bitc] in its last bitc words and
-//               the voted bits from its start), g[256] float2, twiddles (tw1 rows 1-7, tw2),
-//               rows[rows_cap + 1] (word-aligned bit row per data symbol)
+//   stage 2   : tmpl[768] m[FC + 8] yw[FC + 800] q[FC + 280] (folded window) E[FC + 800]
+//               (prefix of squares of yw); FC = the launch's fine-search capacity
 extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_F (reinterpret_cast<float *>(amod_dyn))
 #define LDS_F2 (reinterpret_cast<float2 *>(amod_dyn))
 #define LDS_U (reinterpret_cast<uint32_t *>(amod_dyn))
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
-#ifndef AMOD_FINE_MFMA
-#define AMOD_FINE_MFMA 1 // folded fine correlation as Toeplitz tiles on the matrix cores
-#endif
-#if AMOD_FINE_MFMA
-// the metrics m overwrite the folded window q once every tile has been read (barrier)
-constexpr int FINE_TM = 0, FINE_YW = 768, FINE_Q = FINE_YW + FINE_MAX + 800, FINE_M = FINE_Q;
-#else
-constexpr int FINE_TM = 0, FINE_M = 768, FINE_YW = 768 + FINE_MAX + 8, FINE_Q = FINE_YW + FINE_MAX + 800;
-#endif
-constexpr int FINE_E = FINE_Q + FINE_MAX + 280; // prefix of squares of the window, span + 1 entries
-// zero-padded template table of the MFMA fine path for n taps: 16 zeros, n taps, zeros
-// up to the last K step (K = n + 15 rounded up to 4)
-__host__ __device__ constexpr int fine_tab_len(int n) { return 16 + 4 * ((n + 15 + 3) >> 2); }
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+__host__ __device__ constexpr int fine_m(int) { return 768; }
+__host__ __device__ constexpr int fine_yw(int fc) { return 768 + fc + 8; }
+__host__ __device__ constexpr int fine_q(int fc) { return fine_yw(fc) + fc + 800; }
+__host__ __device__ constexpr int fine_e(int fc) { return fine_q(fc) + fc + 280; }
+__host__ __device__ constexpr int fine_floats(int fc) { return fine_e(fc) + fc + 800; }
 typedef float f2v __attribute__((ext_vector_type(2)));
-constexpr int FQ_G = NWAVE * 512;             // float2 index of g
-#ifndef AMOD_TW_LDS
-#define AMOD_TW_LDS 1                        // FFT twiddles staged in LDS
-#endif
-constexpr int FQ_TW = FQ_G + kMaxBand;        // float2 index of the twiddles (tw1 rows 1-7, tw2[64])
-constexpr int TW_WORDS = AMOD_TW_LDS ? 2 * (7 * 64 + 8 * 8) : 0;
-constexpr int FQ_XCH_WORDS = 2 * NWAVE * 512; // words of the exchange buffers
-constexpr int FQ_ROWS = 2 * (FQ_G + kMaxBand) + TW_WORDS; // word index of the symbol rows
 
 struct Smem {  // fixed part (static LDS)
   float rf[4 * NWAVE];
@@ -103,8 +81,8 @@ struct Smem {  // fixed part (static LDS)
   double rd[2 * NWAVE];
   uint32_t ru[16];
   // per-frame scalars (written by one thread, read after a barrier)
-  int status, flags, coarse, clo, chi, start, ncand, target, last_blk;
-  float A, B, Bu, errw, cbest, cblo, cbhi, fbest, gmax, zce;
+  int status, flags, coarse, clo, chi, start, ncand, last_blk;
+  float A, B, Bu, errw, cbest, cblo, cbhi, fbest;
   double mean, mx;
 };
 
@@ -143,10 +121,10 @@ __device__ __forceinline__ int swz2(int q, int l1, int p1) {
 __device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2); }
 
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); X[n] is
-// left in the wave's exchange buffer (float2 index xb) at spec_idx(n).
-__device__ void fft512_wave(float2 (&v)[8], const int xb, const float2 *__restrict__ tw1,
+// left in the wave's 512-entry LDS exchange buffer X2 at spec_idx(n).
+// tw1: rows 1-7 of e^{-2 pi i l q / 512} (row q at tw1[64 q]); tw2: [8][8] pass-2 twiddles
+__device__ void fft512_wave(float2 (&v)[8], float2 *const X2, const float2 *__restrict__ tw1,
                             const float2 *__restrict__ tw2) {
-  float2 *const X2 = LDS_F2;
   int l = wave_lane();
   asm volatile("" : "+v"(l)); // keep lane-derived swizzles inside the job loop
   dft8(v);
@@ -154,10 +132,10 @@ __device__ void fft512_wave(float2 (&v)[8], const int xb, const float2 *__restri
   for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], tw1[q * 64 + l]);
   // exchange 1: row q, col l ^ (q<<3)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) X2[xb + q * 64 + (l ^ (q << 3))] = v[q];
+  for (int q = 0; q < 8; ++q) X2[q * 64 + (l ^ (q << 3))] = v[q];
   __builtin_amdgcn_wave_barrier();
   const int l1 = l & 7, q2 = l >> 3; // pass-2 lane = (l1, q)
-  const int r2 = xb + q2 * 64;
+  const int r2 = q2 * 64;
 #pragma unroll
   for (int l2 = 0; l2 < 8; ++l2) v[l2] = X2[r2 + l1 + 8 * (l2 ^ q2)];
   dft8(v);
@@ -174,10 +152,10 @@ __device__ void fft512_wave(float2 (&v)[8], const int xb, const float2 *__restri
   dft8(v); // v[p2] = X[q2 + 8 p1 + 64 p2]
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int p2 = 0; p2 < 8; ++p2) X2[xb + spec_idx(q2 + 8 * p1 + 64 * p2)] = v[p2];
+  for (int p2 = 0; p2 < 8; ++p2) X2[spec_idx(q2 + 8 * p1 + 64 * p2)] = v[p2];
   __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ float2 spec_read(const int xb, int n) { return LDS_F2[xb + spec_idx(n & 511)]; }
+__device__ __forceinline__ float2 spec_read(const float2 *X2, int n) { return X2[spec_idx(n & 511)]; }
 
 // Symbol rows (one word-aligned row of wsym words per data symbol, MSB-first) ->
 // the frame's contiguous MSB-first bit stream (bitsToBytes order, modem.js:468-476):
@@ -204,7 +182,6 @@ __device__ void repack_rows(const uint32_t *rows, int wsym, int per_sym, int nsy
     out[W] = acc;
   }
 }
-
 // Constellation decision (modem.js:140-150) and its distance to the nearest
 // decision boundary. Ties resolve to the lowest index like the reference loop.
 __device__ __forceinline__ int decide(int mod, float cr, float ci, float &margin) {
@@ -294,6 +271,18 @@ __device__ __forceinline__ float wmax_b(float v) {
   return rlane(v, 63);
 }
 
+// max over the wave of non-negative floats (or NaN): their bit patterns order like the
+// values, so the reduction runs on integers (v_max_i32 with DPP fused, no NaN
+// canonicalisation steps); a wave-uniform result via one readlane. Whole wave active.
+__device__ __forceinline__ float wmax_nn(float x) {
+  int v = __float_as_int(x);
+  v = max(v, AMOD_DPP_I(v, 0xB1)); v = max(v, AMOD_DPP_I(v, 0x4E));
+  v = max(v, AMOD_DPP_I(v, 0x141)); v = max(v, AMOD_DPP_I(v, 0x140));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_readlane(v, 63));
+}
+
 // inclusive prefix sum inside each aligned 32-lane group: row_shr 1/2/4/8 inside rows of
 // 16, then row_bcast:15 carries row 0 (2) into row 1 (3). The group's lanes all active.
 __device__ __forceinline__ float scan32(float v) {
@@ -325,11 +314,34 @@ __device__ __forceinline__ float dpp_sum8(float v) {
   return v;
 }
 
+// Why a frame skips the fast path (0: it does not). Depends on the frame, the options and
+// the launch's fast-path length only (never on other frames of the batch).
 __device__ __forceinline__ int frame_route(const DevCfg &cfg, const DevWork &w, int N) {
   if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
   if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) return AMOD_FLAG_FORCED; // opt-in soft vote
-  if (8 * ((N + 3 + 255) >> 8) > w.nb_cap) return AMOD_FLAG_BIG; // moment arrays of this launch
+  if ((int64_t)N > w.fast_len) return AMOD_FLAG_BIG; // longer than the launch's fast-path workspace
   return 0;
+}
+
+// append frame f to k_decode_exact's list (one thread)
+__device__ __forceinline__ void list_exact(const DevWork &w, int f, int flags) {
+  const int i = atomicAdd(w.fb_count, 1);
+  w.fb_list[i] = f;
+  w.fb_flags[i] = flags;
+  if (w.det) w.det[f].route = ROUTE_EXACT;
+}
+
+// scalar (SMEM) load of a wave-uniform record: waits on lgkmcnt, not behind vector loads
+template <typename T> __device__ __forceinline__ T sload(const T *p) {
+  static_assert(sizeof(T) % 4 == 0, "whole dwords");
+  typedef const __attribute__((address_space(4))) uint32_t *cptr;
+  const cptr q = reinterpret_cast<cptr>(reinterpret_cast<uintptr_t>(p));
+  uint32_t v[sizeof(T) / 4];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) v[i] = q[i];
+  T out;
+  __builtin_memcpy(&out, v, sizeof(T));
+  return out;
 }
 
 // chunk q of the frame in k-space (k = i + ph; 64 float4 = 256 samples); lanes
@@ -376,12 +388,11 @@ __device__ __forceinline__ const KArgs &kargs() {
 // SCAN_ONLY: the same code stopped after the Schmidl-Cox decision (k_corr_scan, the
 // correlation-scan phase measured on its own; nothing is written).
 // DBG: parity-test build that also records intermediates (amod_decode_device_debug);
-// the production instantiation carries none of that code.
-template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast() {
+template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
   __shared__ Smem sm;
   FRESH_ARGS;
-  const int nbc = w.nb_cap, bitc = w.bits_cap; // dynamic LDS capacities of this launch
-  const int f = blockIdx.x;
+  const int nbc = w.nb_cap; // dynamic LDS capacity of this launch
+  const int f = w.f0 + (int)blockIdx.x; // frames [f0, f1) of this launch
   const int tid = ltid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform (SGPR)
   // frame geometry in SGPRs: every branch and loop bound below is wave-uniform
@@ -399,11 +410,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
   {
     const int route = frame_route(cfg, w, N);
     if (route) {
-      if (tid == 0) {
-        const int i = atomicAdd(w.fb_count, 1);
-        w.fb_list[i] = f;
-        w.fb_flags[i] = route;
-      }
+      if (tid == 0) list_exact(w, f, route);
       return;
     }
   }
@@ -421,7 +428,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
   __syncthreads();
   if (sm.status != AMOD_OK) goto finish_error;
 
-  if (cfg.mode == AMOD_MODE_RECEIVED) {
+  {
     // ------------------------------------------------ stage 0: stream pass
     const int nch = (K + 255) >> 8;
     const int NB = (K + BLK - 1) / BLK;
@@ -842,12 +849,15 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     // ---------------------------------------------- stage 2: fine timing
     {
       FRESH_ARGS;
+      const int FC = w.fine_cap; // positions the launch's LDS holds (>= 12 CP + 1: every window the
+                                 // coarse stage lets through)
+      const int FM = fine_m(FC), FYW = fine_yw(FC), FQ = fine_q(FC), FE = fine_e(FC);
       const float A = sm.A, B = sm.B;
       const int R = 3 * CP;
       const int c_lo = sm.clo, c_hi = sm.chi;
       const int w0 = max(0, c_lo - R), w1 = min(N - SYM, c_hi + R);
       const int P = w1 - w0 + 1;
-      if (P > FINE_MAX) {
+      if (P > FC) {
         if (tid == 0) sm.flags |= AMOD_FLAG_FINE;
         __syncthreads();
         goto to_exact;
@@ -857,105 +867,87 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         __syncthreads();
         goto finish_error;
       }
-      // template + the normalised search window, staged once in LDS. All loads of a
-      // thread are issued before its first store (one memory latency, not one per
-      // loop trip): raw buffer loads past the frame end return 0 without a branch.
+      // template + the normalised search window, staged once in LDS; a thread issues a
+      // batch of loads before its first store (one memory latency per batch): raw buffer
+      // loads past the frame end return 0 without a branch
       const int span = P + SYM + 16;
       {
-        constexpr int TR = (768 + WG - 1) / WG, YR = (FINE_MAX + 768 + 16 + WG - 1) / WG;
+        constexpr int TR = (768 + WG - 1) / WG, YB = 8;
         const __amdgpu_buffer_rsrc_t rx =
             __builtin_amdgcn_make_buffer_rsrc((void *)(X + w0), (short)0, 4 * (N - w0), 0x00020000);
         const __amdgpu_buffer_rsrc_t rt =
             __builtin_amdgcn_make_buffer_rsrc((void *)cfg.t.pre1, (short)0, 4 * SYM, 0x00020000);
-        float tv[TR], yv[YR];
-#if AMOD_FINE_MFMA
-        // folded: two zero-padded template tables (the MFMA A operand, fine_mfma)
-        const int la = fine_tab_len(256), lb = fine_tab_len(CP);
-        auto tab_src = [&](int j) { // template index feeding table entry j (-1: zero)
-          const int i = j < la ? j - 16 : j - la - 16, n = j < la ? 256 : CP;
-          return (i >= 0 && i < n && j < la + lb) ? i : -1;
-        };
-#endif
+        float tv[TR];
 #pragma unroll
-        for (int r = 0; r < TR; ++r) {
-          int src = tid + r * WG;
-#if AMOD_FINE_MFMA
-          if (cfg.fold) src = tab_src(src);
-#endif
-          tv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, 4 * src, 0, 0)); // src < 0: 0
-        }
+        for (int r = 0; r < TR; ++r)
+          tv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rt, 4 * (tid + r * WG), 0, 0));
+        for (int j0 = 0; j0 < span; j0 += YB * WG) {
+          float yv[YB];
 #pragma unroll
-        for (int r = 0; r < YR; ++r)
-          yv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, 4 * (tid + r * WG), 0, 0));
+          for (int r = 0; r < YB; ++r)
+            yv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, 4 * (j0 + tid + r * WG), 0, 0));
+          if (j0 == 0) {
 #pragma unroll
-        for (int r = 0; r < TR; ++r) {
-          const int j = tid + r * WG;
-#if AMOD_FINE_MFMA
-          if (cfg.fold) { if (j < la + lb) LDS_F[FINE_TM + j] = tab_src(j) >= 0 ? tv[r] : 0.f; }
-          else
-#endif
-          if (j < SYM) LDS_F[FINE_TM + j] = tv[r];
-        }
+            for (int r = 0; r < TR; ++r)
+              if (tid + r * WG < SYM) LDS_F[tid + r * WG] = tv[r];
+          }
 #pragma unroll
-        for (int r = 0; r < YR; ++r) {
-          const int j = tid + r * WG;
-#if AMOD_FINE_MFMA
-          // the tiles read past the window: zeros (finite) up to the region's end
-          if (j < FINE_MAX + 800) LDS_F[FINE_YW + j] = (j < span && w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
-#else
-          if (j < span) LDS_F[FINE_YW + j] = (w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
-#endif
+          for (int r = 0; r < YB; ++r) {
+            const int j = j0 + tid + r * WG;
+            if (j < span) LDS_F[FYW + j] = (w0 + j < N) ? fmaf(yv[r], A, B) : 0.f;
+          }
         }
       }
       __syncthreads();
       const float te = cfg.te_f;
       const int noct = (P + 7) >> 3;
-      const float *yw = LDS_F + FINE_YW;
-      const float *tm = LDS_F + FINE_TM;
+      const float *yw = LDS_F + FYW;
+      const float *tm = LDS_F;
+      const float *qw = LDS_F + FQ;
       const int fold = cfg.fold;
       if (fold) {
         // corr(d) = sum_{i<256} t[i] (y[d+i] + fold y[d+i+256]) + sum_{i<CP} t[i] y[d+i+512]
         // (t[i+256] = fold t[i]): 256 + CP taps instead of SYM
-#if AMOD_FINE_MFMA
-        const int qn = 256 * ((P + 255) >> 8) + 256; // everything the tiles read
-#else
         const int qn = 8 * noct + 264;
-#endif
-        for (int j = tid; j < qn; j += WG) LDS_F[FINE_Q + j] = fmaf((float)fold, yw[j + 256], yw[j]);
+        for (int j = tid; j < qn; j += WG) LDS_F[FQ + j] = fmaf((float)fold, yw[j + 256], yw[j]);
       }
-      // window energies from a prefix of squares: E[j] = sum_{i<j} y[i]^2, en(d) = E[d+SYM] - E[d].
-      // Each E[j] carries <= ~26 roundings of partial sums <= E[span]: |err en| <= en_err.
+      // window energies from a prefix of squares: E[j] = sum_{i<j} y[i]^2, en(d) = E[d+SYM] - E[d],
+      // built 2048 entries at a time with a carried base. Each E[j] carries <= ~40 roundings of
+      // partial sums <= E[span]: |err en| <= en_err.
       float en_err;
       {
-        float sq[8], s = 0.f;
-        const int b0 = 8 * tid;
+        float carry = 0.f;
+        for (int base = 0; base <= span; base += 8 * WG) {
+          float sq[8], s = 0.f;
+          const int b0 = base + 8 * tid;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float v = b0 + k < span ? yw[b0 + k] : 0.f;
-          sq[k] = v * v;
-          s += sq[k];
-        }
-        const float inc = scan64(s);
-        if (lane == 63) sm.rf[wave] = inc;
-        __syncthreads();
-        float run = -s + inc, tot = 0.f;
-        for (int i = 0; i < NWAVE; ++i) {
-          const float wv = sm.rf[i];
-          if (i < wave) run += wv;
-          tot += wv;
-        }
+          for (int k = 0; k < 8; ++k) {
+            const float v = b0 + k < span ? yw[b0 + k] : 0.f;
+            sq[k] = v * v;
+            s += sq[k];
+          }
+          const float inc = scan64(s);
+          if (lane == 63) sm.rf[wave] = inc;
+          __syncthreads();
+          float run = carry - s + inc, tot = 0.f;
+          for (int i = 0; i < NWAVE; ++i) {
+            const float wv = sm.rf[i];
+            if (i < wave) run += wv;
+            tot += wv;
+          }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (b0 + k <= span) LDS_F[FINE_E + b0 + k] = run;
-          run += sq[k];
+          for (int k = 0; k < 8; ++k) {
+            if (b0 + k <= span) LDS_F[FE + b0 + k] = run;
+            run += sq[k];
+          }
+          carry += tot;
+          __syncthreads(); // sm.rf is reused by the next chunk
         }
-        en_err = 4e-6f * tot + 1e-30f;
+        en_err = 6e-6f * carry + 1e-30f;
       }
-      __syncthreads();
-      const float *qw = LDS_F + FINE_Q;
       // metric of window position d from its correlation cj; energies from the prefix E
       auto fine_metric = [&](int d, float cj) {
-        float en = LDS_F[FINE_E + d + SYM] - LDS_F[FINE_E + d];
+        float en = LDS_F[FE + d + SYM] - LDS_F[FE + d];
         if (en < 1e4f * en_err) { // low-energy window: the difference is not accurate enough
           en = 0.f;
           for (int i = 0; i < SYM; ++i) en = fmaf(yw[d + i], yw[d + i], en);
@@ -967,61 +959,8 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
         if (et > g_hi * g_hi) m = cj * rsq_a(et);
         else if (et > g_lo * g_lo) m = cj * rsq_a(et) + 4.f; // uncertain gate: tagged
         else m = -8.f;                                      // gated out
-        LDS_F[FINE_M + d] = m;
+        LDS_F[FM + d] = m;
       };
-#if AMOD_FINE_MFMA
-      if (fold) {
-        // Toeplitz tiles of 256 positions on the matrix cores (v_mfma_f32_16x16x4_f32,
-        // f32 in, f32 accumulate), one tile per wave:
-        //   C[r][n] = corr(256 t + 16 n + r) = sum_k T[r][k] Y[k][n],
-        //   T[r][k] = tpad[16 + k - r]   (zero-padded template table),
-        //   Y[k][n] = q[256 t + 16 n + k] (folded window), then the CP tail taps on y at
-        //   offset 512 with their own table; K in steps of 4.
-        // Lane l supplies A = T[l % 16][4 s + l / 16] and B = Y[4 s + l / 16][l % 16] (one
-        // LDS word each, immediate offsets) and receives C[4 (l / 16) + i][l % 16], i < 4:
-        // four consecutive positions. Two accumulators alternate to halve the chain.
-        const int la = fine_tab_len(256);
-        const int r16 = lane & 15, kk = lane >> 4;
-        const int ntile = (P + 255) >> 8;
-        const int sb = (CP + 15 + 3) >> 2;
-        static_assert(FINE_MAX <= 256 * NWAVE, "one tile per wave");
-        const int t = wave;
-        floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-        if (t < ntile) {
-          const float *ta = LDS_F + FINE_TM + 16 + kk - r16;
-          const float *tb = ta + la;
-          const float *ya = LDS_F + FINE_Q + 256 * t + 16 * r16 + kk;
-          const float *yb = LDS_F + FINE_YW + 512 + 256 * t + 16 * r16 + kk;
-          // operands of the next step pair are requested before this pair's MFMAs issue
-          // (the LDS latency hides under the matrix pipe instead of stalling each pair)
-          float a0 = ta[0], y0 = ya[0], a1 = ta[4], y1 = ya[4];
-#pragma unroll
-          for (int st = 0; st < 68; st += 2) {
-            float na0 = 0.f, ny0 = 0.f, na1 = 0.f, ny1 = 0.f;
-            if (st + 2 < 68) { na0 = ta[4 * st + 8]; ny0 = ya[4 * st + 8]; na1 = ta[4 * st + 12]; ny1 = ya[4 * st + 12]; }
-            __builtin_amdgcn_sched_barrier(0);
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, y0, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, y1, c1, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            a0 = na0; y0 = ny0; a1 = na1; y1 = ny1;
-          }
-          int st = 0;
-          for (; st + 1 < sb; st += 2) {
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st], yb[4 * st], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st + 4], yb[4 * st + 4], c1, 0, 0, 0);
-          }
-          if (st < sb) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[4 * st], yb[4 * st], c0, 0, 0, 0);
-        }
-        __syncthreads(); // every tile has read q: the metrics may overwrite it
-        if (t < ntile) {
-          const int d0 = 256 * t + 16 * r16 + 4 * kk;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (d0 + i < P) fine_metric(d0 + i, c0[i] + c1[i]);
-        }
-      } else
-#endif
-      {
       // lane = (octet of 8 positions, one of 8 tap ranges): per tap one window read,
       // one template read, 8 correlations. The 8 ranges of an octet are 8 aligned
       // lanes, combined by DPP; energies come from the prefix E.
@@ -1071,7 +1010,6 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
           fine_metric(j0 + sp, cj);
         }
       }
-      }
       __syncthreads();
       // argmax (first index), second best and the best uncertain-gate candidate in one
       // pass: per lane its best (first index), the best of its other positions and its
@@ -1081,7 +1019,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
       float b1 = -8.f, b2 = -8.f, mt = -INFINITY;
       int i1x = 0x7fffffff;
       for (int k = tid; k < P; k += WG) {
-        float m = LDS_F[FINE_M + k];
+        float m = LDS_F[FM + k];
         const bool tagged = m > 2.f;
         if (tagged) { m -= 4.f; mt = fmaxf(mt, m); }
         if (m > b1) { b2 = b1; b1 = m; i1x = k; }
@@ -1132,424 +1070,614 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void decode_fast(
     // CE / data checks (modem.js:591-600)
     if (start + 3 * SYM > N) { if (tid == 0) sm.status = AMOD_E_SHORT_CE; __syncthreads(); goto finish_error; }
     if (start + 3 * SYM >= N) { if (tid == 0) sm.status = AMOD_E_NO_DATA; __syncthreads(); goto finish_error; }
-  } else {
-    // decodeChunkFrame (modem.js:774-786): no preprocessing, the frame starts at pre1
-    if (3 * SYM > N) { if (tid == 0) sm.status = AMOD_E_FRAME_SHORT_CE; __syncthreads(); goto finish_error; }
-    if (3 * SYM >= N) { if (tid == 0) sm.status = AMOD_E_NO_DATA; __syncthreads(); goto finish_error; }
   }
 
-  // ------------------------------------------------ stage 3: FFT jobs
-  {
-    FRESH_ARGS;
-    const float A = sm.A, B = sm.B;
-    const int ce0 = start + 2 * SYM, data0 = start + 3 * SYM;
-    const int M = (N - data0) / SYM;           // whole data symbols (demodulateOFDM numSym)
-    const int per_sym = cfg.ndata * cfg.bps;
-    const int nbits = M * per_sym;
-    const int nbytes_total = (nbits / cfg.rep) >> 3;
-    const int nband = cfg.nband;
-    const int wsym = (per_sym + 31) >> 5;      // words per symbol row
-    const int fq_sa = FQ_ROWS;                 // word index of the symbol rows
-    // the packed stream lives in the exchange buffers (dead between rounds and at finish;
-    // rebuilt from the rows after every round); bitc <= 2048 words, so it never reaches
-    // the voted bits written from the start of the region
-    uint32_t *const fq_bits = LDS_U + FQ_XCH_WORDS - bitc;
-    // Jobs are numbered over the whole frame: job 0 = (CE, symbol 0), job j = (2j-1, 2j);
-    // wave w owns jobs w, w+4, ... and prefetches its next job's samples while it
-    // transforms and demaps the current one (across the round boundary too: the
-    // first-round prefetch is speculative and simply dropped if unused).
-    auto jobs_for = [](int T) { return T == 0 ? 1 : 1 + T / 2; };
-    auto job_syms = [&](int j, int T, int &s1, int &s2) {
-      if (j == 0) { s1 = -2; s2 = T > 0 ? 0 : -1; }
-      else { s1 = 2 * j - 1; s2 = 2 * j < T ? 2 * j : -1; }
-    };
-    float pf1[8], pf2[8];
-    int pf_job = -1;
-    auto load_job = [&](int j, int T, float (&r1)[8], float (&r2)[8]) {
-      int a, b;
-      job_syms(j, T, a, b);
-      const int p1 = a == -2 ? ce0 : data0 + a * SYM, p2 = b >= 0 ? data0 + b * SYM : p1;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        r1[m] = X[p1 + CP + lane + 64 * m];
-        r2[m] = X[p2 + CP + lane + 64 * m];
-      }
-    };
-    // this wave's first-round job (job `wave`: its symbols are the same for the round-1
-    // target and for M) is requested before the tables, so its latency overlaps them
-    if (wave == 0 || 2 * wave - 1 < M) { load_job(wave, M, pf1, pf2); pf_job = wave; }
-    // tables: every load issued before the first LDS store
-    {
-      const float2 t1a = cfg.t.tw1[64 + tid], t1b = cfg.t.tw1[64 + min(tid + WG, 447)], t2 = cfg.t.tw2[tid & 63];
-      const float kn = cfg.t.known[min(tid, nband - 1)];
-      if (AMOD_TW_LDS) {
-        LDS_F2[FQ_TW + tid] = t1a; // tw1 row q at FQ_TW + 64 (q - 1): row 0 is never read
-        if (tid + WG < 7 * 64) LDS_F2[FQ_TW + WG + tid] = t1b;
-        if (tid < 64) LDS_F2[FQ_TW + 7 * 64 + tid] = t2;
-      }
-      // the CE signs ride in the G slots until the CE job overwrites them with G
-      if (tid < nband) LDS_F[2 * (FQ_G + tid)] = kn;
-    }
-    // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
-    int di_l[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) di_l[rr] = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
-    // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
-    // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
-    int prr = -1, npl = 0;
-#pragma unroll
-    for (int rr = 3; rr >= 0; --rr)
-      if (di_l[rr] == -1) { prr = rr; ++npl; }
-    const bool pil_multi = __ballot(npl > 1) != 0;
-    if (tid == 0) {
-      sm.gmax = 0.f; sm.zce = 0.f;
-      int t = min(M, FIRST_SYMS);
-      if (t * per_sym > bitc * 32 || t * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
-      // the first round also covers every symbol up to the end of the frame's signal
-      // energy (the trailing silence is skipped as before): a transmitted frame's data
-      // then decodes in one round. Rounds stay header-driven, so this only sets the
-      // round size, never what the result holds.
+  // the detection record the demodulation launches read
+  if (tid == 0) {
+    const int data0 = start + 3 * SYM;
+    const int M = (N - data0) / SYM; // whole data symbols (demodulateOFDM numSym)
+    int T = M;
+    // symbols up to the end of the frame's signal energy (the trailing silence is not
+    // demodulated; k_finish sends a frame whose parse reads past them to the exact path)
+    if (!dbg && sm.last_blk >= 0) {
       const int act_end = BLK * (sm.last_blk + 1) - ph; // first sample after the last active block
-      const int tact = ((act_end - data0 + SYM - 1) / SYM) | 1;  // whole jobs
-      const int tcap = min(bitc * 32 / per_sym, w.rows_cap / wsym);
-      if (sm.last_blk >= 0) t = max(t, min(min(M, tact), tcap));
-      sm.target = dbg ? M : t;
+      const int tact = (act_end - data0 + SYM - 1) / SYM;
+      T = min(M, max(min(M, FIRST_SYMS), tact));
     }
-    __syncthreads();
-    if (sm.flags) goto to_exact;
-    STAMP(7);
-    int done = 0;                  // data symbols decoded so far (a prefix)
-    int need_bytes = 0;
-    int wflags = 0;
-    int jdone = 0;                // jobs completed in earlier rounds
-    for (;;) {
-      FRESH_ARGS;
-      const int target = sm.target;
-      const bool first = done == 0;
-      const int jend = jobs_for(target);
-      // round: jobs [jdone, jend); the first round is exactly one job per wave
-      for (int j = jdone + ((wave - jdone) & (NWAVE - 1)), r = 0; (first && r == 0) || j < jend; j += NWAVE, ++r) {
-        const bool active = j < jend;
-        int s1 = -1, s2 = -1;      // data-symbol indices; s1 = -2 marks the CE symbol
-        if (active) job_syms(j, target, s1, s2);
-        const int xb = wave * 512;
-        float2 v[8];
-        int const1 = 0, const2 = 0;
-        if (active) {
-          float r1[8], r2[8];
-          if (pf_job == j) {
-#pragma unroll
-            for (int m = 0; m < 8; ++m) { r1[m] = pf1[m]; r2[m] = pf2[m]; }
-          } else {
-            load_job(j, target, r1, r2);
-          }
-          // next job of this wave: inside this round, or speculatively the next round's
-          const int jn = j + NWAVE;
-          if (jn < jend || (first && 2 * jn - 1 < M)) { load_job(jn, M, pf1, pf2); pf_job = jn; }
-          else pf_job = -1;
-          // a window is constant iff every raw sample equals its first one
-          const float f1 = rlane(r1[0], 0), f2 = rlane(r2[0], 0);
-          int ne1 = 0, ne2 = 0, nf = 0;
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            ne1 |= r1[m] != f1;
-            ne2 |= r2[m] != f2;
-            if (cfg.mode == AMOD_MODE_CHUNK) nf |= !isfinite(r1[m]) || !isfinite(r2[m]); // received: stage 0 saw them
-            v[m] = make_float2(fmaf(r1[m], A, B), s2 >= 0 ? fmaf(r2[m], A, B) : 0.f);
-          }
-          const1 = __ballot(ne1) == 0;
-          const2 = __ballot(ne2) == 0;
-          if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
-          if (r == 0) STAMP(first ? 8 : 16);
-          if (AMOD_TW_LDS) fft512_wave(v, xb, LDS_F2 + FQ_TW - 64, LDS_F2 + FQ_TW + 7 * 64);
-          else fft512_wave(v, xb, cfg.t.tw1, cfg.t.tw2);
-          if (r == 0) STAMP(first ? 9 : 17);
-          if (j == 0) {
-            // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
-            float zmax = 0.f, gmax_local = 0.f;
-            for (int b = lane; b < nband; b += 64) {
-              const int k = cfg.sub_start + b;
-              const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
-              zmax = fmaxf(zmax, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
-            }
-            zmax = wmax(zmax);
-            for (int b = lane; b < nband; b += 64) {
-              const int k = cfg.sub_start + b;
-              float2 h = make_float2(0.f, 0.f);
-              if (!const1) {
-                const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
-                const float2 y = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-                const float kn = LDS_F[2 * (FQ_G + b)]; // staged CE sign (overwritten with G below)
-                h = make_float2(y.x * kn, y.y * kn);
-              }
-              const float m2 = h.x * h.x + h.y * h.y;
-              float2 g;
-              if (m2 > 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the 2e-6 eq bound
-              else g = make_float2(1.f, 0.f);
-              // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
-              if (!const1 && m2 < 1e-6f) wflags |= AMOD_FLAG_CHANNEL;
-              LDS_F2[FQ_G + b] = g;
-              gmax_local = fmaxf(gmax_local, fabsf(g.x) + fabsf(g.y));
-              if (dbg) { D->h_re[b] = h.x; D->h_im[b] = h.y; }
-            }
-            gmax_local = wmax(gmax_local);
-            if (lane == 0) { sm.zce = zmax; sm.gmax = gmax_local; }
-          }
-        }
-        if (first && r == 0) __syncthreads(); // publish G, |G|max and the CE spectrum scale (every wave passes r = 0)
-        if (first && r == 0) STAMP(10);
-        if (!active) continue;
-        const float gmax = sm.gmax, zce = sm.zce;
-        // ---- both data symbols of this job in one pass: equalise, pilot phase, demap
-        {
-          int ln = lane;
-          asm volatile("" : "+v"(ln)); // per-round lane (keeps debug/bit addresses out of registers)
-          const bool live1 = s1 >= 0 && !const1, live2 = s2 >= 0 && !const2;
-          float2 e1[4], e2[4];
-          float zm = 0.f, em1 = 0.f, em2 = 0.f;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int b = ln + 64 * rr;
-            e1[rr] = e2[rr] = make_float2(0.f, 0.f);
-            if (b < nband) {
-              const int k = cfg.sub_start + b;
-              const float2 zk = spec_read(xb, k), zn = spec_read(xb, kFft - k);
-              zm = fmaxf(zm, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
-              // Z = x1 + i x2:  X1 = (Z[k] + conj Z[-k]) / 2,  X2 = (Z[k] - conj Z[-k]) / 2i
-              const float2 x1 = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-              const float2 x2 = make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
-              const float2 g = LDS_F2[FQ_G + b];
-              e1[rr] = cmul(x1, g);
-              e2[rr] = cmul(x2, g);
-              em1 = fmaxf(em1, fabsf(e1[rr].x) + fabsf(e1[rr].y));
-              em2 = fmaxf(em2, fabsf(e2[rr].x) + fabsf(e2[rr].y));
-              if (dbg && (s1 == 0 || s2 == 0)) {
-                const bool one = s1 == 0;
-                const float2 xx = one ? x1 : x2, ee = one ? e1[rr] : e2[rr];
-                const bool c = one ? const1 : const2;
-                D->x_re[b] = c ? 0.f : xx.x; D->x_im[b] = c ? 0.f : xx.y;
-                D->eq_re[b] = c ? 0.f : ee.x; D->eq_im[b] = c ? 0.f : ee.y;
-              }
-            }
-          }
-          // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
-          const float gsc = 2e-6f * cfg.guard * gmax;
-          float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
-          d1 = wmax_b(d1); d2 = wmax_b(d2);
-          d1 += 1e-12f; d2 += 1e-12f;
-          // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
-          float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
-          int pflag = 0;
-          auto pilot = [&](bool pil, float2 q1e, float2 q2e) {
-            const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
-            // 0/1 weights in VGPRs (no lane masks kept live)
-            const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
-            // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below
-            // signed 1/eqRe, finite for every lane (weight 0 where the reference skips)
-            const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), q1e.x));
-            const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), q2e.x));
-            const float r1 = fabsf(q1), r2 = fabsf(q2);
-            ps1 = fmaf(w1 * q1, q1e.y, ps1);
-            ps2 = fmaf(w2 * q2, q2e.y, ps2);
-            pe1 = fmaf(w1 * r1, fmaf(fabsf(q1e.y), r1, 1.f), pe1);
-            pe2 = fmaf(w2 * r2, fmaf(fabsf(q2e.y), r2, 1.f), pe2);
-            pc1 += w1;
-            pc2 += w2;
-            pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
-          };
-          if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
-            float2 p1 = e1[0], p2 = e2[0];
-#pragma unroll
-            for (int rr = 1; rr < 4; ++rr) {
-              p1 = prr == rr ? e1[rr] : p1;
-              p2 = prr == rr ? e2[rr] : p2;
-            }
-            pilot(prr >= 0, p1, p2);
-          } else {
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) pilot(di_l[rr] == -1, e1[rr], e2[rr]);
-          }
-          ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); pc1 = wsum_b(pc1); pc2 = wsum_b(pc2);
-          if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
-          const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
-          const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
-          const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
-          const float dp1 = d1 * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d2 * pe2 * ip2 + 1e-6f * fabsf(ph2);
-          const float tau1 = 4.f * (d1 * (1.f + fabsf(ph1)) + em1 * dp1) + 1e-9f;
-          const float tau2 = 4.f * (d2 * (1.f + fabsf(ph2)) + em2 * dp2) + 1e-9f;
-          if (dbg && ln == 0) {
-            if (s1 >= 0 && s1 < AMOD_DBG_SYMS) D->phase[s1] = const1 ? 0.f : ph1;
-            if (s2 >= 0 && s2 < AMOD_DBG_SYMS) D->phase[s2] = const2 ? 0.f : ph2;
-          }
-          // a constant FFT window has an all-zero spectrum in the reference: every data
-          // subcarrier takes the origin decision (ties resolve to the first point).
-          // Decisions are staged as bytes by data index in the wave's exchange buffer
-          // (free once the band is read), then packed below.
-          int dflag = 0;
-          uint8_t *const stg = reinterpret_cast<uint8_t *>(LDS_F2 + xb);
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int b = ln + 64 * rr;
-            if (b >= nband) continue;
-            const int di = di_l[rr];
-            if (di < 0) continue;
-#pragma unroll
-            for (int which = 0; which < 2; ++which) {
-              const int sidx = which == 0 ? s1 : s2;
-              if (sidx < 0) continue;
-              const bool live = which == 0 ? live1 : live2;
-              int idx = cfg.origin_idx;
-              if (live) {
-                const float2 e = which == 0 ? e1[rr] : e2[rr];
-                const float ph = which == 0 ? ph1 : ph2;
-                const float cr = fmaf(e.y, ph, e.x);
-                const float ci = fmaf(-e.x, ph, e.y);
-                float margin;
-                idx = decide(cfg.mod, cr, ci, margin);
-                dflag |= margin <= (which == 0 ? tau1 : tau2);
-              }
-              stg[256 * which + di] = (uint8_t)idx;
-            }
-          }
-          if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
-          __builtin_amdgcn_wave_barrier();
-          // pack: lane t takes data subcarrier 64 q + t; each aligned group of 32/bps lanes
-          // ORs (DPP) its bits into one word of the symbol's word-aligned row, written by
-          // the group's first lane (no atomics: a symbol belongs to one wave)
-          {
-            const int bps = cfg.bps, ndata = cfg.ndata;
-#pragma unroll
-            for (int which = 0; which < 2; ++which) {
-              const int sidx = which == 0 ? s1 : s2;
-              if (sidx < 0) continue;
-              uint32_t *const row = LDS_U + fq_sa + sidx * wsym;
-              for (int q = 0; 64 * q < ndata; ++q) {
-                const int di = 64 * q + ln;
-                const uint32_t idx = di < ndata ? (uint32_t)stg[256 * which + di] : 0u;
-                uint32_t v = idx << (32 - bps - ((di * bps) & 31));
-                v |= (uint32_t)AMOD_DPP_I((int)v, 0xB1);
-                v |= (uint32_t)AMOD_DPP_I((int)v, 0x4E);
-                v |= (uint32_t)AMOD_DPP_I((int)v, 0x141); // groups of 8 (16-QAM)
-                if (bps < 4) v |= (uint32_t)AMOD_DPP_I((int)v, 0x140); // 16 (QPSK)
-                if (bps < 2) v |= (uint32_t)__shfl_xor((int)v, 16, 32); // 32 (BPSK)
-                if ((ln & (32 / bps - 1)) == 0 && di < ndata) row[(di * bps) >> 5] = v;
-              }
-            }
-          }
-          if (r == 0) STAMP(first ? 11 : 18);
-        }
-      }
-      __syncthreads(); // the round's symbol rows are complete
-      STAMP(first ? 12 : 19);
-      done = target;
-      jdone = jend;
-      // rows [0, done) -> the MSB-first bit stream the parse, vote and CRC read
-      repack_rows(LDS_U + fq_sa, wsym, per_sym, min(done, M), fq_bits);
-      __syncthreads();
-      // how much of the voted stream the parse reads; decode more symbols if needed
-      if (tid == 0) {
-        const int avail = ((min(done * per_sym, nbits) / cfg.rep) >> 3);
-        need_bytes = parse_need(fq_bits, cfg.rep, avail, nbytes_total, cfg.mode);
-        int t = done;
-        if (need_bytes > avail) {
-          const int64_t raw = (int64_t)need_bytes * 8 * cfg.rep;
-          t = (int)min<int64_t>((int64_t)M, ((raw + per_sym - 1) / per_sym) | 1); // whole jobs
-          if ((int64_t)t * per_sym > bitc * 32 || t * wsym > w.rows_cap) sm.flags |= AMOD_FLAG_BIG;
-        }
-        sm.target = t;
-        sm.ru[0] = (uint32_t)need_bytes;
-      }
-      __syncthreads();
-      if (sm.flags || sm.target <= done) break;
-    }
-    need_bytes = (int)sm.ru[0];
-    wflags = wor_i(wflags);
-    if (lane == 0 && wflags) atomicOr(&sm.flags, wflags);
-    __syncthreads();
-    if (sm.flags) goto to_exact;
-    STAMP(14);
-    // ------------------------------------------------ stage 4: finish
-    if (cfg.stop_after == 3) return;
-    {
-      FRESH_ARGS;
-      if (dbg && tid == 0) D->nsym = M;
-      const uint32_t *v = fq_bits;
-      const int nv = nbits / cfg.rep;
-      if (cfg.rep > 1) {
-        // vote only the decoded prefix (the parse reads need_bytes bytes)
-        uint32_t *voted = reinterpret_cast<uint32_t *>(LDS_F2);
-        const int decoded = min(done * per_sym, nbits);
-        block_vote(fq_bits, min(decoded, need_bytes * 8 * cfg.rep), cfg.rep, voted);
-        __syncthreads();
-        v = voted;
-      }
-      amod_result r;
-      init_result(r);
-      r.nbits = nbits;
-      if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = sm.fbest; r.coarse_idx = sm.coarse; r.preamble_idx = start; }
-      finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru + 4, nullptr,
-                   need_bytes);
-      STAMP(15);
-      return;
-    }
+    DetRec d;
+    d.route = ROUTE_DEMOD; d.flags = 0; d.start = start; d.M = M; d.T = T; d.coarse = sm.coarse;
+    d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
+    w.det[f] = d;
   }
+  return;
 
 finish_error:
   if (tid == 0) {
     amod_result r;
     init_result(r);
     r.status = sm.status;
-    if (cfg.mode == AMOD_MODE_RECEIVED) {
-      r.coarse_idx = sm.status == AMOD_E_PREAMBLE ? -1 : sm.coarse;
-      r.fine_metric = sm.status == AMOD_E_PREAMBLE ? 0.f : sm.fbest;
-    }
+    r.coarse_idx = sm.status == AMOD_E_PREAMBLE ? -1 : sm.coarse;
+    r.fine_metric = sm.status == AMOD_E_PREAMBLE ? 0.f : sm.fbest;
     r.preamble_idx = -1;
     w.res[f] = r;
+    if (w.det) w.det[f].route = ROUTE_DONE;
   }
   return;
 
 to_exact:
-  if (tid == 0) {
-    const int i = atomicAdd(w.fb_count, 1);
-    w.fb_list[i] = f;
-    w.fb_flags[i] = sm.flags;
-  }
+  if (tid == 0) list_exact(w, f, sm.flags);
 }
 
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast(const DevCfg cfg_arg, const DevWork w_arg) {
+// ------------------------------------------------------------ detection kernels
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_detect(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  decode_fast<false, false>();
+  detect<false, false>();
 }
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_decode_fast_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_detect_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  decode_fast<false, true>();
+  detect<false, true>();
 }
 // stream pass + Schmidl-Cox only (diagnostics: AMOD_STOP_AFTER=1); launched with the same
-// dynamic LDS as k_decode_fast, so the same number of workgroups share a CU
+// dynamic LDS as k_detect, so the same number of workgroups share a CU
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_SCAN_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  decode_fast<true, false>();
+  detect<true, false>();
 }
+
+// decodeChunkFrame (modem.js:770-786): no preprocessing, the frame starts at pre1;
+// one thread per window writes its detection record (or its geometry error)
+__global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWork w) {
+  const int f = w.f0 + (int)(blockIdx.x * WG + threadIdx.x);
+  if (f >= w.f1) return;
+  const int N = w.len[f], SYM = cfg.sym;
+  const int route = frame_route(cfg, w, N);
+  if (route) { list_exact(w, f, route); return; }
+  if (3 * SYM >= N) {
+    amod_result r;
+    init_result(r);
+    r.status = 3 * SYM > N ? AMOD_E_FRAME_SHORT_CE : AMOD_E_NO_DATA;
+    w.res[f] = r;
+    w.det[f].route = ROUTE_DONE;
+    return;
+  }
+  DetRec d;
+  d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = d.M; d.coarse = -1;
+  d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
+  w.det[f] = d;
+}
+
+// ------------------------------------------------------------ demodulation
+// k_demod: persistent waves, one frame at a time per wave (frames last-first: the ones
+// k_detect streamed last are the likeliest to still sit in the Infinity Cache), no
+// workgroup barrier after the twiddle staging. A frame is a sequence of FFT jobs:
+// job 0 = (CE, data symbol 0), job j = (2j-1, 2j); two real symbols share one complex
+// 512-pt FFT (X1 = (Z[k] + conj Z[-k]) / 2, X2 = (Z[k] - conj Z[-k]) / 2i). Job 0's CE
+// half gives the channel estimate (estimateChannel, modem.js:421-440) kept in registers
+// as G = 1/H for the lane's band subcarriers; every data symbol is equalised, pilot-phase
+// corrected and demapped (demodulateOFDM 365-418) with decision margins and its
+// decisions OR-ed into the frame's MSB-first bit stream in the wave's LDS. The next
+// job's samples (the next frame's first job at a frame's end) are in flight while the
+// current one computes. At the frame's end the wave runs majorityVote, the parse, the
+// CRC-32 and the stores (modem.js:468-495, 605-654, 805-849). A decision inside its
+// guard band (or a parse that reads past the demodulated symbols) lists the frame for
+// the exact kernel instead.
+
+// Wave-level CRC-32 (modem.js:443-457) of bytes [0, L) of stream v. The message is cut
+// into 16-byte chunks, right-aligned (chunk 0 may be short); every chunk's register is
+// computed independently with slice-by-4 tables (chunk 0 from the initial ~0, the others
+// from 0), moved to the message end by the GF(2) matrix of its zero-byte shift, and the
+// images are XOR-combined (CRC linearity). Lane l takes chunks l, l + 64, ... (ILP across
+// them), so one pass covers up to kCrcMats chunks; longer messages carry the register
+// into the next block.
+// bytes i .. i + 3 of an MSB-first stream as one little-endian word (CRC byte order)
+__device__ __forceinline__ uint32_t le_word_at(const uint32_t *v, int i) {
+  const int wi = i >> 2, sh = 8 * (i & 3);
+  const uint32_t lo = v[wi];
+  return __builtin_bswap32(sh ? (lo << sh) | (v[wi + 1] >> (32 - sh)) : lo);
+}
+// CRC register over bytes [beg, end) from c; t4 = the slice-by-4 tables (LDS)
+__device__ __forceinline__ uint32_t crc_chunk(const uint32_t *v, int beg, int end, uint32_t c, const uint32_t *t4) {
+  int i = beg;
+  for (; i + 4 <= end; i += 4) {
+    c ^= le_word_at(v, i);
+    c = t4[768 + (c & 0xFF)] ^ t4[512 + ((c >> 8) & 0xFF)] ^ t4[256 + ((c >> 16) & 0xFF)] ^ t4[c >> 24];
+  }
+  for (; i < end; ++i) c = t4[(c ^ stream_byte(v, i)) & 0xFF] ^ (c >> 8);
+  return c;
+}
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32_t c) {
+  const uint4 *const mq = reinterpret_cast<const uint4 *>(mat + 32 * q);
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 m = mq[k];
+    r ^= m.x & (uint32_t)((int32_t)(c << (31 - 4 * k)) >> 31);
+    r ^= m.y & (uint32_t)((int32_t)(c << (30 - 4 * k)) >> 31);
+    r ^= m.z & (uint32_t)((int32_t)(c << (29 - 4 * k)) >> 31);
+    r ^= m.w & (uint32_t)((int32_t)(c << (28 - 4 * k)) >> 31);
+  }
+  return r;
+}
+__device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4) {
+  const int lane = wave_lane();
+  constexpr int BLOCKB = kCrcMats * kCrcChunk; // bytes per block
+  uint32_t reg = 0xFFFFFFFFu; // carried between blocks (uniform)
+  for (int p0 = 0; p0 < L; p0 += BLOCKB) {
+    const int plen = min(BLOCKB, L - p0);
+    const int nch = (plen + kCrcChunk - 1) / kCrcChunk; // chunks, right-aligned
+    uint32_t acc = 0;
+    for (int j = lane; j < nch; j += 64) {
+      const int end = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
+      const int beg = max(0, end - kCrcChunk);
+      const uint32_t c = crc_chunk(v, p0 + beg, p0 + end, j == 0 ? reg : 0u, t4);
+      acc ^= crc_shift(t.crc_mat, nch - 1 - j, c);
+    }
+    reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
+  }
+  return reg ^ 0xFFFFFFFFu;
+}
+
+// Majority vote (modem.js:487-495) of the first nbits of `bits` into `voted`, one wave.
+__device__ inline void wave_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
+  const int nv = nbits / rep;
+  const int nw = (nv + 31) >> 5;
+  const int thr = (rep + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
+  for (int wd = wave_lane(); wd < nw; wd += 64) {
+    uint32_t word = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int j = wd * 32 + b;
+      if (j >= nv) break;
+      int sum = 0;
+      for (int u = 0; u < rep; ++u) {
+        const int pos = j * rep + u;
+        sum += (bits[pos >> 5] >> (31 - (pos & 31))) & 1;
+      }
+      word |= (uint32_t)(sum >= thr) << (31 - b);
+    }
+    voted[wd] = word;
+  }
+}
+
+struct FrameS {  // wave-uniform facts of one frame on the demodulation path
+  int f, T, M, nj, start, coarse;
+  float A, B, fbest;
+  const float *X;
+};
+
+// MOD: the launch's modulation as a template argument (decisions and packing unroll)
+template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
+  constexpr int BPS = MOD == AMOD_BPSK ? 1 : (MOD == AMOD_QPSK ? 2 : 4);
+  __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][512];
+  __shared__ float2 twl[512];   // tw1 rows 1-7 (row q at 64 (q - 1)), then tw2[64]
+  __shared__ uint32_t crc4[1024]; // slice-by-4 CRC tables
+  FRESH_ARGS;
+  const int tid = ltid();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  {
+    const float2 t1a = cfg.t.tw1[64 + tid], t1b = cfg.t.tw1[64 + min(tid + WG, 447)], t2 = cfg.t.tw2[tid & 63];
+    const uint4 c4 = reinterpret_cast<const uint4 *>(cfg.t.crc_s4)[tid];
+    twl[tid] = t1a;
+    if (tid + WG < 7 * 64) twl[WG + tid] = t1b;
+    if (tid < 64) twl[7 * 64 + tid] = t2;
+    reinterpret_cast<uint4 *>(crc4)[tid] = c4;
+  }
+  __syncthreads();
+  const int lane = tid & 63;
+  const int SYM = cfg.sym, CP = cfg.cp, nband = cfg.nband, sub_start = cfg.sub_start;
+  const int ndata = cfg.ndata, per_sym = ndata * BPS, origin_idx = cfg.origin_idx;
+  const bool chunk_mode = cfg.mode == AMOD_MODE_CHUNK;
+  const float guard = cfg.guard;
+  const int nfr = w.f1 - w.f0; // frames [f0, f1) of this launch
+  const int wstride = (int)gridDim.x * NWAVE;
+  // the wave's bit stream (and voted stream) in dynamic LDS
+  uint32_t *const bits = LDS_U + wave * w.stream_words;
+  uint32_t *const voted = bits + w.vote_off;
+  float2 *const X2 = xch[wave];
+  const float2 *const tw1 = twl - 64, *const tw2 = twl + 7 * 64;
+  // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
+  // (two 16-bit fields per register: registers bound k_demod's occupancy)
+  uint32_t di_pk[2] = {0u, 0u};
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int di = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
+    di_pk[rr >> 1] |= ((uint32_t)di & 0xFFFFu) << (16 * (rr & 1));
+  }
+  auto di_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
+  // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
+  // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
+  int prr = -1, npl = 0;
+#pragma unroll
+  for (int rr = 3; rr >= 0; --rr)
+    if (di_of(rr) == -1) { prr = rr; ++npl; }
+  const bool pil_multi = __ballot(npl > 1) != 0;
+  uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(lane + 64 * rr < nband && cfg.t.known[lane + 64 * rr] < 0.f) << rr;
+
+  // next frame on the demodulation path at or after wave-iteration k (frames last-first)
+  auto next_frame = [&](int k, FrameS &F) -> int {
+    for (; k < nfr; k += wstride) {
+      const int f = w.f1 - 1 - k;
+      const DetRec d = sload(w.det + f);
+      if (d.route != ROUTE_DEMOD) continue;
+      F.f = f; F.T = d.T; F.M = d.M; F.nj = d.T > 0 ? 1 + d.T / 2 : 0; F.start = d.start; F.coarse = d.coarse;
+      F.A = d.A; F.B = d.B; F.fbest = d.fbest;
+      F.X = w.samples + sload(w.off + f);
+      return k;
+    }
+    return nfr;
+  };
+  // symbols of job j: s1 (-2 = the CE symbol), s2 (-1 = none)
+  auto job_syms = [](const FrameS &F, int j, int &s1, int &s2) {
+    if (j == 0) { s1 = -2; s2 = 0; }
+    else { s1 = 2 * j - 1; s2 = 2 * j < F.T ? 2 * j : -1; }
+  };
+  auto job_loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) {
+    int s1, s2;
+    job_syms(F, j, s1, s2);
+    const int data0 = F.start + 3 * SYM;
+    const int p1 = (s1 == -2 ? F.start + 2 * SYM : data0 + s1 * SYM) + CP;
+    const int p2 = s2 >= 0 ? data0 + s2 * SYM + CP : p1;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      r1[m] = F.X[p1 + lane + 64 * m];
+      r2[m] = F.X[p2 + lane + 64 * m];
+    }
+  };
+
+  float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
+  float gmax = 0.f, zce = 0.f; // guard scales of the frame (job 0)
+  int wflags = 0;
+  // one job of frame `cur` (jcur = 0 starts the frame; a frame without data symbols has
+  // one empty job, so every frame passes through its frame end)
+  auto run_job = [&](const FrameS &cur, const int jcur, const float (&c1)[8], const float (&c2)[8]) {
+#define DSTAMP(k, cond)                                                                   \
+  do {                                                                                  \
+    if (w.stamps && (cond) && lane == 0) w.stamps[(int64_t)cur.f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+    const int f = cur.f;
+    amod_debug *const D = DBG ? w.dbg + f : nullptr;
+    if (jcur == 0) { // a new frame: clear its bit stream
+      const int nwz = (cur.T * per_sym + 31) / 32 + 2;
+      for (int i = lane; i < nwz; i += 64) bits[i] = 0u;
+      wflags = 0;
+    }
+    // ---------------------------------------------------------------- job (cur, jcur)
+    if (cur.T > 0) {
+      int s1, s2;
+      job_syms(cur, jcur, s1, s2);
+      const bool ce = s1 == -2;
+      const float f1v = rlane(c1[0], 0), f2v = rlane(c2[0], 0);
+      int ne1 = 0, ne2 = 0, nf = 0;
+      float2 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        ne1 |= c1[m] != f1v;
+        ne2 |= c2[m] != f2v;
+        if (chunk_mode) nf |= !isfinite(c1[m]) || !isfinite(c2[m]); // received: stage 0 saw them
+        v[m] = make_float2(fmaf(c1[m], cur.A, cur.B), s2 >= 0 ? fmaf(c2[m], cur.A, cur.B) : 0.f);
+      }
+      // a window is constant iff every raw sample equals its first one (all-zero spectrum)
+      const bool const1 = __ballot(ne1) == 0, const2 = __ballot(ne2) == 0;
+      if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
+      DSTAMP(16, jcur == 1);
+      fft512_wave(v, X2, tw1, tw2);
+      DSTAMP(17, jcur == 1);
+      int ln = lane;
+      asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
+      float zm = 0.f;
+      float2 x1[4], x2[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int b = ln + 64 * rr;
+        x1[rr] = x2[rr] = make_float2(0.f, 0.f);
+        if (b < nband) {
+          const int k = sub_start + b;
+          const float2 zk = spec_read(X2, k), zn = spec_read(X2, kFft - k);
+          zm = fmaxf(zm, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
+          // Z = x1 + i x2:  X1 = (Z[k] + conj Z[-k]) / 2,  X2 = (Z[k] - conj Z[-k]) / 2i
+          x1[rr] = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
+          x2[rr] = make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
+        }
+      }
+      if (ce) {
+        // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
+        zce = wmax_nn(zm);
+        float gm = 0.f;
+        int ch = 0;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int b = ln + 64 * rr;
+          const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
+          const float2 h = const1 ? make_float2(0.f, 0.f) : make_float2(x1[rr].x * kn, x1[rr].y * kn);
+          const float m2 = h.x * h.x + h.y * h.y;
+          float2 g;
+          if (m2 > 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the 2e-6 eq bound
+          else g = make_float2(1.f, 0.f);
+          // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
+          ch |= b < nband && !const1 && m2 < 1e-6f;
+          gl[rr] = g;
+          if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
+          if (DBG && b < nband) { D->h_re[b] = h.x; D->h_im[b] = h.y; }
+        }
+        gmax = wmax_nn(gm);
+        if (__ballot(ch)) wflags |= AMOD_FLAG_CHANNEL;
+      }
+      // equalise both halves (the CE half of job 0 is not a data symbol)
+      float2 e1[4], e2[4];
+      float em1 = 0.f, em2 = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        e1[rr] = cmul(x1[rr], gl[rr]);
+        e2[rr] = cmul(x2[rr], gl[rr]);
+        em1 = fmaxf(em1, fabsf(e1[rr].x) + fabsf(e1[rr].y));
+        em2 = fmaxf(em2, fabsf(e2[rr].x) + fabsf(e2[rr].y));
+        const int b = ln + 64 * rr;
+        if (DBG && b < nband && (s1 == 0 || s2 == 0)) {
+          const bool one = s1 == 0;
+          const float2 xx = one ? x1[rr] : x2[rr], ee = one ? e1[rr] : e2[rr];
+          const bool c = one ? const1 : const2;
+          D->x_re[b] = c ? 0.f : xx.x; D->x_im[b] = c ? 0.f : xx.y;
+          D->eq_re[b] = c ? 0.f : ee.x; D->eq_im[b] = c ? 0.f : ee.y;
+        }
+      }
+      DSTAMP(18, jcur == 1);
+      // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
+      const float gsc = 2e-6f * guard * gmax;
+      float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
+      d1 = wmax_nn(d1); d2 = wmax_nn(d2);
+      d1 += 1e-12f; d2 += 1e-12f;
+      const bool live1 = !ce && !const1, live2 = s2 >= 0 && !const2;
+      // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
+      float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
+      int pflag = 0;
+      auto pilot = [&](bool pil, float2 q1e, float2 q2e) {
+        const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
+        // 0/1 weights in VGPRs (no lane masks kept live)
+        const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
+        // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below;
+        // signed 1/eqRe, finite for every lane (weight 0 where the reference skips)
+        const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), q1e.x));
+        const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), q2e.x));
+        const float r1 = fabsf(q1), r2 = fabsf(q2);
+        ps1 = fmaf(w1 * q1, q1e.y, ps1);
+        ps2 = fmaf(w2 * q2, q2e.y, ps2);
+        pe1 = fmaf(w1 * r1, fmaf(fabsf(q1e.y), r1, 1.f), pe1);
+        pe2 = fmaf(w2 * r2, fmaf(fabsf(q2e.y), r2, 1.f), pe2);
+        pc1 += w1;
+        pc2 += w2;
+        pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
+      };
+      if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
+        float2 p1 = e1[0], p2 = e2[0];
+#pragma unroll
+        for (int rr = 1; rr < 4; ++rr) {
+          p1 = prr == rr ? e1[rr] : p1;
+          p2 = prr == rr ? e2[rr] : p2;
+        }
+        pilot(prr >= 0, p1, p2);
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) pilot(di_of(rr) == -1, e1[rr], e2[rr]);
+      }
+      ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); pc1 = wsum_b(pc1); pc2 = wsum_b(pc2);
+      if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
+      const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
+      const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
+      const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
+      const float dp1 = d1 * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d2 * pe2 * ip2 + 1e-6f * fabsf(ph2);
+      const float tau1 = 4.f * (d1 * (1.f + fabsf(ph1)) + em1 * dp1) + 1e-9f;
+      const float tau2 = 4.f * (d2 * (1.f + fabsf(ph2)) + em2 * dp2) + 1e-9f;
+      DSTAMP(19, jcur == 1);
+      if (DBG && ln == 0) {
+        if (s1 >= 0 && s1 < AMOD_DBG_SYMS) D->phase[s1] = const1 ? 0.f : ph1;
+        if (s2 >= 0 && s2 < AMOD_DBG_SYMS) D->phase[s2] = const2 ? 0.f : ph2;
+      }
+      // a constant FFT window has an all-zero spectrum in the reference: every data
+      // subcarrier takes the origin decision (ties resolve to the first point).
+      // Each decision is OR-ed straight into the frame's MSB-first stream (LDS atomic OR;
+      // BPS divides 32, so a decision never straddles a word)
+      int dflag = 0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int b = ln + 64 * rr;
+        const int di = di_of(rr);
+        const bool dat = b < nband && di >= 0;
+#pragma unroll
+        for (int which = 0; which < 2; ++which) {
+          const int sidx = which == 0 ? s1 : s2;
+          if (sidx < 0) continue; // wave-uniform
+          const bool live = which == 0 ? live1 : live2;
+          const float2 e = which == 0 ? e1[rr] : e2[rr];
+          const float ph = which == 0 ? ph1 : ph2;
+          const float cr = fmaf(e.y, ph, e.x);
+          const float ci = fmaf(-e.x, ph, e.y);
+          float margin;
+          const int dec = decide(MOD, cr, ci, margin);
+          const int idx = live ? dec : origin_idx;
+          dflag |= dat && live && margin <= (which == 0 ? tau1 : tau2);
+          const int pos = sidx * per_sym + di * BPS;
+          if (dat && idx) atomicOr(bits + (pos >> 5), (uint32_t)idx << (32 - BPS - (pos & 31)));
+        }
+      }
+      if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
+      DSTAMP(20, jcur == 1);
+      __builtin_amdgcn_wave_barrier();
+      DSTAMP(21, jcur == 1);
+    }
+    // ---------------------------------------------------------------- frame end
+    if (jcur + 1 >= max(cur.nj, 1)) {
+      DSTAMP(22, true);
+      if (wflags) {
+        if (lane == 0) list_exact(w, f, wflags);
+      } else {
+        const int nbits = cur.M * per_sym;
+        const int nbytes_total = (nbits / cfg.rep) >> 3;
+        const int decoded = cur.T * per_sym;
+        int need = 0;
+        if (lane == 0) {
+          const int avail = (min(decoded, nbits) / cfg.rep) >> 3;
+          need = parse_need(bits, cfg.rep, avail, nbytes_total, cfg.mode);
+          if (need > avail) need = -1;
+        }
+        need = __builtin_amdgcn_readfirstlane(need);
+        DSTAMP(23, true);
+        if (need < 0) {
+          if (lane == 0) list_exact(w, f, AMOD_FLAG_SPAN);
+        } else {
+          const uint32_t *v = bits;
+          if (cfg.rep > 1) { // vote only the decoded prefix the parse reads
+            wave_vote(bits, min(decoded, need * 8 * cfg.rep), cfg.rep, voted);
+            __builtin_amdgcn_wave_barrier();
+            v = voted;
+          }
+          // parse (modem.js:605-654, 793-849), CRC over [0, off), payload prefix
+          amod_result r;
+          init_result(r);
+          r.nbits = nbits;
+          if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = cur.fbest; r.coarse_idx = cur.coarse; r.preamble_idx = cur.start; }
+          const int nbytes = (nbits / cfg.rep) >> 3;
+          const int crc_len = parse_stream(v, nbytes, cfg.mode, r); // every lane: the same bytes
+          if (cfg.mode == AMOD_MODE_RECEIVED) {
+            // preambleIdx is reported on legacy success and on every 0xFE/0xFF result (609-620)
+            const bool keep = (r.frame_type == 0xFE || r.frame_type == 0xFF) || (r.frame_type == 0 && r.status == AMOD_OK);
+            if (!keep) r.preamble_idx = -1;
+          } else {
+            r.preamble_idx = -1;
+          }
+          DSTAMP(24, true);
+          if (crc_len >= 0) {
+            r.actual_crc = wave_crc32(v, crc_len, cfg.t, crc4);
+            r.crc_valid = r.expected_crc == r.actual_crc;
+          }
+          DSTAMP(25, true);
+          const int store_bytes = min(need, nbytes);
+          r.payload_valid = store_bytes;
+          // payload bytes, big-endian words -> memory order
+          const int nw = (store_bytes + 3) >> 2;
+          uint32_t *const dst = reinterpret_cast<uint32_t *>(w.payload + (int64_t)f * w.stride);
+          const int cap_w = (int)(w.stride >> 2);
+          for (int i = lane; i < nw && i < cap_w; i += 64) {
+            uint32_t word = v[i];
+            const int keep = store_bytes - 4 * i; // bytes of this word that were decoded
+            if (keep < 4) word &= ~(0xFFFFFFFFu >> (8 * keep));
+            dst[i] = __builtin_bswap32(word);
+          }
+          if (DBG && lane == 0) D->nsym = cur.M;
+          // the record: 24 words, one per lane
+          const int32_t *const rw = reinterpret_cast<const int32_t *>(&r);
+          int32_t val = 0;
+#pragma unroll
+          for (int i = 0; i < 24; ++i) val = lane == i ? rw[i] : val;
+          if (lane < 24) reinterpret_cast<int32_t *>(w.res + f)[lane] = val;
+          DSTAMP(26, true);
+        }
+      }
+      __builtin_amdgcn_wave_barrier(); // the stream is read before the next frame clears it
+    }
+  };
+  // the job after (F, k, j): the frame's next, or the next frame's first; false at the end
+  auto advance = [&](FrameS &F, int &k, int &j) -> bool {
+    if (j + 1 < max(F.nj, 1)) { ++j; return true; }
+    FrameS nf;
+    const int kn = next_frame(k + wstride, nf);
+    if (kn >= nfr) return false;
+    F = nf; k = kn; j = 0;
+    return true;
+  };
+  // every load is unconditional (a frame without data symbols reads its CE window, the
+  // last job re-reads its own samples), so the in-order vmcnt accounting stays exact
+  auto loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) { job_loads(F, j, r1, r2); };
+  // two-stage pipeline, unrolled by two with ping-pong registers (no loop-carried copies,
+  // so the compiler's waits cover only the job being computed): the next job's samples
+  // are in flight while this one computes
+  FrameS fa, fb;
+  int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
+  if (ka >= nfr) return;
+  const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
+  if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
+  float a1[8], a2[8], b1[8], b2[8];
+  loads(fa, ja, a1, a2);
+  for (;;) {
+    fb = fa; kb = ka; jb = ja;
+    const bool hb = advance(fb, kb, jb);
+    if (!hb) { fb = fa; jb = ja; }
+    loads(fb, jb, b1, b2);
+    run_job(fa, ja, a1, a2);
+    if (!hb) break;
+    fa = fb; ka = kb; ja = jb;
+    const bool ha = advance(fa, ka, ja);
+    if (!ha) { fa = fb; ja = jb; }
+    loads(fa, ja, a1, a2);
+    run_job(fb, jb, b1, b2);
+    if (!ha) break;
+  }
+  if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
+}
+template <int MOD> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  demod_loop<false, MOD>();
+}
+template <int MOD> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  demod_loop<true, MOD>();
+}
+typedef void (*demod_fn)(const DevCfg, const DevWork);
+__host__ demod_fn demod_kernel(int mod, bool dbg) {
+  if (mod == AMOD_BPSK) return dbg ? k_demod_dbg<AMOD_BPSK> : k_demod<AMOD_BPSK>;
+  if (mod == AMOD_QPSK) return dbg ? k_demod_dbg<AMOD_QPSK> : k_demod<AMOD_QPSK>;
+  return dbg ? k_demod_dbg<AMOD_QAM16> : k_demod<AMOD_QAM16>;
+}
+
 
 } // namespace
 } // namespace amod
 
-extern "C" hipError_t amod_launch_fast(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s) {
-  if (w.nframes <= 0) return hipSuccess;
-  auto *k = w.dbg ? amod::k_decode_fast_dbg : (cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_decode_fast);
-  hipLaunchKernelGGL(k, dim3(w.nframes), dim3(amod::WG),
-                     (unsigned)amod_fast_lds_bytes(w.nb_cap, w.bits_cap, w.rows_cap), s, cfg, w);
-  return hipGetLastError();
-}
-// dynamic LDS bytes of a launch with nb_cap moment blocks, bits_cap stream words and
-// rows_cap symbol-row words
-extern "C" int amod_fast_lds_bytes(int nb_cap, int bits_cap, int rows_cap) {
+// ------------------------------------------------------------ launchers
+// dynamic LDS bytes of a k_detect workgroup with nb_cap moment blocks and fine_cap
+// fine-search positions
+extern "C" int amod_fast_lds_bytes(int nb_cap, int fine_cap) {
   using namespace amod;
   const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND + 8 * 32 * SC_CACHE;
-  const int fine = 4 * (FINE_E + FINE_MAX + 800);
-  const int fq = 4 * (FQ_ROWS + rows_cap + 1);
-  return (std::max(mom, std::max(fine, fq)) + 15) & ~15;
+  const int fine = 4 * fine_floats(fine_cap);
+  return (std::max(mom, fine) + 15) & ~15;
+}
+// per-wave bit-stream words of k_demod (stream, then the voted stream when rep > 1)
+extern "C" void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_words, int *vote_off) {
+  const int s = ((mcap * cfg.ndata * cfg.bps + 31) / 32 + 4 + 3) & ~3;
+  const int v = cfg.rep > 1 ? ((s / cfg.rep + 4 + 3) & ~3) : 0;
+  *vote_off = s;
+  *stream_words = s + v;
+}
+
+// both launchers take frames [w.f0, w.f1)
+extern "C" hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s) {
+  const int n = w.f1 - w.f0;
+  if (n <= 0) return hipSuccess;
+  if (cfg.mode == AMOD_MODE_CHUNK) {
+    hipLaunchKernelGGL(amod::k_chunk_prep, dim3((n + amod::WG - 1) / amod::WG), dim3(amod::WG), 0, s, cfg, w);
+    return hipGetLastError();
+  }
+  auto *k = w.dbg ? amod::k_detect_dbg : (cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_detect);
+  hipLaunchKernelGGL(k, dim3(n), dim3(amod::WG), (unsigned)amod_fast_lds_bytes(w.nb_cap, w.fine_cap), s, cfg, w);
+  return hipGetLastError();
+}
+extern "C" hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s) {
+  if (w.f1 <= w.f0 || nblocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amod::demod_kernel(cfg.mod, w.dbg != nullptr), dim3(nblocks), dim3(amod::WG),
+                     (unsigned)(4 * amod::NWAVE * w.stream_words), s, cfg, w);
+  return hipGetLastError();
+}
+// k_demod blocks resident at once on one CU for a dynamic LDS of lds bytes
+extern "C" int amod_demod_blocks_per_cu(int mod, int lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, amod::demod_kernel(mod, false), amod::WG, lds) != hipSuccess ||
+      n <= 0)
+    n = 4;
+  return n;
 }

@@ -224,6 +224,9 @@ std::vector<int32_t> cfg_key(const amod_cfg &c) {
 
 } // namespace
 
+constexpr int kMaxChunks = 16;   // frame chunks of one decode (two-stream overlap)
+constexpr int kOverlapChunks = 1; // default chunk count (measured: overlap slows both launches)
+
 struct amod_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -233,6 +236,10 @@ struct amod_ctx {
   DevBuf fb;           // fb_count + list + flags
   DevBuf xs, bits;     // exact-kernel scratch
   DevBuf soft;         // exact-kernel soft bit values (AMOD_OPT_SOFT_COMBINE only)
+  DevBuf det;          // fast path: per-frame detection records (k_detect -> k_demod)
+  hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
+  std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
+  int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_bpc = 0;
   int64_t soft_stride = 0;
   int soft_slots = 0;
   int64_t xs_stride = 0, bits_stride = 0;
@@ -246,7 +253,8 @@ struct amod_ctx {
   int64_t nstamps = 0;
   // kernel timing (amod_set_profiling)
   bool profiling = false;
-  std::vector<std::array<hipEvent_t, 3>> ev_used, ev_free;
+  // per decode: before k_detect, after k_detect, after k_demod, after k_decode_exact
+  std::vector<std::array<hipEvent_t, 4>> ev_used, ev_free;
 };
 
 namespace {
@@ -272,8 +280,8 @@ int validate(const amod_cfg *c) {
 
 int build_crc(amod_ctx *ctx) {
   if (ctx->crc.p) return AMOD_SUCCESS;
-  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024);
-  uint32_t *s4 = h.data(), *m1 = s4 + 1024, *m2 = m1 + 32 * 1024, *mb = m2 + 32 * 1024;
+  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024 + amod::kCrcMats * 32);
+  uint32_t *s4 = h.data(), *m1 = s4 + 1024, *m2 = m1 + 32 * 1024, *mb = m2 + 32 * 1024, *mat = mb + 1024;
   const uint32_t *t0 = crc_table();
   for (int i = 0; i < 256; ++i) s4[i] = t0[i];
   for (int k = 1; k < 4; ++k)
@@ -283,6 +291,13 @@ int build_crc(amod_ctx *ctx) {
     shift_operator((int64_t)amod::kCrcChunk * 32 * q, m2 + q * 1024);
   }
   shift_operator(amod::kCrcBlock, mb);
+  for (int b = 0; b < 32; ++b) { // matrices: column b = the register 1 << b after 16 q zero bytes
+    uint32_t r = 1u << b;
+    for (int q = 0; q < amod::kCrcMats; ++q) {
+      mat[32 * q + b] = r;
+      for (int i = 0; i < 16; ++i) r = crc_table()[r & 0xFF] ^ (r >> 8);
+    }
+  }
   HIP_TRY(ctx->crc.ensure(h.size() * 4));
   HIP_TRY(hipMemcpy(ctx->crc.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   return AMOD_SUCCESS;
@@ -382,6 +397,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.t.crc_m1 = crc + 1024;
     d.t.crc_m2 = crc + 1024 + 32 * 1024;
     d.t.crc_mb = crc + 1024 + 64 * 1024;
+    d.t.crc_mat = crc + 1024 + 64 * 1024 + 1024;
     it = ctx->tables.emplace(key, std::move(ts)).first;
   }
   out = it->second->cfg;
@@ -390,6 +406,28 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
 
 int64_t max_bits_for(const amod_cfg *c, int64_t max_len) {
   return (max_len / c->symbol_len) * (int64_t)amod_num_data_subs(c) * bps_of(c->modulation);
+}
+
+constexpr int64_t kFastMaxLen = int64_t(1) << 18; // longest frame the fast path takes (k_detect moments in LDS)
+
+// capacities of one fast-path launch over frames of up to max_len samples
+struct ChainDims {
+  int64_t fast_len;
+  int nb_cap, fine_cap, mcap;
+};
+ChainDims chain_dims(const amod_cfg *c, int64_t max_len) {
+  ChainDims d;
+  d.fast_len = std::min<int64_t>(std::max<int64_t>(max_len, 0), kFastMaxLen);
+  d.nb_cap = 8 * (int)((d.fast_len + 3 + 255) / 256) + 8;
+  d.fine_cap = (12 * c->cp_len + 1 + 7) & ~7; // every window the coarse stage lets through
+  d.mcap = (int)std::max<int64_t>(0, d.fast_len / c->symbol_len - 3);
+  return d;
+}
+
+// device buffers of the fast path for nframes frames (grow-only)
+int ensure_chain(amod_ctx *ctx, int32_t nframes) {
+  HIP_TRY(ctx->det.ensure(sizeof(amod::DetRec) * (size_t)std::max(nframes, 1)));
+  return AMOD_SUCCESS;
 }
 
 int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
@@ -413,7 +451,7 @@ int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) 
   ctx->bits_stride = bits_stride;
   ctx->nslots = (int)slots;
   ctx->max_len = std::max<int64_t>(ctx->max_len, max_len);
-  return AMOD_SUCCESS;
+  return ensure_chain(ctx, nframes);
 }
 
 int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, const int64_t *offsets,
@@ -455,13 +493,18 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.soft = (float *)ctx->soft.p;
     w.soft_stride = ctx->soft_stride;
   }
-  { // fast-kernel LDS sized for the longest frame of this launch (host path) or reservation
-    const int64_t flen = max_len >= 0 ? max_len : ctx->max_len;
-    w.nb_cap = 8 * (int)((flen + 3 + 255) / 256) + 8;
-    const int64_t words = (flen / cfg->symbol_len) * amod_num_data_subs(cfg) * bps_of(cfg->modulation) / 32 + 2;
-    w.bits_cap = (int)std::min<int64_t>(2048, words);
-    const int64_t wsym = ((int64_t)amod_num_data_subs(cfg) * bps_of(cfg->modulation) + 31) / 32;
-    w.rows_cap = (int)std::min<int64_t>(4096, (flen / cfg->symbol_len) * wsym + 2);
+  // fast-path capacities from the longest frame of this launch (host path) or of the
+  // reservation (device path); a frame's route depends only on it and on the frame
+  const ChainDims dims = chain_dims(cfg, max_len >= 0 ? max_len : ctx->max_len);
+  rc = ensure_chain(ctx, nframes);
+  if (rc) return rc;
+  w.nb_cap = dims.nb_cap; w.fine_cap = dims.fine_cap; w.mcap = dims.mcap; w.fast_len = dims.fast_len;
+  amod_demod_stream_words(d, dims.mcap, &w.stream_words, &w.vote_off);
+  w.det = (amod::DetRec *)ctx->det.p;
+  if (!ctx->cu_count) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, ctx->device));
+    ctx->cu_count = prop.multiProcessorCount;
   }
   if (getenv("AMOD_STAMPS")) { // diagnostics: per-frame s_memtime marks of the fast kernel
     HIP_TRY(ctx->stamps.ensure(sizeof(unsigned long long) * 32 * (size_t)nframes));
@@ -469,8 +512,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.stamps = (unsigned long long *)ctx->stamps.p;
     ctx->nstamps = nframes;
   }
-  HIP_TRY(hipMemsetAsync(fb, 0, 256, s));
-  std::array<hipEvent_t, 3> ev{};
+  HIP_TRY(hipMemsetAsync(fb, 0, 256, s)); // exact-list and job counters
+  std::array<hipEvent_t, 4> ev{};
   if (ctx->profiling) {
     if (ctx->ev_free.empty()) {
       for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
@@ -478,15 +521,52 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       ev = ctx->ev_free.back();
       ctx->ev_free.pop_back();
     }
-    HIP_TRY(hipEventRecord(ev[0], s));
   }
-  HIP_TRY(amod_launch_fast(d, w, s));
-  if (ctx->profiling) HIP_TRY(hipEventRecord(ev[1], s));
+  auto mark = [&](int i) -> hipError_t { return ctx->profiling ? hipEventRecord(ev[i], s) : hipSuccess; };
+  // d.stop_after (diagnostics, AMOD_STOP_AFTER): <= 2 stops after detection
+  const bool demod = d.stop_after >= 3;
+  const int lds = 4 * 4 * w.stream_words; // k_demod: 4 waves per block
+  if (ctx->demod_lds != lds || ctx->demod_mod != d.mod) {
+    ctx->demod_lds = lds; ctx->demod_mod = d.mod; ctx->demod_bpc = amod_demod_blocks_per_cu(d.mod, lds);
+  }
+  int64_t per_cu = ctx->demod_bpc;
+  if (const char *g = getenv("AMOD_DEMOD_BPC")) per_cu = std::max(1, atoi(g)); // diagnostics: grid size
+  auto demod_blocks = [&](int n) { return (int)std::min<int64_t>(((int64_t)n + 3) / 4, (int64_t)ctx->cu_count * per_cu); };
+  // Frames in chunks over two streams: k_detect of chunk c + 1 (HBM-bound) runs on `s`
+  // while k_demod of chunk c (latency-bound FFT jobs) runs on the context's second
+  // stream, so the demodulation hides under the next chunk's stream pass.
+  int nchunk = 1;
+  if (demod && !debug && nframes >= 2048) nchunk = kOverlapChunks;
+  if (const char *oc = getenv("AMOD_CHUNKS")) nchunk = std::max(1, std::min(kMaxChunks, atoi(oc)));
+  if (!demod || debug) nchunk = 1;
+  nchunk = std::min(nchunk, std::max(1, nframes));
+  HIP_TRY(mark(0));
+  if (nchunk == 1) {
+    w.f0 = 0; w.f1 = nframes;
+    HIP_TRY(amod_launch_detect(d, w, s));
+    HIP_TRY(mark(1));
+    if (demod) HIP_TRY(amod_launch_demod(d, w, demod_blocks(nframes), s));
+  } else {
+    if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    for (auto &e : ctx->chunk_ev)
+      if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int c = 0; c < nchunk; ++c) {
+      w.f0 = (int)((int64_t)nframes * c / nchunk);
+      w.f1 = (int)((int64_t)nframes * (c + 1) / nchunk);
+      HIP_TRY(amod_launch_detect(d, w, s));
+      HIP_TRY(hipEventRecord(ctx->chunk_ev[c], s));
+      HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[c], 0));
+      HIP_TRY(amod_launch_demod(d, w, demod_blocks(w.f1 - w.f0), ctx->aux));
+    }
+    HIP_TRY(mark(1)); // every k_detect done (on s)
+    HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0));
+  }
+  w.f0 = 0; w.f1 = nframes;
+  HIP_TRY(mark(2));
   HIP_TRY(amod_launch_exact(d, w, std::min(ctx->nslots, nframes), s));
-  if (ctx->profiling) {
-    HIP_TRY(hipEventRecord(ev[2], s));
-    ctx->ev_used.push_back(ev);
-  }
+  HIP_TRY(mark(3));
+  if (ctx->profiling) ctx->ev_used.push_back(ev);
   return AMOD_SUCCESS;
 }
 
@@ -629,6 +709,11 @@ int amod_close(amod_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->aux) { (void)hipStreamSynchronize(ctx->aux); (void)hipStreamDestroy(ctx->aux); }
+  for (auto &e : ctx->chunk_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &ev : ctx->ev_used) for (auto &e : ev) (void)hipEventDestroy(e);
+  for (auto &ev : ctx->ev_free) for (auto &e : ev) (void)hipEventDestroy(e);
   delete ctx;
   return AMOD_SUCCESS;
 }
@@ -758,24 +843,35 @@ int amod_set_profiling(amod_ctx *ctx, int enable) {
   return AMOD_SUCCESS;
 }
 
-int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_n, double *exact_ms, int64_t *exact_n) {
+int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n) {
   if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->device));
-  double f = 0, x = 0;
+  double acc[3] = {0, 0, 0};
   for (auto &ev : ctx->ev_used) {
-    HIP_TRY(hipEventSynchronize(ev[2]));
-    float a = 0, b = 0;
-    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
-    f += a; x += b;
+    HIP_TRY(hipEventSynchronize(ev[3]));
+    for (int i = 0; i < 3; ++i) {
+      float t = 0;
+      HIP_TRY(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      acc[i] += t;
+    }
     ctx->ev_free.push_back(ev);
   }
-  if (fast_ms) *fast_ms = f;
-  if (exact_ms) *exact_ms = x;
-  if (fast_n) *fast_n = (int64_t)ctx->ev_used.size();
-  if (exact_n) *exact_n = (int64_t)ctx->ev_used.size();
+  if (ms) for (int i = 0; i < 3; ++i) ms[i] = acc[i];
+  if (n) *n = (int64_t)ctx->ev_used.size();
   ctx->ev_used.clear();
+  return AMOD_SUCCESS;
+}
+
+int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_n, double *exact_ms, int64_t *exact_n) {
+  double ms[3];
+  int64_t n = 0;
+  const int rc = amod_kernel_breakdown(ctx, ms, &n);
+  if (rc) return rc;
+  if (fast_ms) *fast_ms = ms[0] + ms[1];
+  if (exact_ms) *exact_ms = ms[2];
+  if (fast_n) *fast_n = n;
+  if (exact_n) *exact_n = n;
   return AMOD_SUCCESS;
 }
 

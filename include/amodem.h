@@ -87,6 +87,8 @@ extern "C" {
 #define AMOD_FLAG_PHASE (1 << 6)     /* pilot |eqRe| near the 1e-6 threshold        */
 #define AMOD_FLAG_DEMAP (1 << 7)     /* a constellation decision within guard band  */
 #define AMOD_FLAG_THRESH (1 << 8)    /* preprocess peak near the 1e-6 threshold     */
+#define AMOD_FLAG_SPAN (1 << 9)      /* the parse reads bytes past the symbols the fast
+                                        path demodulated (signal energy ended early)   */
 #define AMOD_FLAG_EXACT (1 << 15)    /* result produced by the exact-replica kernel */
 
 /* OFDM parameters + modulation; mirrors OFDM (modem.js:69-98) */
@@ -160,12 +162,16 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
                      amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options);
 int amod_synchronize(amod_ctx *ctx);
 
-/* kernel timing: when enabled, every decode brackets k_decode_fast and
-   k_decode_exact with hipEvents on the launch stream; amod_kernel_times waits
-   for them, returns the accumulated milliseconds and launch counts, and resets */
+/* kernel timing: when enabled, every decode brackets each launch of the fast path
+   (k_detect, k_demod) and k_decode_exact with hipEvents on the launch
+   stream; amod_kernel_times waits for them, returns the accumulated milliseconds of
+   the fast path and of the exact kernel and the decode count, and resets */
 int amod_set_profiling(amod_ctx *ctx, int enable);
 int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_launches, double *exact_ms,
                       int64_t *exact_launches);
+/* the same events split by launch: ms[0..2] = k_detect (k_chunk_prep in chunk mode),
+   k_demod, k_decode_exact, accumulated over *n decodes; resets like amod_kernel_times */
+int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n);
 
 /* parity-test view of one frame's intermediates (filled when debug != NULL) */
 #define AMOD_DBG_BAND 256
