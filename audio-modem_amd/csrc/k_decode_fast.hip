@@ -54,7 +54,7 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone)
 #endif
 #ifndef AMOD_DEMOD_WPE
-#define AMOD_DEMOD_WPE 4                     // k_demod: 109 registers, no spills
+#define AMOD_DEMOD_WPE 5                     // k_demod: 96 registers, no spills
 #endif
 
 // Dynamic LDS of k_detect, sized per launch (amod_fast_lds_bytes): one region reused
@@ -1178,7 +1178,7 @@ __device__ __forceinline__ uint32_t le_word_at(const uint32_t *v, int i) {
   const uint32_t lo = v[wi];
   return __builtin_bswap32(sh ? (lo << sh) | (v[wi + 1] >> (32 - sh)) : lo);
 }
-// CRC register over bytes [beg, end) from c; t4 = the slice-by-4 tables (LDS)
+// CRC register over bytes [beg, end) from c; t4 = the slice-by-4 tables
 __device__ __forceinline__ uint32_t crc_chunk(const uint32_t *v, int beg, int end, uint32_t c, const uint32_t *t4) {
   int i = beg;
   for (; i + 4 <= end; i += 4) {
@@ -1252,17 +1252,14 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   constexpr int BPS = MOD == AMOD_BPSK ? 1 : (MOD == AMOD_QPSK ? 2 : 4);
   __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][512];
   __shared__ float2 twl[512];   // tw1 rows 1-7 (row q at 64 (q - 1)), then tw2[64]
-  __shared__ uint32_t crc4[1024]; // slice-by-4 CRC tables
   FRESH_ARGS;
   const int tid = ltid();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   {
     const float2 t1a = cfg.t.tw1[64 + tid], t1b = cfg.t.tw1[64 + min(tid + WG, 447)], t2 = cfg.t.tw2[tid & 63];
-    const uint4 c4 = reinterpret_cast<const uint4 *>(cfg.t.crc_s4)[tid];
     twl[tid] = t1a;
     if (tid + WG < 7 * 64) twl[WG + tid] = t1b;
     if (tid < 64) twl[7 * 64 + tid] = t2;
-    reinterpret_cast<uint4 *>(crc4)[tid] = c4;
   }
   __syncthreads();
   const int lane = tid & 63;
@@ -1333,7 +1330,9 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   int wflags = 0;
   // one job of frame `cur` (jcur = 0 starts the frame; a frame without data symbols has
   // one empty job, so every frame passes through its frame end)
-  auto run_job = [&](const FrameS &cur, const int jcur, const float (&c1)[8], const float (&c2)[8]) {
+  // c1 / c2: the job's samples; issue_next() refills them with the next job's once the
+  // FFT has consumed them, so those loads fly under this job's equalise / demap / finish
+  auto run_job = [&](const FrameS &cur, const int jcur, float (&c1)[8], float (&c2)[8], auto &&issue_next) {
 #define DSTAMP(k, cond)                                                                   \
   do {                                                                                  \
     if (w.stamps && (cond) && lane == 0) w.stamps[(int64_t)cur.f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -1346,6 +1345,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       wflags = 0;
     }
     // ---------------------------------------------------------------- job (cur, jcur)
+    if (cur.T <= 0) issue_next();
     if (cur.T > 0) {
       int s1, s2;
       job_syms(cur, jcur, s1, s2);
@@ -1365,6 +1365,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
       DSTAMP(16, jcur == 1);
       fft512_wave(v, X2, tw1, tw2);
+      issue_next();
       DSTAMP(17, jcur == 1);
       int ln = lane;
       asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
@@ -1550,7 +1551,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
           }
           DSTAMP(24, true);
           if (crc_len >= 0) {
-            r.actual_crc = wave_crc32(v, crc_len, cfg.t, crc4);
+            r.actual_crc = wave_crc32(v, crc_len, cfg.t, cfg.t.crc_s4); // 4 KB table, L1-resident
             r.crc_valid = r.expected_crc == r.actual_crc;
           }
           DSTAMP(25, true);
@@ -1591,29 +1592,20 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   // every load is unconditional (a frame without data symbols reads its CE window, the
   // last job re-reads its own samples), so the in-order vmcnt accounting stays exact
   auto loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) { job_loads(F, j, r1, r2); };
-  // two-stage pipeline, unrolled by two with ping-pong registers (no loop-carried copies,
-  // so the compiler's waits cover only the job being computed): the next job's samples
-  // are in flight while this one computes
+  // the sample registers are refilled with the next job right after each FFT
   FrameS fa, fb;
   int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
   if (ka >= nfr) return;
   const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
-  float a1[8], a2[8], b1[8], b2[8];
-  loads(fa, ja, a1, a2);
+  float r1[8], r2[8];
+  loads(fa, ja, r1, r2);
   for (;;) {
     fb = fa; kb = ka; jb = ja;
     const bool hb = advance(fb, kb, jb);
-    if (!hb) { fb = fa; jb = ja; }
-    loads(fb, jb, b1, b2);
-    run_job(fa, ja, a1, a2);
+    run_job(fa, ja, r1, r2, [&] { if (hb) loads(fb, jb, r1, r2); });
     if (!hb) break;
     fa = fb; ka = kb; ja = jb;
-    const bool ha = advance(fa, ka, ja);
-    if (!ha) { fa = fb; ja = jb; }
-    loads(fa, ja, a1, a2);
-    run_job(fb, jb, b1, b2);
-    if (!ha) break;
   }
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
 }
