@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--stream-chunks", type=int, default=2000,
                     help="C4-shaped stream for the streaming-receiver leg (0 = skip)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="CPU-baseline sample (0 = auto, -1 = skip)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive leg")
     args = ap.parse_args()
 
     import torch
@@ -179,6 +180,11 @@ def main():
     lib.amod_set_profiling(dm.ctx, 0)
     stage_ms = [kms[i] / max(1, kn.value) for i in range(3)]  # per decode: detect, demod, exact
 
+    e2e = None
+    if not args.no_e2e:
+        e2e = e2e_leg(torch, dm, cfg, mode, xs, nsamples, d_doff, d_dlen, F, d_res, d_pay, stride, dev, ndecoded,
+                      payload_bytes)
+
     gather = None
     if world > 1:
         gather = gather_leg(amodem, dist, torch, dev, rank, world, F, stride, d_res, d_pay, C4, payload_bytes)
@@ -276,12 +282,41 @@ def main():
                                 "unit": "GB/s", "frac": tx_bytes / (tx_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
                    "cpu_baseline": tx_cpu},
             "stream": stream_res,
+            "e2e": e2e,
             "gather": gather,
         }
         print(json.dumps(out), flush=True)
     dm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def e2e_leg(torch, dm, cfg, mode, xs, nsamples, d_off, d_len, F, d_res, d_pay, stride, dev, ndecoded, payload_bytes,
+            reps=3):
+    """Host-resident batch, PCIe included (BASELINE.md "two timing modes"): the samples
+    in pinned host memory, copied H2D, decoded, result records and payload slots copied
+    back to pinned memory, on one stream; wall time per pass (never `value`)."""
+    h_x = torch.empty(nsamples, dtype=torch.float32, pin_memory=True)
+    h_x.copy_(xs[:nsamples])
+    h_res = torch.empty(d_res.numel(), dtype=torch.uint8, pin_memory=True)
+    h_pay = torch.empty(d_pay.numel(), dtype=torch.uint8, pin_memory=True)
+    st = torch.cuda.Stream(dev)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(st):
+            xs[:nsamples].copy_(h_x, non_blocking=True)
+            dm.decode_device(cfg, mode, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F, d_res.data_ptr(),
+                             d_pay.data_ptr(), stride, stream=st.cuda_stream)
+            h_res.copy_(d_res, non_blocking=True)
+            h_pay.copy_(d_pay, non_blocking=True)
+        st.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts[1:])[len(ts[1:]) // 2]
+    return {"what": "pinned host samples -> H2D -> decode -> D2H records + payload, one stream, median of %d" % reps,
+            "samples_per_s": ndecoded / t, "payload_MB_per_s": payload_bytes * F / t / 1e6, "ms": t * 1e3,
+            "h2d_GBps": 4.0 * nsamples / t / 1e9}
 
 
 def gather_leg(amodem, dist, torch, dev, rank, world, F, stride, d_res, d_pay, chunk_mode, payload_bytes, reps=3):
@@ -378,9 +413,12 @@ def stream_leg(amodem, L, device, nchunks=2000, chunk=2048):
 
 
 def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
-    """The C restatement of the reference RX (oracle/, kind 'port') on this host's
-    cores over a bounded sample of the same frames, repeated to ~1 s of wall time
-    (~16 s of CPU work on 16 threads)."""
+    """The C restatement of the reference RX (oracle/, kind 'port') on this host's cores
+    over a bounded sample of the same frames: all cores (16 threads, repeated to ~1 s of
+    wall time, ~16 s of CPU work) and one core (~2 s). profiles/cpu_calibration.json
+    (tools/calibrate_cpu.py, build container) holds the measured speed ratio of this port
+    to the reference modem.js on one core; dividing by it gives the modem.js-equivalent
+    rates reported beside the port's own."""
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
     c = O.cfg("standard")
@@ -391,10 +429,25 @@ def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
         t += dt
         reps += 1
     samples = float(lens.sum()) * reps
-    return {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{len(offs)} {name} frames x {reps} passes ({int(samples)} samples), "
-                      f"oracle/amodem_oracle.c{' (decodeChunkFrame)' if chunk else ''}, {threads} threads",
-            "payload_MB_per_s": payload * len(offs) * reps / t / 1e6, "seconds": t}
+    n1 = min(len(offs), 1000)  # one core: ~2 s
+    t1, st, _ = O.bench_decode(c, x, offs[:n1], lens[:n1], mod, 1, 1, chunk=chunk)
+    assert (st == 0).all()
+    single = float(lens[:n1].sum()) / t1
+    out = {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
+           "sample": f"{len(offs)} {name} frames x {reps} passes ({int(samples)} samples) on {threads} threads; "
+                     f"{n1} frames on 1 thread; oracle/amodem_oracle.c{' (decodeChunkFrame)' if chunk else ''}",
+           "payload_MB_per_s": payload * len(offs) * reps / t / 1e6, "seconds": t + t1,
+           "single_core": single}
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    key = {"C2": "c2", "C3": "c3", "C4": "c4", "C5": "c5"}.get(name)
+    if os.path.exists(cal) and key:
+        with open(cal) as f:
+            r = json.load(f)["workloads"][key]["ratio_oracle_over_modem_js"]
+        out["port_over_modem_js"] = r
+        out["modem_js_equivalent"] = {"single_core": single / r, "all_cores": samples / t / r,
+                                      "note": "port rates / the port-to-modem.js ratio measured in the build "
+                                              "container (profiles/cpu_calibration.json)"}
+    return out
 
 
 def tx_cpu_baseline(amodem, cfg, nframes, spf):
