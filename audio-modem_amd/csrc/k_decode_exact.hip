@@ -149,17 +149,59 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     const float *sig = xr; // samples the demodulator reads
 
     const bool loop = cfg.mode == AMOD_MODE_LOOPBACK; // analyzeLoopback's receive core
+    // A frame the fast path listed only for demodulation-stage guards (k_demod: decision
+    // margins, pilot |eqRe|, |H|^2, a parse past the demodulated symbols) already has a
+    // proven preambleIdx: the replica runs preprocess + demodulation only.
+    const bool demod_only = cfg.mode == AMOD_MODE_RECEIVED && w.det && flags0 != 0 &&
+        (flags0 & ~(AMOD_FLAG_DEMAP | AMOD_FLAG_PHASE | AMOD_FLAG_CHANNEL | AMOD_FLAG_SPAN)) == 0;
     if (cfg.mode != AMOD_MODE_CHUNK) {
-      // ---- preprocessSignal: sequential mean, then |f32(x - mean)| max, then scale
-      double sum = 0.0;
-      for (int c0 = 0; c0 < N; c0 += CH) {
-        const int n = min(CH, N - c0);
-        for (int i = tid; i < n; i += XT) sm.chunk[i] = xr[c0 + i];
-        __syncthreads();
-        if (tid == 0) for (int i = 0; i < n; ++i) sum += (double)sm.chunk[i];
-        __syncthreads();
+      // ---- preprocessSignal: the mean is a sequential double sum (modem.js:215-217).
+      // Every partial sum of floats is a multiple of 2^emin (the smallest sample ulp) and
+      // at most sum|x| in magnitude; when sum|x| < 2^(emin + 53) no partial sum rounds, in
+      // any order, so the parallel sum is bit-equal to the sequential one. Otherwise (or
+      // with non-finite samples) the sum runs sequentially.
+      double ps = 0.0, pa = 0.0;
+      int emin = 1 << 20, nonfin = 0;
+      for (int i = tid; i < N; i += XT) {
+        const float x = xr[i];
+        ps += (double)x;
+        pa += fabs((double)x);
+        const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
+        if (e == 0xFFu) nonfin = 1;
+        else if (x != 0.0f) emin = min(emin, e == 0 ? -149 : (int)e - 150);
       }
-      if (tid == 0) sm.mean = sum / (double)N;
+      for (int o = 32; o > 0; o >>= 1) {
+        ps += __shfl_xor(ps, o, 64);
+        pa += __shfl_xor(pa, o, 64);
+        emin = min(emin, __shfl_xor(emin, o, 64));
+        nonfin |= __shfl_xor(nonfin, o, 64);
+      }
+      if (lane == 0) { sm.rd[wave] = ps; sm.ri[wave] = emin; sm.ri[XT / 64 + wave] = nonfin; }
+      if (lane == 0) sm.er[wave] = pa;
+      __syncthreads();
+      bool exact_par = true;
+      if (tid == 0) {
+        double S = 0.0, PA = 0.0;
+        int EM = 1 << 20, NF = 0;
+        for (int i = 0; i < XT / 64; ++i) { S += sm.rd[i]; PA += sm.er[i]; EM = min(EM, sm.ri[i]); NF |= sm.ri[XT / 64 + i]; }
+        exact_par = !NF && (EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53));
+        sm.mean = S / (double)N;
+        sm.status = exact_par;
+      }
+      __syncthreads();
+      exact_par = sm.status != 0;
+      __syncthreads();
+      if (!exact_par) {
+        double sum = 0.0;
+        for (int c0 = 0; c0 < N; c0 += CH) {
+          const int n = min(CH, N - c0);
+          for (int i = tid; i < n; i += XT) sm.chunk[i] = xr[c0 + i];
+          __syncthreads();
+          if (tid == 0) for (int i = 0; i < n; ++i) sum += (double)sm.chunk[i];
+          __syncthreads();
+        }
+        if (tid == 0) sm.mean = sum / (double)N;
+      }
       __syncthreads();
       const double mean = sm.mean;
       double mx = 0.0;
@@ -188,7 +230,13 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       const int half = kFft / 2;
       int coarse = -1;
       double best = 0.0;
-      if (N >= 2 * half) {
+      if (demod_only) {
+        // the fast path's detection record: preambleIdx proven by its guards
+        const DetRec dr = w.det[f];
+        r.coarse_idx = dr.coarse;
+        r.fine_metric = dr.fbest;
+        r.preamble_idx = start = dr.start;
+      } else if (N >= 2 * half) {
         const int end = N - 2 * half;
         double p = 0.0, ra = 0.0, rb = 0.0;
         for (int c0 = 0; c0 <= end; c0 += CH) {
@@ -224,6 +272,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         sm.best = 0.0; sm.coarse = -1;
       }
       __syncthreads();
+      if (!demod_only) {
       coarse = sm.coarse;
       if (loop && coarse < 0) coarse = crosscorr_detect(xs, N, cfg, sm); // modem.js:982-985
       r.coarse_idx = coarse;
@@ -275,6 +324,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         else if (start + 3 * SYM > N) status = AMOD_E_SHORT_CE;
         else if (start + 3 * SYM >= N) status = AMOD_E_NO_DATA;
         r.preamble_idx = start;
+      }
       }
     } else {
       if (3 * SYM > N) status = AMOD_E_FRAME_SHORT_CE;

@@ -1,7 +1,8 @@
-"""The fast kernel answers clean frames itself: no exact-path routing on the presets
-whose fine search window fits its LDS stage (standard, acoustic). A regression here
-is a silent slowdown (the exact replica still gives the right bytes), so it is pinned
-on the flags the kernel reports, not on the results."""
+"""The fast path answers clean frames itself: no exact-path routing on any preset
+(the fine-search stage holds 12 CP + 1 positions, so narrowband's 6 x 256-sample
+window fits too). A regression here is a silent slowdown (the exact replica still
+gives the right bytes), so it is pinned on the flags the kernels report, not on the
+results."""
 import numpy as np
 import pytest
 
@@ -10,7 +11,7 @@ import amodem
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("preset", ["standard", "acoustic"])
+@pytest.mark.parametrize("preset", ["standard", "acoustic", "narrowband"])
 @pytest.mark.parametrize("mod", ["BPSK", "QPSK", "QAM16"])
 def test_clean_frames_stay_on_fast_path(preset, mod):
     cfg = amodem.preset(preset, mod, 1)
@@ -21,3 +22,27 @@ def test_clean_frames_stay_on_fast_path(preset, mod):
     assert (rec["status"] == 0).all() and (rec["crc_valid"] == 1).all()
     flags = rec["flags"] & ~(1 << 15)
     assert (flags == 0).all(), np.unique(flags)
+
+
+@pytest.mark.parametrize("preset", ["standard", "acoustic", "narrowband"])
+def test_noisy_demap_fallback_keeps_detection(preset):
+    """Frames routed to the exact kernel only for demodulation-stage guards (decision
+    margins under AWGN) reuse the fast path's proven preambleIdx: the replica runs the
+    demodulation alone. Results equal a forced full-exact decode."""
+    from amodem import _lib as L
+    cfg = amodem.preset(preset, "BPSK", 3)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, 48, payload_len=128, threads=8)
+    rng = np.random.default_rng(7)
+    sig_pow = float(np.mean(x[x != 0] ** 2))
+    xn = (x + rng.standard_normal(len(x)).astype(np.float32) * np.float32(np.sqrt(sig_pow / 10 ** 0.5))).astype(np.float32)
+    dm = amodem.Demodulator(0)
+    rec, pay = dm.decode_batch(xn, offs, lens, cfg=cfg)
+    ref, rpay = dm.decode_batch(xn, offs, lens, cfg=cfg, options=L.OPT_FORCE_EXACT)
+    dm.close()
+    vis = [n for n in amodem.RESULT_DTYPE.names if n not in ("flags", "payload_valid", "fine_metric", "coarse_idx",
+                                                             "reserved")]
+    for n in vis:
+        assert (rec[n] == ref[n]).all(), n
+    for i in range(len(rec)):
+        k = int(rec["payload_valid"][i])
+        assert pay[i, :k].tobytes() == rpay[i, :k].tobytes(), i

@@ -98,6 +98,8 @@ def _debug_decode(dm, case, x, options):
 
 
 DEBUG_CASES = [c for c in frames() if "sym0" in c["inter"]]
+# flags raised by k_demod (demodulation stage): DEMAP, PHASE, CHANNEL, SPAN
+DEMOD_FLAGS = (1 << 7) | (1 << 6) | (1 << 5) | (1 << 9)
 
 
 @pytest.mark.parametrize("exact", [False, True], ids=["fast", "exact"])
@@ -122,8 +124,16 @@ def test_intermediates(dm, case, exact):
         assert np.array_equal(ph, phref)
         if case["rx"] == "legacy":
             assert d.mean == inter["mean"] and d.mx == inter["mx"]
-            assert d.coarse_lo == inter["coarseIdx"] and d.fine_idx == inter["startIdx"]
-            assert d.fine_metric == inter["fineMetric"]
+            assert d.fine_idx == inter["startIdx"]
+            # a frame listed only for demodulation-stage guards keeps the fast path's
+            # (proven) detection: plateau + fp32 fine metric; otherwise the replica's own
+            demod_only = not exact and (int(r["flags"]) & ~(L.FLAG_EXACT | DEMOD_FLAGS)) == 0
+            if demod_only:
+                assert d.coarse_lo <= inter["coarseIdx"] <= d.coarse_hi
+                assert abs(d.fine_metric - inter["fineMetric"]) <= 1e-4
+            else:
+                assert d.coarse_lo == inter["coarseIdx"]
+                assert d.fine_metric == inter["fineMetric"]
     else:
         scale = max(1.0, float(np.abs(href).max()))
         assert np.abs(h - href).max() <= ABS_TOL * scale
