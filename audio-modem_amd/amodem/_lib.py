@@ -24,6 +24,7 @@ OPT_SOFT_COMBINE = 2  # not reference behaviour: soft repetition combining (opt-
 OK = 0
 E_CAPACITY = 100
 FLAG_SPAN = 1 << 9
+FLAG_SOFT = 1 << 10
 FLAG_EXACT = 1 << 15
 
 

@@ -305,6 +305,11 @@ def crc32(data: bytes) -> int:
     return int(L.load().amod_crc32(data, len(data)))
 
 
+def num_data_subs(cfg: L.Cfg) -> int:
+    """numDataSubs (modem.js:89-93): in-band subcarriers that are not pilots."""
+    return int(L.load().amod_num_data_subs(C.byref(cfg)))
+
+
 def payload_stride(cfg: L.Cfg, max_len: int) -> int:
     return int(L.load().amod_payload_stride(C.byref(cfg), int(max_len)))
 

@@ -150,10 +150,11 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
 
     const bool loop = cfg.mode == AMOD_MODE_LOOPBACK; // analyzeLoopback's receive core
     // A frame the fast path listed only for demodulation-stage guards (k_demod: decision
-    // margins, pilot |eqRe|, |H|^2, a parse past the demodulated symbols) already has a
-    // proven preambleIdx: the replica runs preprocess + demodulation only.
+    // margins, pilot |eqRe|, |H|^2, a parse past the demodulated symbols) or for opt-in
+    // soft combining already has a proven preambleIdx: the replica runs preprocess +
+    // demodulation only.
     const bool demod_only = cfg.mode == AMOD_MODE_RECEIVED && w.det && flags0 != 0 &&
-        (flags0 & ~(AMOD_FLAG_DEMAP | AMOD_FLAG_PHASE | AMOD_FLAG_CHANNEL | AMOD_FLAG_SPAN)) == 0;
+        (flags0 & ~(AMOD_FLAG_DEMAP | AMOD_FLAG_PHASE | AMOD_FLAG_CHANNEL | AMOD_FLAG_SPAN | AMOD_FLAG_SOFT)) == 0;
     if (cfg.mode != AMOD_MODE_CHUNK) {
       // ---- preprocessSignal: the mean is a sequential double sum (modem.js:215-217).
       // Every partial sum of floats is a multiple of 2^emin (the smallest sample ulp) and

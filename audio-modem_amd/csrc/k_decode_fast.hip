@@ -318,7 +318,6 @@ __device__ __forceinline__ float dpp_sum8(float v) {
 // the launch's fast-path length only (never on other frames of the batch).
 __device__ __forceinline__ int frame_route(const DevCfg &cfg, const DevWork &w, int N) {
   if (w.options & AMOD_OPT_FORCE_EXACT) return AMOD_FLAG_FORCED;
-  if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) return AMOD_FLAG_FORCED; // opt-in soft vote
   if ((int64_t)N > w.fast_len) return AMOD_FLAG_BIG; // longer than the launch's fast-path workspace
   return 0;
 }
@@ -1088,6 +1087,8 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
     d.route = ROUTE_DEMOD; d.flags = 0; d.start = start; d.M = M; d.T = T; d.coarse = sm.coarse;
     d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
     w.det[f] = d;
+    // opt-in soft combining (not reference behaviour): the exact kernel demodulates
+    if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
   }
   return;
 
@@ -1147,6 +1148,7 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
   d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = d.M; d.coarse = -1;
   d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
   w.det[f] = d;
+  if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
 }
 
 // ------------------------------------------------------------ demodulation
@@ -1327,7 +1329,24 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
 
   float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
   float gmax = 0.f, zce = 0.f; // guard scales of the frame (job 0)
-  int wflags = 0;
+  // state of the frame being demodulated (wave-uniform): jobs it takes (shrinks once the
+  // header says how many bytes the parse reads), those bytes (-1: not yet known), the
+  // first data symbol with a decision inside its guard band, flags
+  int live_f = -1, fnj = 0, fneed = -1, flag_sym = 0x7fffffff;
+  int wflags = 0;  // NONFINITE / CHANNEL: the whole frame goes to the exact kernel
+  int sflags = 0;  // DEMAP / PHASE of flag_sym and later: only if the parse reads them
+  const int rep = cfg.rep;
+  // bytes the parse reads once `dsym` data symbols are demodulated (-1: more needed)
+  auto eval_need = [&](const FrameS &F, int dsym) -> int {
+    const int nbits = F.M * per_sym;
+    int need = 0;
+    if (lane == 0) {
+      const int avail = (min(dsym * per_sym, nbits) / rep) >> 3;
+      need = parse_need(bits, rep, avail, (nbits / rep) >> 3, cfg.mode);
+      if (need > avail) need = -1 - need;
+    }
+    return __builtin_amdgcn_readfirstlane(need);
+  };
   // one job of frame `cur` (jcur = 0 starts the frame; a frame without data symbols has
   // one empty job, so every frame passes through its frame end)
   // c1 / c2: the job's samples; issue_next() refills them with the next job's once the
@@ -1342,7 +1361,11 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
     if (jcur == 0) { // a new frame: clear its bit stream
       const int nwz = (cur.T * per_sym + 31) / 32 + 2;
       for (int i = lane; i < nwz; i += 64) bits[i] = 0u;
-      wflags = 0;
+      live_f = f; fnj = max(cur.nj, 1); fneed = -1; flag_sym = 0x7fffffff;
+      wflags = 0; sflags = 0;
+    } else if (jcur >= fnj) { // prefetched before the header showed the frame was complete
+      issue_next();
+      return;
     }
     // ---------------------------------------------------------------- job (cur, jcur)
     if (cur.T <= 0) issue_next();
@@ -1434,7 +1457,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       const bool live1 = !ce && !const1, live2 = s2 >= 0 && !const2;
       // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
       float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
-      int pflag = 0;
+      int pflag1 = 0, pflag2 = 0;
       auto pilot = [&](bool pil, float2 q1e, float2 q2e) {
         const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
         // 0/1 weights in VGPRs (no lane masks kept live)
@@ -1450,7 +1473,8 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
         pe2 = fmaf(w2 * r2, fmaf(fabsf(q2e.y), r2, 1.f), pe2);
         pc1 += w1;
         pc2 += w2;
-        pflag |= pil && ((live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f) || (live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f));
+        pflag1 |= pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f;
+        pflag2 |= pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f;
       };
       if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
         float2 p1 = e1[0], p2 = e2[0];
@@ -1465,7 +1489,8 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
         for (int rr = 0; rr < 4; ++rr) pilot(di_of(rr) == -1, e1[rr], e2[rr]);
       }
       ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); pc1 = wsum_b(pc1); pc2 = wsum_b(pc2);
-      if (__ballot(pflag)) wflags |= AMOD_FLAG_PHASE;
+      // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
+      const bool ph_unc1 = __ballot(pflag1) != 0, ph_unc2 = __ballot(pflag2) != 0;
       const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
       const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
       const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
@@ -1481,7 +1506,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       // subcarrier takes the origin decision (ties resolve to the first point).
       // Each decision is OR-ed straight into the frame's MSB-first stream (LDS atomic OR;
       // BPS divides 32, so a decision never straddles a word)
-      int dflag = 0;
+      int dflag1 = 0, dflag2 = 0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int b = ln + 64 * rr;
@@ -1499,39 +1524,60 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
           float margin;
           const int dec = decide(MOD, cr, ci, margin);
           const int idx = live ? dec : origin_idx;
-          dflag |= dat && live && margin <= (which == 0 ? tau1 : tau2);
+          const int unc = dat && live && margin <= (which == 0 ? tau1 : tau2);
+          if (which == 0) dflag1 |= unc; else dflag2 |= unc;
           const int pos = sidx * per_sym + di * BPS;
           if (dat && idx) atomicOr(bits + (pos >> 5), (uint32_t)idx << (32 - BPS - (pos & 31)));
         }
       }
-      if (__ballot(dflag)) wflags |= AMOD_FLAG_DEMAP;
+      {
+        const bool d1u = __ballot(dflag1) != 0, d2u = __ballot(dflag2) != 0;
+        if (s1 >= 0 && (d1u || ph_unc1)) {
+          flag_sym = min(flag_sym, s1);
+          sflags |= (d1u ? AMOD_FLAG_DEMAP : 0) | (ph_unc1 ? AMOD_FLAG_PHASE : 0);
+        }
+        if (s2 >= 0 && (d2u || ph_unc2)) {
+          flag_sym = min(flag_sym, s2);
+          sflags |= (d2u ? AMOD_FLAG_DEMAP : 0) | (ph_unc2 ? AMOD_FLAG_PHASE : 0);
+        }
+      }
       DSTAMP(20, jcur == 1);
       __builtin_amdgcn_wave_barrier();
       DSTAMP(21, jcur == 1);
+      // once the header is decoded the parse's byte range is known: the frame takes only
+      // the jobs that demodulate it (trailing silence or noise is never transformed)
+      if (!DBG && fneed < 0 && !wflags) { // (parity-debug launches demodulate every symbol)
+        const int dsym = jcur == 0 ? 1 : min(2 * jcur + 1, cur.T);
+        // (the job count only ever shrinks, once the answer is final: the next job was
+        // chosen before this one ran, so a frame whose count grew would lose jobs)
+        const int need = eval_need(cur, dsym);
+        if (need >= 0) {
+          fneed = need;
+          fnj = jcur + 1;
+        }
+      }
     }
     // ---------------------------------------------------------------- frame end
-    if (jcur + 1 >= max(cur.nj, 1)) {
+    if (jcur + 1 >= fnj) {
       DSTAMP(22, true);
+      const int nbits = cur.M * per_sym;
+      const int decoded = cur.T * per_sym;
+      int need = fneed;
+      if (need < 0 && !wflags) {
+        need = eval_need(cur, cur.T); // no job (T = 0), or the symbols ran out first
+        if (need < 0) wflags |= AMOD_FLAG_SPAN;
+      }
+      // the last data symbol whose bits the parse reads
+      const int last_sym = need > 0 ? (int)(((int64_t)need * 8 * rep + per_sym - 1) / per_sym) - 1 : -1;
+      if (flag_sym <= last_sym) wflags |= sflags;
+      DSTAMP(23, true);
       if (wflags) {
         if (lane == 0) list_exact(w, f, wflags);
       } else {
-        const int nbits = cur.M * per_sym;
-        const int nbytes_total = (nbits / cfg.rep) >> 3;
-        const int decoded = cur.T * per_sym;
-        int need = 0;
-        if (lane == 0) {
-          const int avail = (min(decoded, nbits) / cfg.rep) >> 3;
-          need = parse_need(bits, cfg.rep, avail, nbytes_total, cfg.mode);
-          if (need > avail) need = -1;
-        }
-        need = __builtin_amdgcn_readfirstlane(need);
-        DSTAMP(23, true);
-        if (need < 0) {
-          if (lane == 0) list_exact(w, f, AMOD_FLAG_SPAN);
-        } else {
+        {
           const uint32_t *v = bits;
-          if (cfg.rep > 1) { // vote only the decoded prefix the parse reads
-            wave_vote(bits, min(decoded, need * 8 * cfg.rep), cfg.rep, voted);
+          if (rep > 1) { // vote only the decoded prefix the parse reads
+            wave_vote(bits, min(decoded, need * 8 * rep), rep, voted);
             __builtin_amdgcn_wave_barrier();
             v = voted;
           }
@@ -1540,7 +1586,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
           init_result(r);
           r.nbits = nbits;
           if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = cur.fbest; r.coarse_idx = cur.coarse; r.preamble_idx = cur.start; }
-          const int nbytes = (nbits / cfg.rep) >> 3;
+          const int nbytes = (nbits / rep) >> 3;
           const int crc_len = parse_stream(v, nbytes, cfg.mode, r); // every lane: the same bytes
           if (cfg.mode == AMOD_MODE_RECEIVED) {
             // preambleIdx is reported on legacy success and on every 0xFE/0xFF result (609-620)
@@ -1582,7 +1628,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   };
   // the job after (F, k, j): the frame's next, or the next frame's first; false at the end
   auto advance = [&](FrameS &F, int &k, int &j) -> bool {
-    if (j + 1 < max(F.nj, 1)) { ++j; return true; }
+    if (j + 1 < (F.f == live_f ? fnj : max(F.nj, 1))) { ++j; return true; }
     FrameS nf;
     const int kn = next_frame(k + wstride, nf);
     if (kn >= nfr) return false;

@@ -40,13 +40,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: 10k QPSK 1 KB frames per GPU (the metric's config); c3: 100k 16-QAM 1 KB frames; "
-                         "c4: 32k QPSK 2 KB data-chunk windows (decodeChunkFrame)")
+                         "c4: 32k QPSK 2 KB data-chunk windows (decodeChunkFrame); c5: 10k acoustic BPSK rep3 "
+                         "256 B frames + AWGN (--snr)")
+    ap.add_argument("--snr", type=float, default=20.0, help="c5: AWGN SNR in dB (active-sample power)")
+    ap.add_argument("--soft", action="store_true", help="c5: also decode once with AMOD_OPT_SOFT_COMBINE")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames per GPU (0: the config's, C2 10,000 / C3 100,000 / C4 32,000)")
-    ap.add_argument("--stream-chunks", type=int, default=2000,
-                    help="C4-shaped stream for the streaming-receiver leg (0 = skip)")
+    ap.add_argument("--stream-chunks", type=int, default=-1,
+                    help="C4-shaped stream for the streaming-receiver leg (0 = skip; default 2000 with c2)")
     ap.add_argument("--cpu-frames", type=int, default=0, help="CPU-baseline sample (0 = auto, -1 = skip)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive leg")
     args = ap.parse_args()
@@ -78,8 +81,10 @@ def main():
         if world > 1:
             dist.barrier()
 
-    C3, C4 = args.config == "c3", args.config == "c4"
-    cfg = amodem.preset("standard", "QAM16" if C3 else "QPSK", 1)
+    C3, C4, C5 = args.config == "c3", args.config == "c4", args.config == "c5"
+    if args.stream_chunks < 0:
+        args.stream_chunks = 2000 if args.config == "c2" else 0
+    cfg = amodem.preset("acoustic", "BPSK", 3) if C5 else amodem.preset("standard", "QAM16" if C3 else "QPSK", 1)
     F = args.frames if args.frames > 0 else (100000 if C3 else (32000 if C4 else 10000))
     dm = amodem.Demodulator(local)
     # ---- synthetic input, built on the GPU by k_tx (the reference transmitter, bit-exact)
@@ -95,9 +100,11 @@ def main():
         po = np.concatenate([[0], np.cumsum(pl)[:-1]]).astype(np.int64)
         pk = np.frombuffer(b"".join(pkts), np.uint8).copy()
     else:
-        spf = SAMPLES_PER_FRAME_C3 if C3 else SAMPLES_PER_FRAME
-        pk, po, pl = amodem.synth_legacy_packets(F, PAYLOAD, "f.bin", first=rank * F)
+        plen = PAYLOAD_C5 if C5 else PAYLOAD
+        pk, po, pl = amodem.synth_legacy_packets(F, plen, "f.bin", first=rank * F)
         pre, post = amodem.tx_silence(cfg, L.TX_LEGACY)
+        spf = SAMPLES_PER_FRAME_C3 if C3 else (int(lib_frame_samples(amodem, L, cfg, int(pl[0]), pre, post)) if C5
+                                               else SAMPLES_PER_FRAME)
     offs = (np.arange(F, dtype=np.int64) * spf)
     lens = np.full(F, spf, np.int32)
     nsamples = int(lens.sum())
@@ -107,7 +114,7 @@ def main():
     doffs = offs + pre if C4 else offs
     dlens = np.full(F, win, np.int32) if C4 else lens
     ndecoded = int(dlens.sum())
-    payload_bytes = CHUNK if C4 else PAYLOAD
+    payload_bytes = CHUNK if C4 else (PAYLOAD_C5 if C5 else PAYLOAD)
     xs = torch.empty(nsamples + 16, dtype=torch.float32, device=dev)
     d_pk = torch.from_numpy(pk).to(dev)
     d_po, d_pl = torch.from_numpy(po).to(dev), torch.from_numpy(pl).to(dev)
@@ -136,6 +143,15 @@ def main():
         tx_ms.append(e0.elapsed_time(e1))
     torch.cuda.synchronize(dev)
     tx_avg_ms = sum(tx_ms) / len(tx_ms)
+    sigma = None
+    if C5:  # AWGN on the GPU, seeded per rank; power from the first frame's active samples
+        x0 = xs[: int(lens[0])]
+        act = x0[x0 != 0]
+        sigma = float(torch.sqrt((act.double() ** 2).mean() / 10 ** (args.snr / 10)).item())
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(0xC5 + rank)
+        xs[:nsamples] += torch.randn(nsamples, generator=gen, device=dev, dtype=torch.float32) * sigma
+        torch.cuda.synchronize(dev)
     stride = amodem.payload_stride(cfg, int(dlens.max()))
     d_res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
     d_pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
@@ -153,9 +169,16 @@ def main():
     rec = np.frombuffer(d_res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
     ok = int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum())
     fallback = int((rec["flags"] != 0).sum())
+    fallback_flags = {}
+    for fl in rec["flags"][rec["flags"] != 0]:
+        for b in range(16):
+            if int(fl) & (1 << b) and b != 15:
+                fallback_flags[FLAG_NAMES.get(b, str(b))] = fallback_flags.get(FLAG_NAMES.get(b, str(b)), 0) + 1
     pay = d_pay.view(F, stride).cpu().numpy()
     for i in range(0, F, max(1, F // 16)):
         r = amodem.to_reference(rec[i], pay[i].tobytes(), not C4)
+        if C5 and not r.get("crcValid"):
+            continue  # noisy frames: checked against the oracle in the cpu_baseline leg
         assert r.get("data") == amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), payload_bytes), (i, r.get("error"))
         if C4:
             assert r.get("seqNum") == rank * F + i, (i, r.get("seqNum"))
@@ -211,8 +234,9 @@ def main():
         spf_dec = int(dlens[0])
         if dom == 0:
             dom_bytes = algo_bytes
-        else:
-            nsym_dec = (spf_dec // 576 - 3) if C4 else (21 if not C3 else 11)
+        else:  # CE + the symbols holding the packet (trailing silence skipped)
+            per_sym = amodem.num_data_subs(cfg) * {0: 1, 1: 2, 2: 4}[cfg.modulation]
+            nsym_dec = -(-int(pl[0]) * 8 * cfg.repetition // per_sym)
             dom_bytes = 4.0 * 512 * (nsym_dec + 1) * F
         achieved = dom_bytes / (stage_ms[dom] / 1e3) / 1e9
         traffic = None
@@ -222,17 +246,19 @@ def main():
                 tj = json.load(f)
             if tj.get("frames") == F and tj.get("samples_per_frame") == spf:
                 traffic = tj.get("hbm_bytes_per_launch")
-        mod = "QAM16" if C3 else "QPSK"
-        name = "C3" if C3 else ("C4" if C4 else "C2")
+        mod = "QAM16" if C3 else ("BPSK" if C5 else "QPSK")
+        name = "C3" if C3 else ("C4" if C4 else ("C5" if C5 else "C2"))
         cpu, tx_cpu, d2h = None, None, None
         if args.cpu_frames >= 0:
             # the CPU legs need the samples on the host: copy back the sample's frames
-            ncpu = args.cpu_frames if args.cpu_frames > 0 else min(F, 1000 * min(16, os.cpu_count() or 1))
+            per_thread = 100 if C5 else 1000
+            ncpu = args.cpu_frames if args.cpu_frames > 0 else min(F, per_thread * min(16, os.cpu_count() or 1))
             t0 = time.perf_counter()
             xh = xs[: ncpu * spf].cpu().numpy()
             d2h = 4.0 * ncpu * spf / (time.perf_counter() - t0) / 1e9
-            cpu = cpu_baseline(xh, doffs[:ncpu], dlens[:ncpu], mod, name, chunk=C4, payload=payload_bytes)
-            tx_cpu = None if C4 else tx_cpu_baseline(amodem, cfg, min(ncpu, 4000), spf)
+            cpu = cpu_baseline(xh, doffs[:ncpu], dlens[:ncpu], mod, name, chunk=C4, payload=payload_bytes,
+                               preset="acoustic" if C5 else "standard", rep=cfg.repetition, gpu_rec=rec[:ncpu])
+            tx_cpu = None if C4 else tx_cpu_baseline(amodem, cfg, min(ncpu, 4000), spf, payload_bytes)
         tx_bytes = 4.0 * nsamples + float(pl.sum())  # samples written + packet bytes read
         out = {
             "metric": METRIC,
@@ -249,14 +275,19 @@ def main():
             "data": "synthetic (reference-equivalent TX, xorshift32 payloads)",
             "config": {"workload": ("C4: 32k QPSK 2 KB data-chunk windows per GPU (decodeChunkFrame; value counts "
                                     "the window samples decoded, 25,344 of each 28,431-sample frame)" if C4 else
-                                    ("C3: 100k-frame 16-QAM batch demod per GPU" if C3 else
-                                     "C2: 10k-frame QPSK batch demod per GPU") +
-                                    " (decodeReceivedSignal, legacy 1 KB frames)"),
+                                    ("C5: 10k acoustic BPSK rep3 256 B legacy frames per GPU + AWGN at %.0f dB "
+                                     "(decodeReceivedSignal, hard majority vote = reference behaviour)" % args.snr
+                                     if C5 else
+                                     ("C3: 100k-frame 16-QAM batch demod per GPU" if C3 else
+                                      "C2: 10k-frame QPSK batch demod per GPU") +
+                                     " (decodeReceivedSignal, legacy 1 KB frames)")),
                        "frames_per_gpu": F, "samples_per_frame": int(dlens[0]), "fft": 512,
                        "modulation": mod, "payload_bytes": payload_bytes, "parallelism": f"frame-sharded x{world}"},
             "payload_MB_per_s": payload_mbps,
             "frames_ok": ok,
             "frames_exact_fallback": fallback,
+            "fallback_flags": fallback_flags,
+            "awgn_sigma": sigma,
             "d2h_GBps": d2h,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -269,6 +300,8 @@ def main():
                       "kernels_ms_avg": dict(zip(names + ["k_decode_exact"], stage_ms)),
                       "symbols_demodulated_per_frame": "header..CRC symbols only (C2: 21 of 36; trailing "
                                                        "silence skipped, SURVEY.md 8d)" if not C4 else "all"},
+            "soft_combine": soft_leg(amodem, L, dm, cfg, mode, xs, d_doff, d_dlen, F, d_res, d_pay, stride, stream,
+                                     rec) if (C5 and args.soft) else None,
             "cpu_baseline": cpu,
             "scan_roofline": None if scan is None else {
                 "phase": "stream pass + Schmidl-Cox coarse search ("
@@ -289,6 +322,33 @@ def main():
     dm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+FLAG_NAMES = {0: "FORCED", 1: "NONFINITE", 2: "BIG", 3: "COARSE", 4: "FINE", 5: "CHANNEL", 6: "PHASE", 7: "DEMAP",
+              8: "THRESH", 9: "SPAN", 10: "SOFT"}
+PAYLOAD_C5 = 256
+
+
+def lib_frame_samples(amodem, L, cfg, pkt_len, pre, post):
+    import ctypes as C
+    return L.load().amod_tx_frame_samples(C.byref(cfg), pkt_len, pre, post)
+
+
+def soft_leg(amodem, L, dm, cfg, mode, xs, d_off, d_len, F, d_res, d_pay, stride, stream, hard_rec):
+    """C5's opt-in soft combining of the repeated bits (AMOD_OPT_SOFT_COMBINE, NOT reference
+    behaviour: the exact kernel demodulates after the fast detection), one timed pass."""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dm.decode_device(cfg, mode, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F, d_res.data_ptr(),
+                     d_pay.data_ptr(), stride, stream=stream, options=L.OPT_SOFT_COMBINE)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    rec = np.frombuffer(d_res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
+    ok_soft = int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum())
+    ok_hard = int(((hard_rec["status"] == 0) & (hard_rec["crc_valid"] == 1)).sum())
+    return {"what": "AMOD_OPT_SOFT_COMBINE (|H|^2-weighted soft vote; not reference behaviour)", "ms": t * 1e3,
+            "frames_crc_valid_soft": ok_soft, "frames_crc_valid_hard": ok_hard}
 
 
 def e2e_leg(torch, dm, cfg, mode, xs, nsamples, d_off, d_len, F, d_res, d_pay, stride, dev, ndecoded, payload_bytes,
@@ -412,7 +472,7 @@ def stream_leg(amodem, L, device, nchunks=2000, chunk=2048):
             "reference_rate_note": "reference StreamingReceiver: 2.0e6 samples/s per core (SURVEY.md section 3.2)"}
 
 
-def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
+def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD, preset="standard", rep=1, gpu_rec=None):
     """The C restatement of the reference RX (oracle/, kind 'port') on this host's cores
     over a bounded sample of the same frames: all cores (16 threads, repeated to ~1 s of
     wall time, ~16 s of CPU work) and one core (~2 s). profiles/cpu_calibration.json
@@ -421,23 +481,29 @@ def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
     rates reported beside the port's own."""
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
-    c = O.cfg("standard")
+    c = O.cfg(preset)
     t, reps = 0.0, 0
+    agree = None
     while t < 1.0 and reps < 8:
-        dt, st, _ = O.bench_decode(c, x, offs, lens, mod, 1, threads, chunk=chunk)
-        assert (st == 0).all()
+        dt, st, crc = O.bench_decode(c, x, offs, lens, mod, rep, threads, chunk=chunk)
+        if gpu_rec is None:
+            assert (st == 0).all()
+        else:  # noisy frames: the GPU's outcomes must be the reference's (the oracle's)
+            agree = int(((gpu_rec["status"] == st) & ((st != 0) | (gpu_rec["actual_crc"] == crc))).sum())
         t += dt
         reps += 1
     samples = float(lens.sum()) * reps
-    n1 = min(len(offs), 1000)  # one core: ~2 s
-    t1, st, _ = O.bench_decode(c, x, offs[:n1], lens[:n1], mod, 1, 1, chunk=chunk)
-    assert (st == 0).all()
+    n1 = min(len(offs), 1000 if rep == 1 else 160)  # one core: ~2 s
+    t1, st, _ = O.bench_decode(c, x, offs[:n1], lens[:n1], mod, rep, 1, chunk=chunk)
+    assert gpu_rec is not None or (st == 0).all()
     single = float(lens[:n1].sum()) / t1
     out = {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
            "sample": f"{len(offs)} {name} frames x {reps} passes ({int(samples)} samples) on {threads} threads; "
                      f"{n1} frames on 1 thread; oracle/amodem_oracle.c{' (decodeChunkFrame)' if chunk else ''}",
            "payload_MB_per_s": payload * len(offs) * reps / t / 1e6, "seconds": t + t1,
            "single_core": single}
+    if agree is not None:
+        out["oracle_agree"] = f"{agree}/{len(offs)} frames: GPU status and CRC equal the C oracle's"
     cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     key = {"C2": "c2", "C3": "c3", "C4": "c4", "C5": "c5"}.get(name)
     if os.path.exists(cal) and key:
@@ -450,13 +516,13 @@ def cpu_baseline(x, offs, lens, mod, name, chunk=False, payload=PAYLOAD):
     return out
 
 
-def tx_cpu_baseline(amodem, cfg, nframes, spf):
+def tx_cpu_baseline(amodem, cfg, nframes, spf, payload=PAYLOAD):
     """The host C++ builders (libamodem's amod_synth_legacy_batch, the same arithmetic
     as the reference TX) on this host's cores over nframes frames."""
     threads = min(16, os.cpu_count() or 1)
     out = np.empty(nframes * spf, np.float32)
     t0 = time.perf_counter()
-    amodem.synth_legacy_batch(cfg, nframes, payload_len=PAYLOAD, name="f.bin", threads=threads, out=out)
+    amodem.synth_legacy_batch(cfg, nframes, payload_len=payload, name="f.bin", threads=threads, out=out)
     t = time.perf_counter() - t0
     return {"value": nframes * spf / t, "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"{nframes} frames, libamodem host builders, {threads} threads", "seconds": t}

@@ -89,6 +89,8 @@ extern "C" {
 #define AMOD_FLAG_THRESH (1 << 8)    /* preprocess peak near the 1e-6 threshold     */
 #define AMOD_FLAG_SPAN (1 << 9)      /* the parse reads bytes past the symbols the fast
                                         path demodulated (signal energy ended early)   */
+#define AMOD_FLAG_SOFT (1 << 10)     /* AMOD_OPT_SOFT_COMBINE: demodulated by the exact
+                                        kernel after the fast path's detection         */
 #define AMOD_FLAG_EXACT (1 << 15)    /* result produced by the exact-replica kernel */
 
 /* OFDM parameters + modulation; mirrors OFDM (modem.js:69-98) */

@@ -98,8 +98,9 @@ def _debug_decode(dm, case, x, options):
 
 
 DEBUG_CASES = [c for c in frames() if "sym0" in c["inter"]]
-# flags raised by k_demod (demodulation stage): DEMAP, PHASE, CHANNEL, SPAN
-DEMOD_FLAGS = (1 << 7) | (1 << 6) | (1 << 5) | (1 << 9)
+# flags raised after detection (k_demod's demodulation-stage guards: DEMAP, PHASE,
+# CHANNEL, SPAN; opt-in SOFT)
+DEMOD_FLAGS = (1 << 7) | (1 << 6) | (1 << 5) | (1 << 9) | (1 << 10)
 
 
 @pytest.mark.parametrize("exact", [False, True], ids=["fast", "exact"])
@@ -139,7 +140,13 @@ def test_intermediates(dm, case, exact):
         assert np.abs(h - href).max() <= ABS_TOL * scale
         assert np.abs(x0 - x0ref).max() <= ABS_TOL * scale
         assert np.abs(eq - eqref).max() <= ABS_TOL
-        assert np.abs(ph - phref).max() <= ABS_TOL
+        # phase = mean over the pilots of eqIm/eqRe (modem.js:398-405): a pilot near
+        # the imaginary axis (ratio r) amplifies an fp32 equaliser error eps by ~(1 + r^2);
+        # |r| of the worst pilot is at most npilots * |phase| when the others are small
+        npil = O.cfg(case["config"]).npilots
+        tol = ABS_TOL * (1.0 + (npil * np.abs(phref)) ** 2)
+        bad = np.nonzero(np.abs(ph - phref) > tol)[0]
+        assert bad.size == 0, [(int(i), float(ph[i]), float(phref[i])) for i in bad[:4]]
         if case["rx"] == "legacy":
             # mean from fp32 block sums of x - x[0]: within 1e-6 of the peak
             assert abs(d.mean - inter["mean"]) <= 1e-6 * inter["mx"]
