@@ -83,7 +83,9 @@ struct DetRec {
   int32_t coarse;  // Schmidl-Cox index (in the plateau)
   float A, B;      // normalisation y = A x + B (preprocessSignal)
   float fbest;     // best fine metric
-  float pad[3];
+  int32_t sc_lo, sc_hi; // listed frames: positions that can hold detectPreamble's argmax
+                        // (every other position's metric is proven lower), or -1
+  float pad;
 };
 static_assert(sizeof(DetRec) == 48, "DetRec layout");
 

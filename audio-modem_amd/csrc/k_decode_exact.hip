@@ -4,7 +4,9 @@
 // with -ffp-contract=off; fp64 add/mul/div/sqrt are correctly rounded), so every
 // intermediate equals the reference bit for bit:
 //   mean        sequential sum (preprocessSignal 215-217), one lane over LDS chunks
-//   Schmidl-Cox sequential sliding recurrence (detectPreamble 292-316), one lane
+//   Schmidl-Cox sliding recurrence (detectPreamble 292-316): the per-position
+//               increments and the metrics are independent of the running sums, so all
+//               lanes compute them; one lane runs only the three sequential additions
 //   fine timing one lane per candidate offset, sequential 576-tap sums (576-587)
 //   FFT         radix-2 DIT stages with the reference's per-stage twiddle
 //               recurrence tabulated on the host (fftIterative 26-47); each stage's
@@ -21,11 +23,18 @@ namespace {
 constexpr int XT = 256;     // threads per workgroup
 constexpr int CH = 4096;    // sample chunk staged in LDS for the sequential lanes
 
+constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH doubles overlay the FFT arrays)
+
 struct alignas(16) XSmem {
   float chunk[CH + 520];
-  double re[kFft], im[kFft];
-  double hr[kFft], hi[kFft];
-  double er[kFft], ei[kFft];
+  union {
+    struct {
+      double re[kFft], im[kFft];
+      double hr[kFft], hi[kFft];
+      double er[kFft], ei[kFft];
+    };
+    double sc[3 * SCH]; // detectPreamble: per-position increments, then states (p, ra, rb)
+  };
   double rd[XT / 64 + 4];
   float rf[XT / 64];
   int ri[XT / 64 + 4];
@@ -63,6 +72,20 @@ __device__ __forceinline__ void wg_global_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// fn(i, p[i]) for this thread's strided indices i = tid + k XT < N, in ascending order,
+// eight loads in flight per thread (one workgroup streams a whole frame)
+template <typename F> __device__ __forceinline__ void strided8(const float *__restrict__ p, int N, F &&fn) {
+  int i = threadIdx.x;
+  for (; i + 7 * XT < N; i += 8 * XT) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[i + u * XT];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fn(i + u * XT, v[u]);
+  }
+  for (; i < N; i += XT) fn(i, p[i]);
 }
 
 __device__ __forceinline__ double js_max(double a, double b) { // Math.max, NaN-propagating
@@ -120,9 +143,18 @@ __device__ int crosscorr_detect(const float *xs, int N, const DevCfg &cfg, XSmem
   return best > 0.15 ? best_idx : -1;
 }
 
+// diagnostics only (AMOD_STAMPS): shader-clock marks 8-14 of an exact frame
+#define XSTAMP(k)                                                                        \
+  do {                                                                                  \
+    if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const DevWork w) {
   __shared__ XSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // listed frames are latency-bound chains (sequential recurrences) that run beside the
+  // throughput-bound k_demod: their waves issue first on a shared SIMD
+  __builtin_amdgcn_s_setprio(3);
   const int count = *w.fb_count;
   const int SYM = cfg.sym, CP = cfg.cp;
   for (int item = blockIdx.x; item < count; item += gridDim.x) {
@@ -136,6 +168,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     amod_result r;
     init_result(r);
     r.flags = flags0 | AMOD_FLAG_EXACT;
+    XSTAMP(8);
     {
       const int64_t need_bits = (int64_t)(N / SYM) * cfg.ndata * cfg.bps;
       if ((int64_t)N > w.xs_stride || 2 * ((need_bits + 31) / 32) + 16 > w.bits_stride) {
@@ -163,14 +196,13 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       // with non-finite samples) the sum runs sequentially.
       double ps = 0.0, pa = 0.0;
       int emin = 1 << 20, nonfin = 0;
-      for (int i = tid; i < N; i += XT) {
-        const float x = xr[i];
+      strided8(xr, N, [&](int, float x) {
         ps += (double)x;
         pa += fabs((double)x);
         const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
         if (e == 0xFFu) nonfin = 1;
         else if (x != 0.0f) emin = min(emin, e == 0 ? -149 : (int)e - 150);
-      }
+      });
       for (int o = 32; o > 0; o >>= 1) {
         ps += __shfl_xor(ps, o, 64);
         pa += __shfl_xor(pa, o, 64);
@@ -185,7 +217,8 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         double S = 0.0, PA = 0.0;
         int EM = 1 << 20, NF = 0;
         for (int i = 0; i < XT / 64; ++i) { S += sm.rd[i]; PA += sm.er[i]; EM = min(EM, sm.ri[i]); NF |= sm.ri[XT / 64 + i]; }
-        exact_par = !NF && (EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53));
+        // non-finite samples: NaN, or +-Inf, whatever the order (finite sums stay finite)
+        exact_par = NF || EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53);
         sm.mean = S / (double)N;
         sm.status = exact_par;
       }
@@ -193,24 +226,105 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       exact_par = sm.status != 0;
       __syncthreads();
       if (!exact_par) {
-        double sum = 0.0;
-        for (int c0 = 0; c0 < N; c0 += CH) {
-          const int n = min(CH, N - c0);
-          for (int i = tid; i < n; i += XT) sm.chunk[i] = xr[c0 + i];
-          __syncthreads();
-          if (tid == 0) for (int i = 0; i < n; ++i) sum += (double)sm.chunk[i];
-          __syncthreads();
+        // Segments of G samples, certified one by one along the sequential order. A
+        // segment whose sum|x| < 2^(em + 53) (em: its smallest sample ulp exponent) has
+        // exact internal sums in any order, so its total and the extremes pmax / pmin of
+        // its sequential prefix sums P_j come out exact from a parallel scan. With S the
+        // running (sequential) sum at its start and q the smaller of em and the exponent
+        // of S's lowest set bit, every partial sum S + P_j is a multiple of 2^q inside
+        // [S + pmin, S + pmax]; below 2^(q + 53) in magnitude none of them rounds and S +
+        // total is the sequential result. A segment failing either test (a sample far
+        // below the running sum's ulp, or a partial sum that could round) is summed
+        // sample by sample.
+        constexpr int SEGCAP = 3 * SCH / 5;
+        double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_hi = sm.sc + 2 * SEGCAP,
+                     *const seg_lo = sm.sc + 3 * SEGCAP, *const seg_e = sm.sc + 4 * SEGCAP;
+        const int G = 256 * max(1, (N + 256 * SEGCAP - 1) / (256 * SEGCAP));
+        const int nseg = (N + G - 1) / G;
+        constexpr int NW = XT / 64;
+        for (int sg0 = wave; sg0 < nseg; sg0 += 4 * NW) {
+          float v[4][4]; // four segments' first 256 samples in flight at once
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int sg = sg0 + g * NW, i = sg * G + lane + 64 * u;
+              v[g][u] = sg < nseg && i < min(N, (sg + 1) * G) ? xr[i] : 0.f;
+            }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int sg = sg0 + g * NW;
+            if (sg >= nseg) break; // wave-uniform
+            double carry = 0.0, sa = 0.0, pmax = 0.0, pmin = 0.0;
+            int em = 1 << 20;
+            const int e1 = min(N, (sg + 1) * G);
+            for (int r = 0; sg * G + 64 * r < e1; ++r) { // rows of 64 samples, in order
+              const int i = sg * G + 64 * r + lane;
+              const float x = r < 4 ? v[g][r] : (i < e1 ? xr[i] : 0.f);
+              sa += fabs((double)x);
+              const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
+              if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
+              double c = (double)x; // inclusive scan over the row
+#pragma unroll
+              for (int o = 1; o < 64; o <<= 1) {
+                const double t = __shfl_up(c, o, 64);
+                if (lane >= o) c += t;
+              }
+              const double P = carry + c;
+              pmax = fmax(pmax, P);
+              pmin = fmin(pmin, P);
+              carry += __shfl(c, 63, 64);
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+              sa += __shfl_xor(sa, o, 64);
+              pmax = fmax(pmax, __shfl_xor(pmax, o, 64));
+              pmin = fmin(pmin, __shfl_xor(pmin, o, 64));
+              em = min(em, __shfl_xor(em, o, 64));
+            }
+            if (lane == 0) {
+              seg_s[sg] = carry; seg_a[sg] = sa; seg_hi[sg] = pmax; seg_lo[sg] = pmin; seg_e[sg] = (double)em;
+            }
+          }
         }
-        if (tid == 0) sm.mean = sum / (double)N;
+        __syncthreads();
+        if (wave == 0) { // the chain along the segments: wave-uniform S on every lane
+          double S = 0.0;
+          for (int sg = 0; sg < nseg; ++sg) {
+            const int em = (int)seg_e[sg];
+            if (em >= (1 << 19)) continue; // all zeros
+            // S is a multiple of 2^(exponent of its lowest set bit)
+            int qs = 1 << 20;
+            if (S != 0.0) {
+              const uint64_t b = (uint64_t)__double_as_longlong(S);
+              const int be = (int)((b >> 52) & 0x7FF);
+              const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (be ? (1ull << 52) : 0ull);
+              qs = (be ? be : 1) - 1075 + __builtin_ctzll(m);
+            }
+            const int q = min(em, qs);
+            const bool inner = seg_a[sg] * (1.0 + 0x1p-40) < ldexp(1.0, em + 53);
+            const double reach = fmax(fabs(S + seg_hi[sg]), fabs(S + seg_lo[sg])) * (1.0 + 0x1p-50);
+            if (inner && reach < ldexp(1.0, q + 53)) {
+              S += seg_s[sg];
+            } else { // sample by sample: 64 coalesced loads, then lane by lane in order
+              const int e1 = min(N, (sg + 1) * G);
+              for (int b0 = sg * G; b0 < e1; b0 += 64) {
+                const float v = b0 + lane < e1 ? xr[b0 + lane] : 0.f;
+                const int nj = min(64, e1 - b0);
+                for (int j = 0; j < nj; ++j) S += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+              }
+            }
+          }
+          if (lane == 0) sm.mean = S / (double)N;
+        }
       }
       __syncthreads();
       const double mean = sm.mean;
       double mx = 0.0;
-      for (int i = tid; i < N; i += XT) {
-        const float o = (float)((double)xr[i] - mean);
+      strided8(xr, N, [&](int i, float x) {
+        const float o = (float)((double)x - mean);
         xs[i] = o;
         mx = js_max(mx, fabs((double)o));
-      }
+      });
       for (int o = 32; o > 0; o >>= 1) mx = js_max(mx, __shfl_xor(mx, o, 64));
       if (lane == 0) sm.rd[wave] = mx;
       __syncthreads();
@@ -222,10 +336,12 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       }
       __syncthreads();
       mx = sm.mx;
-      if (mx > 1e-6)
-        for (int i = tid; i < N; i += XT) xs[i] = (float)((double)xs[i] / mx);
+      if (mx > 1e-6) {
+        strided8(xs, N, [&](int i, float o) { xs[i] = (float)((double)o / mx); }); // own indices only
+      }
       wg_global_sync();
       sig = xs;
+      XSTAMP(9);
 
       // ---- detectPreamble: sequential recurrence, one lane
       const int half = kFft / 2;
@@ -238,41 +354,113 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         r.fine_metric = dr.fbest;
         r.preamble_idx = start = dr.start;
       } else if (N >= 2 * half) {
+        // chunk of positions [c0, c0 + n): (1) every lane forms the increments
+        // fl(fl(mid bIn) - fl(aOut mid)) etc. of the updates at those positions, (2) lane 0
+        // replaces each increment by the running state at that position and adds it (the
+        // only sequential step: three independent fp64 additions), (3) every lane forms
+        // the metric p^2 / (ra rb) of its positions, first strict maximum per lane;
+        // lanes then combine by (metric, lowest index) = the reference's first maximum
         const int end = N - 2 * half;
-        double p = 0.0, ra = 0.0, rb = 0.0;
-        for (int c0 = 0; c0 <= end; c0 += CH) {
-          const int n = min(CH + 2 * half + 1, N - c0);
-          for (int i = tid; i < n; i += XT) sm.chunk[i] = xs[c0 + i];
+        // a frame the coarse stage listed with a proven hull [sc_lo, sc_hi] of the argmax:
+        // the recurrence runs to sc_hi, metrics are compared there only
+        int d_lo = 0, d_hi = end;
+        if (w.det && cfg.mode == AMOD_MODE_RECEIVED && !loop) {
+          const DetRec dr = w.det[f];
+          if (dr.sc_lo >= 0 && dr.sc_hi >= dr.sc_lo) { d_lo = dr.sc_lo; d_hi = min(dr.sc_hi, end); }
+        }
+        // lanes 0, 1, 2 carry the three independent recurrences p, ra, rb (each lane its
+        // own array of increments -> states), so one instruction stream advances all three
+        double acc = 0.0;
+        double bm = 0.0;                     // > best = 0 like the reference's first test
+        int bi = -1;
+        double *const tp = sm.sc, *const tra = sm.sc + SCH, *const trb = sm.sc + 2 * SCH;
+        for (int c0 = 0; c0 <= d_hi; c0 += SCH) {
+          const int n = min(SCH, d_hi + 1 - c0);
+          const int ns = n + 2 * half; // samples [c0, c0 + n + 512) <= N
+          for (int i = tid; i < ns; i += XT) sm.chunk[i] = c0 + i < N ? xs[c0 + i] : 0.f;
           __syncthreads();
-          if (tid == 0) {
-            if (c0 == 0) {
-              for (int m = 0; m < half; ++m) {
-                const double a = sm.chunk[m], b = sm.chunk[m + half];
-                p += a * b; ra += a * a; rb += b * b;
+          if (c0 == 0 && tid < 3) { // P(0), Ra(0), Rb(0) (modem.js:292-298), one sum per lane
+            for (int m = 0; m < half; ++m) {
+              const double a = sm.chunk[m], b = sm.chunk[m + half];
+              acc += tid == 0 ? a * b : (tid == 1 ? a * a : b * b);
+            }
+          }
+          for (int k = tid; k < n; k += XT) {
+            double ip = 0.0, ia = 0.0, ib = 0.0;
+            if (c0 + k < end) {
+              const double a_out = sm.chunk[k], mid = sm.chunk[k + half], b_in = sm.chunk[k + 2 * half];
+              ip = mid * b_in - a_out * mid;
+              ia = mid * mid - a_out * a_out;
+              ib = b_in * b_in - mid * mid;
+            }
+            tp[k] = ip; tra[k] = ia; trb[k] = ib;
+          }
+          __syncthreads();
+          const bool keep = c0 + n > d_lo; // some position of this chunk is compared
+          if (tid < 3) {
+            double2 *const v = reinterpret_cast<double2 *>(sm.sc + tid * SCH);
+            int k = 0;
+            if (!keep) { // states not needed: the running sum only
+              for (; k + 8 <= n; k += 8) {
+                double2 t[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t[j] = v[(k >> 1) + j];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { acc += t[j].x; acc += t[j].y; }
+              }
+            } else {
+              for (; k + 8 <= n; k += 8) {
+                double2 t[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t[j] = v[(k >> 1) + j];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { // state at the position, then its update
+                  const double s0 = acc;
+                  acc += t[j].x; // zero past `end`: adding +0.0 changes nothing
+                  const double s1 = acc;
+                  acc += t[j].y;
+                  v[(k >> 1) + j] = make_double2(s0, s1);
+                }
               }
             }
-            const int dlast = min(c0 + CH - 1, end);
-            for (int d = c0; d <= dlast; ++d) {
-              if (ra > 0.01 && rb > 0.01) {
-                const double metric = (p * p) / (ra * rb);
-                if (metric > best) { best = metric; coarse = d; }
-              }
-              if (d < end) {
-                const int k = d - c0;
-                const double a_out = sm.chunk[k], mid = sm.chunk[k + half], b_in = sm.chunk[k + 2 * half];
-                p += mid * b_in - a_out * mid;
-                ra += mid * mid - a_out * a_out;
-                rb += b_in * b_in - mid * mid;
-              }
+            double *const vs = sm.sc + tid * SCH;
+            for (; k < n; ++k) {
+              const double t = vs[k];
+              vs[k] = acc;
+              acc += t;
             }
           }
           __syncthreads();
+          for (int k = tid; keep && k < n; k += XT) {
+            if (c0 + k < d_lo) continue;
+            const double pp = tp[k], a = tra[k], b = trb[k];
+            if (a > 0.01 && b > 0.01) {
+              const double metric = (pp * pp) / (a * b);
+              if (metric > bm) { bm = metric; bi = c0 + k; }
+            }
+          }
+          __syncthreads();
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const double om = __shfl_xor(bm, o, 64);
+          const int oi = __shfl_xor(bi, o, 64);
+          if (om > bm || (om == bm && oi >= 0 && (bi < 0 || oi < bi))) { bm = om; bi = oi; }
+        }
+        if (lane == 0) { sm.rd[wave] = bm; sm.ri[wave] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+          best = 0.0; coarse = -1;
+          for (int i = 0; i < XT / 64; ++i)
+            if (sm.rd[i] > best || (sm.rd[i] == best && sm.ri[i] >= 0 && (coarse < 0 || sm.ri[i] < coarse))) {
+              best = sm.rd[i]; coarse = sm.ri[i];
+            }
         }
         if (tid == 0) { sm.best = best; sm.coarse = best > 0.5 ? coarse : -1; }
       } else if (tid == 0) {
         sm.best = 0.0; sm.coarse = -1;
       }
       __syncthreads();
+      XSTAMP(10);
       if (!demod_only) {
       coarse = sm.coarse;
       if (loop && coarse < 0) coarse = crosscorr_detect(xs, N, cfg, sm); // modem.js:982-985
@@ -342,6 +530,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       continue;
     }
 
+    XSTAMP(11);
     // ---- channel estimate (estimateChannel, modem.js:421-440)
     const int ce0 = start + 2 * SYM, data0 = start + 3 * SYM;
     fft_exact(sig + ce0 + CP, sm, cfg.t.tw_exact);
@@ -439,6 +628,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       }
     }
     wg_global_sync();
+    XSTAMP(12);
     if (D && tid == 0) D->nsym = M;
     r.nbits = nbits;
     const uint32_t *v = bits;

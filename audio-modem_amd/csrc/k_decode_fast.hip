@@ -322,12 +322,17 @@ __device__ __forceinline__ int frame_route(const DevCfg &cfg, const DevWork &w, 
   return 0;
 }
 
-// append frame f to k_decode_exact's list (one thread)
-__device__ __forceinline__ void list_exact(const DevWork &w, int f, int flags) {
+// append frame f to k_decode_exact's list (one thread); [sc_lo, sc_hi]: the positions
+// that can hold detectPreamble's argmax when the coarse stage proved that (else -1)
+__device__ __forceinline__ void list_exact(const DevWork &w, int f, int flags, int sc_lo = -1, int sc_hi = -1) {
   const int i = atomicAdd(w.fb_count, 1);
   w.fb_list[i] = f;
   w.fb_flags[i] = flags;
-  if (w.det) w.det[f].route = ROUTE_EXACT;
+  if (w.det) {
+    w.det[f].sc_lo = sc_lo;
+    w.det[f].sc_hi = sc_hi;
+    w.det[f].route = ROUTE_EXACT;
+  }
 }
 
 // scalar (SMEM) load of a wave-uniform record: waits on lgkmcnt, not behind vector loads
@@ -1085,7 +1090,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
     }
     DetRec d;
     d.route = ROUTE_DEMOD; d.flags = 0; d.start = start; d.M = M; d.T = T; d.coarse = sm.coarse;
-    d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
+    d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
     w.det[f] = d;
     // opt-in soft combining (not reference behaviour): the exact kernel demodulates
     if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
@@ -1106,7 +1111,13 @@ finish_error:
   return;
 
 to_exact:
-  if (tid == 0) list_exact(w, f, sm.flags);
+  // past the coarse stage, [clo, chi] holds every position whose metric can reach the
+  // best (the others' upper bounds are below its lower bound): the exact replica's
+  // recurrence stops at chi and compares metrics only there
+  if (tid == 0) {
+    const bool hull = sm.clo >= 0 && sm.chi >= sm.clo;
+    list_exact(w, f, sm.flags, hull ? sm.clo : -1, hull ? sm.chi : -1);
+  }
 }
 
 // ------------------------------------------------------------ detection kernels
@@ -1146,7 +1157,7 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
   }
   DetRec d;
   d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = d.M; d.coarse = -1;
-  d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.pad[0] = d.pad[1] = d.pad[2] = 0.f;
+  d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
   w.det[f] = d;
   if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
 }

@@ -432,13 +432,13 @@ int ensure_chain(amod_ctx *ctx, int32_t nframes) {
 
 int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
   if (max_len < 0) { // device path: keep what amod_reserve set up, or size from a default
-    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 2 * (size_t)std::max(nframes, 1))));
+    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 4 * (size_t)std::max(nframes, 1))));
     if (ctx->nslots > 0) return AMOD_SUCCESS;
     max_len = 65536;
   }
   const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
       std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
-  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 2 * (size_t)std::max(nframes, 1))));
+  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 4 * (size_t)std::max(nframes, 1))));
   // grow-only: a later, smaller reservation never shrinks a stride or the slot count that
   // earlier (longer) frames were sized for
   const int64_t words = (max_bits_for(c, max_len) + 31) / 32;
@@ -479,6 +479,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.samples = samples; w.off = offsets; w.len = lengths; w.nframes = nframes;
   w.res = results; w.payload = payload; w.stride = payload_stride; w.dbg = debug;
   int32_t *fb = (int32_t *)ctx->fb.p;
+  // two exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod
   w.fb_count = fb; w.fb_list = fb + 64; w.fb_flags = fb + 64 + nframes;
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
@@ -540,31 +541,54 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (const char *oc = getenv("AMOD_CHUNKS")) nchunk = std::max(1, std::min(kMaxChunks, atoi(oc)));
   if (!demod || debug) nchunk = 1;
   nchunk = std::min(nchunk, std::max(1, nframes));
+  amod::DevWork wb = w; // every field as w, list B
+  wb.fb_count = fb + 1; wb.fb_list = fb + 64 + 2 * nframes; wb.fb_flags = fb + 64 + 3 * nframes;
+  if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  for (auto &e : ctx->chunk_ev)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const int xslots = std::min(ctx->nslots, nframes);
   HIP_TRY(mark(0));
   if (nchunk == 1) {
     w.f0 = 0; w.f1 = nframes;
     HIP_TRY(amod_launch_detect(d, w, s));
     HIP_TRY(mark(1));
-    if (demod) HIP_TRY(amod_launch_demod(d, w, demod_blocks(nframes), s));
+    if (demod) {
+      // list A is complete: the exact replica of the frames detection listed (long
+      // sequential recurrences) runs on the second stream, under k_demod
+      // (AMOD_EXACT_SERIAL, diagnostics: after it, on the same stream)
+      if (getenv("AMOD_EXACT_SERIAL")) {
+        wb.f0 = 0; wb.f1 = nframes;
+        HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
+        HIP_TRY(amod_launch_exact(d, w, xslots, s));
+      } else {
+      HIP_TRY(hipEventRecord(ctx->chunk_ev[0], s));
+      HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[0], 0));
+      HIP_TRY(amod_launch_exact(d, w, xslots, ctx->aux));
+      HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
+      wb.f0 = 0; wb.f1 = nframes;
+      HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
+      HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0)); // workspace slots are shared
+      }
+    } else {
+      HIP_TRY(amod_launch_exact(d, w, xslots, s));
+    }
   } else {
-    if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-    for (auto &e : ctx->chunk_ev)
-      if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int c = 0; c < nchunk; ++c) {
-      w.f0 = (int)((int64_t)nframes * c / nchunk);
-      w.f1 = (int)((int64_t)nframes * (c + 1) / nchunk);
+      w.f0 = wb.f0 = (int)((int64_t)nframes * c / nchunk);
+      w.f1 = wb.f1 = (int)((int64_t)nframes * (c + 1) / nchunk);
       HIP_TRY(amod_launch_detect(d, w, s));
       HIP_TRY(hipEventRecord(ctx->chunk_ev[c], s));
       HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[c], 0));
-      HIP_TRY(amod_launch_demod(d, w, demod_blocks(w.f1 - w.f0), ctx->aux));
+      HIP_TRY(amod_launch_demod(d, wb, demod_blocks(w.f1 - w.f0), ctx->aux));
     }
     HIP_TRY(mark(1)); // every k_detect done (on s)
     HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
     HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0));
+    HIP_TRY(amod_launch_exact(d, w, xslots, s));
   }
-  w.f0 = 0; w.f1 = nframes;
+  w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(2));
-  HIP_TRY(amod_launch_exact(d, w, std::min(ctx->nslots, nframes), s));
+  HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
   HIP_TRY(mark(3));
   if (ctx->profiling) ctx->ev_used.push_back(ev);
   return AMOD_SUCCESS;

@@ -174,6 +174,14 @@ def main():
         for b in range(16):
             if int(fl) & (1 << b) and b != 15:
                 fallback_flags[FLAG_NAMES.get(b, str(b))] = fallback_flags.get(FLAG_NAMES.get(b, str(b)), 0) + 1
+    if os.environ.get("AMOD_STAMPS"):  # diagnostics: exact-kernel phase marks of the listed frames
+        st = np.zeros(F * 32, dtype=np.uint64)
+        n = L.load().amod_debug_stamps(dm.ctx, st.ctypes.data, st.size)
+        st = st[:n].reshape(-1, 32).astype(np.int64)
+        for i in np.nonzero(rec["flags"] & L.FLAG_EXACT)[0][:32]:
+            print("listed", i, hex(int(rec["flags"][i])), int(rec["coarse_idx"][i]),
+                  [int(st[i, b] - st[i, a]) if st[i, a] and st[i, b] else None
+                   for a, b in ((8, 9), (9, 10), (10, 11), (11, 12))], file=sys.stderr)
     pay = d_pay.view(F, stride).cpu().numpy()
     for i in range(0, F, max(1, F // 16)):
         r = amodem.to_reference(rec[i], pay[i].tobytes(), not C4)

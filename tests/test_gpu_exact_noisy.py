@@ -1,0 +1,116 @@
+"""Exact-replica path under noise, against the C oracle (modem.js restated in fp64).
+
+The replica's two sequential recurrences are restructured for the GPU:
+- preprocessSignal's mean (modem.js:215-217): segments certified along the sequential
+  order (no partial sum inside them can round), the rest summed sample by sample;
+- detectPreamble (286-319): increments and metrics on every lane, only the three running
+  sums sequential, and, for a frame the coarse stage listed with a proven hull of the
+  argmax, the recurrence stops at the hull's end.
+Both must leave every result field bit-equal to the oracle's: status, coarse index
+(Schmidl-Cox argmax), preamble index, fine metric, bytes. Frames include samples far
+below the running sum's ulp (forcing the per-sample segments) and AWGN at 6-12 dB (where
+the fast path lists frames with ambiguous coarse decisions)."""
+import numpy as np
+import pytest
+
+from helpers import ref_dict, struct_to_dict
+
+import amodem
+from amodem import _lib as L
+from oracle import oracle as O
+
+
+def as_golden(d: dict) -> dict:
+    return {k: ({"hex": v.hex()} if isinstance(v, (bytes, bytearray)) else v) for k, v in d.items()}
+
+
+pytestmark = pytest.mark.gpu
+
+
+def _noisy_batch(preset, mod, rep, nframes, payload, snr_db, seed, tiny=False):
+    cfg = amodem.preset(preset, mod, rep)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, nframes, payload_len=payload, threads=8)
+    sp = float(np.mean(x[x != 0] ** 2))
+    rng = np.random.default_rng(seed)
+    x = (x + rng.standard_normal(len(x)).astype(np.float32) * np.float32(np.sqrt(sp / 10 ** (snr_db / 10)))).astype(np.float32)
+    if tiny:  # samples far below any running sum's ulp, at random places of every frame
+        for o, n in zip(offs, lens):
+            idx = o + rng.integers(0, n, 6)
+            x[idx] = np.array([1e-30, -3e-12, 7e-9, -2e-20, 1e-38, 5e-10], np.float32)
+    return cfg, x, offs, lens
+
+
+DEMOD_FLAGS = (1 << 7) | (1 << 6) | (1 << 5) | (1 << 9) | (1 << 10)
+
+
+def _check_against_oracle(cfg_name, mod, rep, x, offs, lens, rec, pay):
+    c = O.cfg(cfg_name)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        r, rp = O.decode(c, x[o:o + n], mod, rep, False)
+        fl = int(rec["flags"][i])
+        ref = ref_dict(struct_to_dict(r), rp.tobytes(), via_legacy=True)
+        got = as_golden(amodem.to_reference(rec[i], pay[i].tobytes(), via_legacy=True))
+        assert got == ref, (i, fl)
+        if fl & L.FLAG_EXACT and fl & ~(L.FLAG_EXACT | DEMOD_FLAGS):
+            # the replica's own Schmidl-Cox argmax and fine metric (demodulation-only
+            # frames keep the fast path's plateau index, pinned in test_gpu_parity)
+            assert int(rec["coarse_idx"][i]) == r.coarse_idx, (i, fl)
+            if r.coarse_idx >= 0:
+                assert float(rec["fine_metric"][i]) == float(np.float32(r.fine_metric)), (i, fl)
+
+
+@pytest.mark.parametrize("snr_db,tiny", [(6, False), (8, True), (12, True)])
+def test_forced_exact_matches_oracle_under_noise(snr_db, tiny):
+    cfg, x, offs, lens = _noisy_batch("acoustic", "BPSK", 3, 12, 64, snr_db, seed=snr_db, tiny=tiny)
+    dm = amodem.Demodulator(0)
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg, options=L.OPT_FORCE_EXACT)
+    dm.close()
+    assert (rec["flags"] & L.FLAG_EXACT).all()
+    _check_against_oracle("acoustic", "BPSK", 3, x, offs, lens, rec, pay)
+
+
+@pytest.mark.parametrize("preset,snr_db", [("acoustic", 6), ("standard", 7)])
+def test_listed_coarse_frames_match_oracle(preset, snr_db):
+    """Frames the fast path lists for an ambiguous coarse decision run the replica's
+    recurrence only up to the proven hull: the argmax still equals the oracle's."""
+    cfg, x, offs, lens = _noisy_batch(preset, "BPSK", 3, 48, 64, snr_db, seed=3)
+    dm = amodem.Demodulator(0)
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    full, fpay = dm.decode_batch(x, offs, lens, cfg=cfg, options=L.OPT_FORCE_EXACT)
+    dm.close()
+    coarse_listed = (rec["flags"] & (1 << 3)) != 0  # AMOD_FLAG_COARSE
+    listed = (rec["flags"] & L.FLAG_EXACT) != 0
+    for i in np.nonzero(coarse_listed & listed)[0]:
+        assert int(rec["coarse_idx"][i]) == int(full["coarse_idx"][i]), i
+        assert float(rec["fine_metric"][i]) == float(full["fine_metric"][i]), i
+    for n in ("status", "preamble_idx", "frame_type", "nbytes", "data_len", "expected_crc", "actual_crc", "crc_valid"):
+        assert (rec[n] == full[n]).all(), n
+    _check_against_oracle(preset, "BPSK", 3, x, offs, lens, rec, pay)
+
+
+def test_exact_mean_is_the_sequential_sum():
+    """preprocessSignal's mean on the exact path equals numpy's sequential (cumsum) fp64
+    sum over a frame with samples far below the running sum's ulp."""
+    import torch
+    cfg, x, offs, lens = _noisy_batch("acoustic", "BPSK", 3, 1, 64, 8, seed=5, tiny=True)
+    fr = x[offs[0]:offs[0] + lens[0]].copy()
+    seq = np.cumsum(fr.astype(np.float64))[-1] / len(fr)
+    dev = torch.device("cuda", 0)
+    xs = torch.from_numpy(np.concatenate([fr, np.zeros(4, np.float32)])).to(dev)
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    ln = torch.tensor([len(fr)], dtype=torch.int32, device=dev)
+    stride = amodem.payload_stride(cfg, len(fr))
+    res = torch.zeros(96, dtype=torch.uint8, device=dev)
+    pay = torch.zeros(stride, dtype=torch.uint8, device=dev)
+    dbg = torch.zeros(L.C.sizeof(L.Debug), dtype=torch.uint8, device=dev)
+    dm = amodem.Demodulator(0)
+    dm.reserve(cfg, 1, len(fr))
+    torch.cuda.synchronize()
+    dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), off.data_ptr(), ln.data_ptr(), 1, res.data_ptr(),
+                     pay.data_ptr(), stride, options=L.OPT_FORCE_EXACT, debug_ptr=dbg.data_ptr())
+    dm.synchronize()
+    d = L.Debug.from_buffer_copy(dbg.cpu().numpy().tobytes())
+    dm.close()
+    _, mean, _ = O.preprocess(fr)
+    assert mean == seq
+    assert d.mean == seq
