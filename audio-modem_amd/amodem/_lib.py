@@ -142,11 +142,14 @@ SIGNATURES = {
     "amod_asm_file": (C.c_int64, [_P, _P, C.c_int64]),
     "amod_stream_receive": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, C.c_int64, C.POINTER(C.c_int64),
                                       _P, C.c_int64, C.POINTER(StreamStats)]),
+    "amod_stream_receive_device": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, C.c_int64,
+                                             C.POINTER(C.c_int64), _P, C.c_int64, C.POINTER(StreamStats)]),
     "amod_stream_shard": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                     C.POINTER(StreamState), C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64,
                                     C.POINTER(C.c_int64), _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_int64), _P,
                                     C.POINTER(StreamState)]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
+    "amod_dc_remove_device": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_double), C.POINTER(C.c_int64), _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),
 }

@@ -228,6 +228,21 @@ class Demodulator:
         stats = {k: getattr(st, k) for k, _ in L.StreamStats._fields_}
         return frames[:min(n.value, max_frames)], rf[:min(st.nrefine_fail, len(rf))].tolist(), stats
 
+    def stream_receive_device(self, cfg: L.Cfg, samples_ptr: int, n: int, assembler: "ChunkAssembler | None" = None,
+                              max_frames: int = 1 << 20):
+        """stream_receive over n samples already in device memory (samples_ptr)."""
+        frames = np.zeros(max_frames, STREAM_FRAME_DTYPE)
+        rf = np.zeros(1 << 16, np.int64)
+        cnt = C.c_int64()
+        st = L.StreamStats()
+        with self._lock:
+            L.check(self._L.amod_stream_receive_device(self.ctx, C.byref(cfg), samples_ptr, n,
+                                                       assembler._h if assembler is not None else None,
+                                                       frames.ctypes.data, max_frames, C.byref(cnt), rf.ctypes.data,
+                                                       len(rf), C.byref(st)), self.ctx)
+        stats = {k: getattr(st, k) for k, _ in L.StreamStats._fields_}
+        return frames[:min(cnt.value, max_frames)], rf[:min(st.nrefine_fail, len(rf))].tolist(), stats
+
     def stream_shard(self, cfg: L.Cfg, samples: np.ndarray, lo: int, hi: int, own_lo: int, own_hi: int,
                      start: "L.StreamState | None" = None, meta_received: bool = False, chunk_size: int = 0,
                      until_meta: bool = False, stride: int = 0, max_events: int | None = None):

@@ -434,17 +434,21 @@ hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, in
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
 int amod_fast_lds_bytes(int nb_cap, int fine_cap); // dynamic LDS of one k_detect workgroup
 // streaming receiver pieces (k_stream.hip)
-hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, float *y, double *warm, double *end,
-                           unsigned long long *fixed, hipStream_t s);
+int64_t amod_ema_chunk();
+hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
+                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s);
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
-hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, const int64_t *first,
-                            const int64_t *base, const int64_t *count, int nranges, int64_t maxcount, double2 *out,
-                            hipStream_t s);
+hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
+                            const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
+                            int64_t maxcount, double *out, hipStream_t s);
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,
                               int nwin, float *out, hipStream_t s);
 // runtime.cpp: a context's device and stream for the host-side orchestrators
 int amod_ctx_device(const amod_ctx *ctx);
 hipStream_t amod_ctx_stream(const amod_ctx *ctx);
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code);
+// per-context state owned by another module (slot: 0 = streaming receiver): *amod_ctx_ext
+// holds it; free_fn runs at amod_close, after the context's streams are drained
+void **amod_ctx_ext(amod_ctx *ctx, int slot, void (*free_fn)(void *));
 int amod_cfg_valid(const amod_cfg *cfg); // the decode entry points' configuration check
 }

@@ -1,24 +1,26 @@
 // k_stream.hip — GPU pieces of the streaming receiver (app.js StreamingReceiver 706-998).
 //
-//   k_ema        processAudioBlock's DC removal (app.js:751-755): the EMA
-//                m_i = 0.999 m_{i-1} + (1 - 0.999) x_i in IEEE double, cleaned_i =
-//                f32(x_i - m_i), bit-exact. One lane per chunk of L samples: the lane
-//                first runs the recurrence over the W samples before its chunk from 0
-//                (the map contracts by 0.999 per step, so chains from different
-//                states coalesce bit for bit after ~36k steps), then over its chunk,
-//                16 samples per float4 x4 load/store. The state it reached at its
-//                chunk start is kept for k_ema_fix.
-//   k_ema_fix    one lane walks the chunks in order: a chunk whose warm-up state is
-//                not bit-equal to its predecessor's true end state is recomputed from
-//                that state. Afterwards every cleaned sample equals the reference's.
+//   k_ema_*      processAudioBlock's DC removal (app.js:751-755): the EMA
+//                m_i = 0.999 m_(i-1) + (1 - 0.999) x_i in IEEE double, cleaned_i =
+//                f32(x_i - m_i), bit-exact. (1) each 1024-sample chunk's contribution
+//                to the state at its end, coalesced; (2) one lane per chunk runs the
+//                exact recurrence from an approximate state 16 chunks back (a short
+//                geometric sum of those contributions; the map
+//                contracts by 0.999 a step, so the chain meets the true one bit for bit)
+//                and through its own chunk, samples staged through per-wave LDS tiles
+//                (coalesced rows, one row per lane); (3) every chunk whose warm-up state
+//                differs from its predecessor's end state is listed, (4) and recomputed
+//                from the true state in order. Afterwards every cleaned sample equals the
+//                reference's.
 //   k_sc_blocks  fp64 32-sample block sums (coalesced, 32-lane reductions), then
 //   k_sc_screen  hot-block screening for the fine precompute: the Schmidl-Cox metric
 //                at each block start from 8-block window sums; only a hint (the host
 //                recomputes anything the hint missed).
-//   k_fine       _refineAndCollect's cross-correlation sums (app.js:864-877) for a
+//   k_fine       _refineAndCollect's cross-correlation metric (app.js:864-877) for a
 //                list of position ranges: corr = sum seg[i] pre1[i] and sEnergy =
-//                sum seg[i]^2 in the reference's order, one lane per position, IEEE
-//                double (f32 x f32 products are exact in double).
+//                sum seg[i]^2 in the reference's order, then corr / sqrt(sEnergy E),
+//                one lane per position, IEEE double (f32 x f32 products are exact in
+//                double; sqrt and the quotient correctly rounded).
 //   k_window     _demodulateFrame's per-window peak normalisation (app.js:916-925):
 //                mx = max |x|, x / mx when mx > 1e-6 (f32 of the double quotient).
 // Built with -ffp-contract=off.
@@ -31,70 +33,200 @@ __device__ __forceinline__ float sample_at(const float *x, int64_t n, int64_t i)
 
 constexpr double kAlpha = 0.999;
 constexpr double kOneMinusAlpha = 1.0 - 0.999; // (1 - this.dcAlpha), evaluated in double
+constexpr int kL = 1024;                       // EMA chunk (one lane each in k_ema_out)
+constexpr int kWarm = 16;                      // warm-up chunks before each chunk (longer than
+                                               // a transmitter's inter-frame silence)
+constexpr int kTile = 64;                      // samples per lane per LDS tile
 
-__global__ __launch_bounds__(64) void k_ema(const float *__restrict__ x, int64_t n, int64_t L, int64_t W,
-                                            float *__restrict__ y, double *__restrict__ warm,
-                                            double *__restrict__ end, int64_t nchunks) {
-  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (t >= nchunks) return;
-  const int64_t s = t * L, e = s + L < n ? s + L : n, w0 = s - W > 0 ? s - W : 0;
-  double m = 0.0;
-  int64_t i = w0;
-  // 16-sample steps on float4 loads (x is 16-byte aligned; L, W multiples of 16)
-  for (; i + 16 <= s; i += 16) {
-    const float4 *p = reinterpret_cast<const float4 *>(x + i);
-    const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    const float v[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+// one step of processAudioBlock's DC removal (app.js:753): fl(fl(a m) + fl((1 - a) x))
+__device__ __forceinline__ double ema_step(double m, float x) { return kAlpha * m + kOneMinusAlpha * (double)x; }
+
+// (1) c_k = sum_i a^(L-1-i) (1-a) x_(kL+i): chunk k's contribution to the EMA at its end
+// from a zero start (fp64, approximate: it only seeds the warm-up). One workgroup per
+// chunk, coalesced. apow[j] = a^j.
+__global__ __launch_bounds__(256) void k_ema_contrib(const float *__restrict__ x, int64_t nx,
+                                                     const double *__restrict__ apow, double *__restrict__ c) {
+  __shared__ double red[4];
+  const int64_t k = blockIdx.x;
+  const int tid = threadIdx.x;
+  double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m = kAlpha * m + kOneMinusAlpha * (double)v[k];
+  for (int u = 0; u < kL / 256; ++u) {
+    const int i = tid + 256 * u;
+    const int64_t g = k * kL + i;
+    if (g < nx) acc += apow[kL - 1 - i] * (kOneMinusAlpha * (double)x[g]);
   }
-  for (; i < s; ++i) m = kAlpha * m + kOneMinusAlpha * (double)x[i];
-  warm[t] = m;
-  for (; i + 16 <= e; i += 16) {
-    const float4 *p = reinterpret_cast<const float4 *>(x + i);
-    const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    const float v[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-    float o[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      m = kAlpha * m + kOneMinusAlpha * (double)v[k];
-      o[k] = (float)((double)v[k] - m);
-    }
-    float4 *r = reinterpret_cast<float4 *>(y + i);
-    r[0] = make_float4(o[0], o[1], o[2], o[3]);
-    r[1] = make_float4(o[4], o[5], o[6], o[7]);
-    r[2] = make_float4(o[8], o[9], o[10], o[11]);
-    r[3] = make_float4(o[12], o[13], o[14], o[15]);
-  }
-  for (; i < e; ++i) {
-    m = kAlpha * m + kOneMinusAlpha * (double)x[i];
-    y[i] = (float)((double)x[i] - m);
-  }
-  end[t] = m;
+  acc = wave_sum(acc);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) c[k] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void k_ema_fix(const float *__restrict__ x, int64_t n, int64_t L, float *__restrict__ y,
-                          const double *__restrict__ warm, double *__restrict__ end, int64_t nchunks,
-                          unsigned long long *__restrict__ fixed) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double prev = end[0];
-  unsigned long long nf = 0;
-  for (int64_t t = 1; t < nchunks; ++t) {
-    if (__double_as_longlong(warm[t]) == __double_as_longlong(prev)) {
-      prev = end[t];
-      continue;
-    }
-    double m = prev;
-    const int64_t s = t * L, e = s + L < n ? s + L : n;
-    for (int64_t i = s; i < e; ++i) {
-      m = kAlpha * m + kOneMinusAlpha * (double)x[i];
-      y[i] = (float)((double)x[i] - m);
-    }
-    prev = m;
-    end[t] = m; // the chunk's true end state (read back by sharded receivers)
-    ++nf;
+// (2) the exact recurrence, one lane per chunk: from the approximate state at the end of
+// chunk k - kWarm - 1 (sum_j A^j c_(k - kWarm - 1 - j), A = a^L = 0.36: forty terms leave
+// a relative error below 1e-17), kWarm chunks of warm-up (the map contracts by 0.999 a step, so the
+// chain reaches the true one bit for bit), then chunk k with its outputs. The samples move
+// through a per-wave LDS tile (64 lanes x 64 samples): rows loaded coalesced one tile
+// ahead (registers), each lane walking its own row, output rows stored coalesced.
+// warm[k] = the state reached at chunk k's start.
+constexpr int kRow = kTile + 4; // row stride (floats): 16-byte rows for ds_read_b128
+__global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, int64_t nx, int64_t n,
+                                                 const double *__restrict__ c,
+                                                 double A, float *__restrict__ y, double *__restrict__ warm,
+                                                 double *__restrict__ end, int64_t nch) {
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * kRow];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t k0 = ((int64_t)blockIdx.x * 4 + wv) * 64; // the wave's first chunk
+  if (k0 >= nch) return;
+  const int64_t k = k0 + lane;
+  const int64_t kw = k - kWarm > 0 ? k - kWarm : 0;           // first warm-up chunk
+  double m = 0.0;                                             // zero start: the true one
+  if (k < nch && kw > 0) {
+    double p = 1.0;
+    for (int64_t j = kw - 1; j >= 0 && j > kw - 41; --j) { m += p * c[j]; p *= A; }
   }
-  *fixed = nf;
+  float *const T = tile[wv];
+  // lane l's row at step j covers samples [(k0 + l - kWarm) L + 64 j, + 64) (warm-up
+  // chunks first, then chunk k0 + l); rows before the stream start are skipped
+  constexpr int steps = (kWarm + 1) * kL / kTile, wsteps = kWarm * kL / kTile;
+  const int rr = lane >> 4, c4 = lane & 15; // load/store slot: rows rr + 4 q, column 4 c4
+  // the wave's window as raw buffers: out-of-range dwords read 0 / are not written, so no
+  // load or store sits under a branch (offsets before the stream start wrap out of range)
+  const int64_t wb = (k0 - kWarm) * kL > 0 ? (k0 - kWarm) * kL : 0, yb = k0 * kL;
+  const int64_t xlen = nx - wb > 0 ? nx - wb : 0, ylen = n - yb > 0 ? n - yb : 0;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(x + wb), (short)0, (int)(4 * (xlen < (1 << 28) ? xlen : (1 << 28))), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(y + yb), (short)0, (int)(4 * (ylen < (1 << 28) ? ylen : (1 << 28))), 0x00020000);
+  float4 pf[16]; // the next tile's samples
+  auto load = [&](int j) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t g = (k0 + rr + 4 * q - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * g), 0, 0);
+      pf[q] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+  };
+  load(0);
+  for (int j = 0; j < steps; ++j) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) *reinterpret_cast<float4 *>(T + (rr + 4 * q) * kRow + 4 * c4) = pf[q];
+    __builtin_amdgcn_wave_barrier();
+    if (j + 1 < steps) load(j + 1); // in flight under this tile's recurrence
+    const int64_t row0 = (k - kWarm) * kL + (int64_t)kTile * j; // first sample of this lane's row
+    const bool out = j >= wsteps;                                // chunk k itself
+    if (j == wsteps && k < nch) warm[k] = m;
+    float *const R = T + lane * kRow;
+    if (row0 >= kw * kL) { // warm-up from the chunk kw (its approximate seed), then chunk k
+      if (row0 + kTile <= n) {
+        // eight samples a group: the (1 - a) x products first, then the dependent chain
+        // fl(fl(a m) + b) alone, then the outputs from the saved states
+#pragma unroll 2
+        for (int i = 0; i < kTile; i += 8) {
+          const float4 v0 = *reinterpret_cast<const float4 *>(R + i), v1 = *reinterpret_cast<const float4 *>(R + i + 4);
+          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          double b[8], ms[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) b[u] = kOneMinusAlpha * (double)xv[u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) { m = kAlpha * m + b[u]; ms[u] = m; }
+          if (out) {
+            float o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = (float)((double)xv[u] - ms[u]);
+            *reinterpret_cast<float4 *>(R + i) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4 *>(R + i + 4) = make_float4(o[4], o[5], o[6], o[7]);
+          }
+        }
+      } else { // the stream's last samples
+        for (int i = 0; row0 + i < n; ++i) {
+          const float xv = R[i];
+          m = ema_step(m, xv);
+          if (out) R[i] = (float)((double)xv - m);
+        }
+      }
+    }
+    if (out) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = rr + 4 * q;
+        const int64_t g = r * kL + (int64_t)kTile * (j - wsteps) + 4 * c4;
+        const float4 v = *reinterpret_cast<const float4 *>(T + r * kRow + 4 * c4);
+        __amdgpu_buffer_rsrc_t yrr = yr;
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, yrr, (int)(4 * g), 0, 0);
+      }
+    }
+  }
+  if (k < nch) end[k] = m;
+}
+
+// (3) chunks whose warm-up state is not bit-equal to the previous chunk's end state
+// (warm-up not converged): listed for k_ema_fix. Chunk 0 starts from the true zero.
+__global__ __launch_bounds__(256) void k_ema_check(const double *__restrict__ warm, const double *__restrict__ end,
+                                                   int64_t nch, unsigned long long *__restrict__ cnt,
+                                                   int64_t *__restrict__ list) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x + 1;
+  if (k >= nch) return;
+  if (__double_as_longlong(warm[k]) != __double_as_longlong(end[k - 1])) {
+    const unsigned long long i = atomicAdd(cnt, 1ull);
+    list[i] = k;
+  }
+}
+
+// (4) one wave: the listed chunks in order, each recomputed from its predecessor's true
+// end state, and the next chunk too while its warm-up state disagrees with the new end.
+// Afterwards every cleaned sample equals the reference's. fixed = chunks recomputed.
+// The state is wave-uniform; 64 samples are loaded coalesced, stepped lane by lane in
+// order (readlane), and stored coalesced.
+__global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int64_t nx, int64_t n, float *__restrict__ y,
+                                                const double *__restrict__ warm, double *__restrict__ end, int64_t nch,
+                                                const unsigned long long *__restrict__ cnt, int64_t *__restrict__ list,
+                                                unsigned long long *__restrict__ fixed) {
+  if (blockIdx.x != 0) return;
+  const int lane = threadIdx.x;
+  const int64_t nl = (int64_t)*cnt;
+  unsigned long long nf = 0;
+  if (nl > 0) {
+    if (lane == 0) // the listed indices in increasing order (atomic append order is arbitrary)
+      for (int64_t i = 1; i < nl; ++i) {
+        const int64_t v = list[i];
+        int64_t j = i - 1;
+        while (j >= 0 && list[j] > v) { list[j + 1] = list[j]; --j; }
+        list[j + 1] = v;
+      }
+    __syncthreads();
+    int64_t done = 0; // chunks below this are final
+    for (int64_t li = 0; li < nl; ++li) {
+      int64_t t = list[li];
+      if (t < done) continue;
+      for (;;) {
+        double m = end[t - 1]; // true: every earlier chunk is verified or recomputed
+        const int64_t a = t * kL, b = a + kL < n ? a + kL : n;
+        for (int64_t b0 = a; b0 < b; b0 += 64) {
+          const float xv = b0 + lane < b && b0 + lane < nx ? x[b0 + lane] : 0.f;
+          const int nj = b - b0 < 64 ? (int)(b - b0) : 64;
+          float yv = 0.f;
+          for (int j = 0; j < nj; ++j) {
+            const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+            m = ema_step(m, xj);
+            const float o = (float)((double)xj - m);
+            yv = lane == j ? o : yv;
+          }
+          if (b0 + lane < b) y[b0 + lane] = yv;
+        }
+        if (lane == 0) end[t] = m; // the chunk's true end state (read back by sharded receivers)
+        ++nf;
+        if (t + 1 < nch && __double_as_longlong(warm[t + 1]) != __double_as_longlong(m)) { ++t; continue; }
+        done = t + 2; // chunk t + 1 started from this true state
+        break;
+      }
+    }
+  }
+  if (lane == 0) *fixed = nf;
 }
 
 // 32-sample block sums of the cleaned stream in fp64: z_b = sum y[k] y[k+256], e_b =
@@ -127,9 +259,9 @@ __global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ z
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
 // base[r] + j; one lane per position
 __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const float *__restrict__ pre1,
-                                              int sym, const int64_t *__restrict__ first,
+                                              int sym, double pre1_energy, const int64_t *__restrict__ first,
                                               const int64_t *__restrict__ base, const int64_t *__restrict__ count,
-                                              int nranges, double2 *__restrict__ out) {
+                                              int nranges, double *__restrict__ out) {
   const int r = blockIdx.y;
   if (r >= nranges) return;
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -141,7 +273,9 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
     corr += s * (double)pre1[i];
     se += s * s;
   }
-  out[base[r] + j] = make_double2(corr, se);
+  // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
+  const double denom = sqrt(se * pre1_energy);
+  out[base[r] + j] = denom > 0.001 ? corr / denom : __builtin_nan("");
 }
 
 __global__ __launch_bounds__(256) void k_window(const float *__restrict__ y, int64_t n, const int64_t *__restrict__ pos,
@@ -168,13 +302,23 @@ __global__ __launch_bounds__(256) void k_window(const float *__restrict__ y, int
 } // namespace amod
 
 extern "C" {
-hipError_t amod_launch_ema(const float *x, int64_t n, int64_t L, int64_t W, float *y, double *warm, double *end,
-                           unsigned long long *fixed, hipStream_t s) {
-  const int64_t nchunks = (n + L - 1) / L;
-  if (nchunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_ema, dim3((unsigned)((nchunks + 63) / 64)), dim3(64), 0, s, x, n, L, W, y, warm, end,
-                     nchunks);
-  hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, n, L, y, warm, end, nchunks, fixed);
+int64_t amod_ema_chunk() { return amod::kL; }
+// DC removal of x[0, n) from a zero EMA state into y (x read for [0, nx), zero past it); warm / end / scr: nch = ceil(n / L)
+// doubles each; list: nch int64; apow: L doubles (a^j); fixed: 2 counters
+hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
+                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s) {
+  const int64_t nch = (n + amod::kL - 1) / amod::kL;
+  if (nch <= 0) return hipSuccess;
+  double A = 1.0;
+  for (int i = 0; i < amod::kL; ++i) A *= amod::kAlpha;
+  hipError_t e = hipMemsetAsync(fixed, 0, 2 * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)nch), dim3(256), 0, s, x, nx, apow, scr);
+  hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, x, nx, n, scr, A, y, warm,
+                     end, nch);
+  hipLaunchKernelGGL(amod::k_ema_check, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, warm, end, nch, fixed + 1,
+                     list);
+  hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, list, fixed);
   return hipGetLastError();
 }
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {
@@ -184,12 +328,12 @@ hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double
   hipLaunchKernelGGL(amod::k_sc_screen, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, ze, nblk, thresh, hot);
   return hipGetLastError();
 }
-hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, const int64_t *first,
-                            const int64_t *base, const int64_t *count, int nranges, int64_t maxcount, double2 *out,
-                            hipStream_t s) {
+hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
+                            const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
+                            int64_t maxcount, double *out, hipStream_t s) {
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
   hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
-                     first, base, count, nranges, out);
+                     pre1_energy, first, base, count, nranges, out);
   return hipGetLastError();
 }
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,

@@ -240,6 +240,8 @@ struct amod_ctx {
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
   int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_bpc = 0;
+  void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
+  void (*ext_free[4])(void *) = {nullptr, nullptr, nullptr, nullptr};
   int64_t soft_stride = 0;
   int soft_slots = 0;
   int64_t xs_stride = 0, bits_stride = 0;
@@ -706,6 +708,11 @@ int amod_abi_version(void) { return AMOD_ABI_VERSION; }
 int amod_ctx_device(const amod_ctx *ctx) { return ctx ? ctx->device : 0; }
 hipStream_t amod_ctx_stream(const amod_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code) { return fail(ctx, msg, code); }
+void **amod_ctx_ext(amod_ctx *ctx, int slot, void (*free_fn)(void *)) {
+  if (!ctx || slot < 0 || slot >= 4) return nullptr;
+  if (free_fn) ctx->ext_free[slot] = free_fn;
+  return &ctx->ext[slot];
+}
 int amod_cfg_valid(const amod_cfg *cfg) { return validate(cfg); }
 
 int amod_open(int device, amod_ctx **out) {
@@ -733,7 +740,10 @@ int amod_close(amod_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamDestroy(ctx->stream);
-  if (ctx->aux) { (void)hipStreamSynchronize(ctx->aux); (void)hipStreamDestroy(ctx->aux); }
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  for (int i = 0; i < 4; ++i)
+    if (ctx->ext[i] && ctx->ext_free[i]) ctx->ext_free[i](ctx->ext[i]);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &ev : ctx->ev_used) for (auto &e : ev) (void)hipEventDestroy(e);

@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -37,17 +38,21 @@
 namespace {
 
 constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
-constexpr int64_t kEmaChunk = 8192;   // k_ema chunk per lane (more lanes than warm-up length: latency bound)
-constexpr int64_t kEmaWarm = 65536;   // warm-up run before each chunk
+const int64_t kEmaChunk = amod_ema_chunk(); // k_ema chunk (EMA end states are reported per chunk)
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
 enum { IDLE = 0, DETECTED = 1, COLLECTING = 2 };
 
 struct DBuf {
   void *p = nullptr;
+  size_t cap = 0;
   ~DBuf() { if (p) (void)hipFree(p); }
-  hipError_t alloc(size_t n) {
-    if (p) { (void)hipFree(p); p = nullptr; }
-    return hipMalloc(&p, std::max<size_t>(n, 256));
+  hipError_t alloc(size_t n) { // grow-only: kept across calls (the context's stream cache)
+    n = std::max<size_t>(n, 256);
+    if (p && cap >= n) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    const hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) cap = n;
+    return e;
   }
   template <typename T> T *as() const { return (T *)p; }
 };
@@ -72,9 +77,9 @@ struct RxState {
 
 struct FineTable {
   std::vector<int64_t> first, base, count;
-  std::vector<double> corr_se; // pairs
+  const double *metric = nullptr; // k_fine's metrics (pinned), NaN where the reference skips
   // refine walks consecutive positions: `last` (the caller's cursor) is tried first
-  bool lookup(int64_t d, double &corr, double &se, size_t &last) const {
+  bool lookup(int64_t d, double &m, size_t &last) const {
     size_t r = last;
     if (r >= first.size() || d < first[r] || d >= first[r] + count[r]) {
       auto it = std::upper_bound(first.begin(), first.end(), d);
@@ -83,9 +88,7 @@ struct FineTable {
       last = r;
     }
     if (d >= first[r] + count[r]) return false;
-    const int64_t k = base[r] + (d - first[r]);
-    corr = corr_se[2 * k];
-    se = corr_se[2 * k + 1];
+    m = metric[base[r] + (d - first[r])];
     return true;
   }
 };
@@ -102,7 +105,16 @@ struct Receiver {
   int64_t fine_host = 0; // positions the host had to correlate itself
   size_t cursor = 0;     // FineTable lookup cursor
 
-  double S(int64_t i) const { return (i >= lo && i < lo + nloc) ? (double)y[i - lo] : 0.0; }
+  // the host copy of the cleaned stream arrives in pieces: local samples [0, avail) are
+  // there; a read past it waits for the piece that holds it
+  const std::function<void(int64_t)> *wait_y = nullptr;
+  mutable int64_t avail = INT64_MAX;
+  double S(int64_t i) const {
+    if (i < lo || i >= lo + nloc) return 0.0;
+    if (i - lo >= avail) { (*wait_y)(i - lo + 1); avail = piece_end(i - lo); }
+    return (double)y[i - lo];
+  }
+  std::function<int64_t(int64_t)> piece_end;
   int64_t tw() const { return (st.block + 1) * kBlock; } // totalWritten after this block's write
 
   // _scanForPreamble (app.js:775-847)
@@ -155,20 +167,19 @@ struct Receiver {
     double best = -INFINITY;
     int64_t best_pos = st.pre_pos;
     for (int64_t d = fs; d <= fe; ++d) {
-      double corr = 0, se = 0;
-      if (!fine || !fine->lookup(d, corr, se, cursor)) {
+      double metric;
+      if (!fine || !fine->lookup(d, metric, cursor)) {
+        double corr = 0, se = 0;
         for (int64_t i = 0; i < plen; ++i) {
           const double s = S(d + i);
           corr += s * (double)pre1[i];
           se += s * s;
         }
         ++fine_host;
+        const double denom = std::sqrt(se * pre1_energy);
+        metric = denom > 0.001 ? corr / denom : NAN;
       }
-      const double denom = std::sqrt(se * pre1_energy);
-      if (denom > 0.001) {
-        const double metric = corr / denom;
-        if (metric > best) { best = metric; best_pos = d; }
-      }
+      if (metric > best) { best = metric; best_pos = d; } // NaN: skipped (denom <= 0.001)
     }
     if (best < 0.1) {
       if (fails) fails->push_back({st.block, st.pre_pos});
@@ -308,50 +319,130 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
 }
 
 struct Pinned {
-  float *p = nullptr;
+  float *p = nullptr; // (any element type: as<T>())
+  size_t cap = 0;
   ~Pinned() { if (p) (void)hipHostFree(p); }
+  void *dp = nullptr; // device view (mapped allocations)
+  hipError_t alloc(size_t n, bool mapped = false) { // grow-only
+    n = std::max<size_t>(n, 16);
+    if (p && cap >= n) return hipSuccess;
+    if (p) { (void)hipHostFree(p); p = nullptr; dp = nullptr; cap = 0; }
+    hipError_t e = hipHostMalloc((void **)&p, n, mapped ? hipHostMallocMapped : hipHostMallocDefault);
+    if (e == hipSuccess && mapped) e = hipHostGetDevicePointer(&dp, p, 0);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  template <typename T> T *as() const { return (T *)p; }
 };
+
+// device and pinned buffers of the streaming receiver, kept per context (grow-only)
+struct StreamCache {
+  DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
+  DBuf d_pre1, d_first, d_base, d_count, d_out;
+  DBuf w_pos, w_len, w_woff, w_win, w_res, w_pay;
+  Pinned yh, hot_h, metric_h;
+  bool apow_ready = false;
+  hipStream_t s2 = nullptr;                 // the cleaned stream's device-to-host copy
+  static constexpr int kPieces = 16;
+  hipEvent_t ema_done = nullptr, piece[kPieces] = {};
+  ~StreamCache() {
+    if (s2) { (void)hipStreamSynchronize(s2); (void)hipStreamDestroy(s2); }
+    if (ema_done) (void)hipEventDestroy(ema_done);
+    for (auto e : piece)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+StreamCache &stream_cache(amod_ctx *ctx) {
+  void **slot = amod_ctx_ext(ctx, 0, [](void *q) { delete static_cast<StreamCache *>(q); });
+  if (!*slot) *slot = new StreamCache;
+  return *static_cast<StreamCache *>(*slot);
+}
 
 // The GPU part before the state machine, over stream samples [lo, lo + n) given on the
 // host (n a multiple of kBlock; lo a multiple of kEmaChunk): exact DC removal (EMA
 // started at lo), screening, fine sums, pinned host copy of the cleaned samples.
 struct Prepass {
-  DBuf d_x, d_y, d_warm, d_end, d_fixed, d_hot, d_ze;
-  Pinned yh;
+  StreamCache *c = nullptr;
+  const float *x = nullptr; // device samples of [lo, lo + nvalid)
   FineTable ft;
   int64_t lo = 0, n = 0, fixed = 0;
   std::vector<double> ema_end; // EMA state after each k_ema chunk (true states)
   double t_ema = 0, t_fine = 0;
+  const float *y() const { return c->d_y.as<float>(); }
+  std::function<void(int64_t)> wait_fn = [this](int64_t g) { wait_y(g); };
+  // the host copy of the cleaned stream holds local samples [0, g)
+  void wait_y(int64_t g) const {
+    for (int q = 0; q < StreamCache::kPieces; ++q) {
+      const int64_t a = n * q / StreamCache::kPieces;
+      if (a >= g) break;
+      (void)hipEventSynchronize(c->piece[q]);
+    }
+  }
 
+  // samples: host memory, or device memory when `device` (read for [0, nvalid); the
+  // padding up to n is zeros, as the reference's last block)
   int run(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t nvalid, int64_t lo_, int64_t n_,
-          hipStream_t s) {
+          hipStream_t s, bool device = false) {
+    c = &stream_cache(ctx);
     lo = lo_; n = n_;
     const int64_t nchunks = std::max<int64_t>(1, (n + kEmaChunk - 1) / kEmaChunk);
-    S_TRY(d_x.alloc(sizeof(float) * (size_t)n + 64));
-    S_TRY(d_y.alloc(sizeof(float) * (size_t)n + 64));
-    S_TRY(d_warm.alloc(sizeof(double) * nchunks));
-    S_TRY(d_end.alloc(sizeof(double) * nchunks));
-    S_TRY(d_fixed.alloc(8));
-    S_TRY(d_hot.alloc((size_t)(n / 32 + 1)));
-    S_TRY(d_ze.alloc(sizeof(double2) * (size_t)(n / 32 + 1)));
-    if (n) {
-      S_TRY(hipMemsetAsync(d_x.p, 0, sizeof(float) * (size_t)n, s));
-      if (nvalid) S_TRY(hipMemcpyAsync(d_x.p, samples, sizeof(float) * (size_t)nvalid, hipMemcpyHostToDevice, s));
+    if (!device) S_TRY(c->d_x.alloc(sizeof(float) * (size_t)n + 64));
+    S_TRY(c->d_y.alloc(sizeof(float) * (size_t)n + 64));
+    S_TRY(c->d_warm.alloc(sizeof(double) * nchunks));
+    S_TRY(c->d_end.alloc(sizeof(double) * nchunks));
+    S_TRY(c->d_scr.alloc(sizeof(double) * nchunks));
+    S_TRY(c->d_list.alloc(sizeof(int64_t) * nchunks));
+    S_TRY(c->d_apow.alloc(sizeof(double) * kEmaChunk));
+    S_TRY(c->d_fixed.alloc(16));
+    if (!c->apow_ready) {
+      std::vector<double> ap((size_t)kEmaChunk);
+      double a = 1.0;
+      for (auto &v : ap) { v = a; a *= 0.999; }
+      S_TRY(hipMemcpy(c->d_apow.p, ap.data(), sizeof(double) * ap.size(), hipMemcpyHostToDevice));
+      c->apow_ready = true;
+    }
+    S_TRY(c->d_hot.alloc((size_t)(n / 32 + 1)));
+    S_TRY(c->d_ze.alloc(sizeof(double2) * (size_t)(n / 32 + 1)));
+    if (device) {
+      x = samples;
+    } else {
+      x = c->d_x.as<float>();
+      if (nvalid) S_TRY(hipMemcpyAsync(c->d_x.p, samples, sizeof(float) * (size_t)nvalid, hipMemcpyHostToDevice, s));
     }
     hipEvent_t ev[3];
     for (auto &e : ev) S_TRY(hipEventCreate(&e));
     S_TRY(hipEventRecord(ev[0], s));
-    S_TRY(amod_launch_ema(d_x.as<float>(), n, kEmaChunk, kEmaWarm, d_y.as<float>(), d_warm.as<double>(),
-                          d_end.as<double>(), d_fixed.as<unsigned long long>(), s));
+    S_TRY(amod_launch_ema(x, nvalid, n, c->d_y.as<float>(), c->d_warm.as<double>(), c->d_end.as<double>(),
+                          c->d_scr.as<double>(), c->d_list.as<int64_t>(), c->d_apow.as<double>(),
+                          c->d_fixed.as<unsigned long long>(), s));
     S_TRY(hipEventRecord(ev[1], s));
-    S_TRY(amod_launch_sc_screen(d_y.as<float>(), n, 0.25f, d_ze.as<double2>(), d_hot.as<uint8_t>(), s));
-    std::vector<uint8_t> hot((size_t)(n / 32));
-    if (!hot.empty()) S_TRY(hipMemcpyAsync(hot.data(), d_hot.p, hot.size(), hipMemcpyDeviceToHost, s));
+    S_TRY(amod_launch_sc_screen(c->d_y.as<float>(), n, 0.25f, c->d_ze.as<double2>(), c->d_hot.as<uint8_t>(), s));
+    const int64_t nhot = n / 32;
+    S_TRY(c->hot_h.alloc((size_t)std::max<int64_t>(nhot, 1)));
+    const uint8_t *const hot = c->hot_h.as<uint8_t>();
+    if (nhot) S_TRY(hipMemcpyAsync(c->hot_h.p, c->d_hot.p, (size_t)nhot, hipMemcpyDeviceToHost, s));
     ema_end.resize(nchunks);
-    S_TRY(hipStreamSynchronize(s));
     unsigned long long fx = 0;
-    S_TRY(hipMemcpy(&fx, d_fixed.p, 8, hipMemcpyDeviceToHost));
-    S_TRY(hipMemcpy(ema_end.data(), d_end.p, sizeof(double) * nchunks, hipMemcpyDeviceToHost));
+    S_TRY(hipMemcpyAsync(&fx, c->d_fixed.p, 8, hipMemcpyDeviceToHost, s));
+    S_TRY(hipMemcpyAsync(ema_end.data(), c->d_end.p, sizeof(double) * nchunks, hipMemcpyDeviceToHost, s));
+    // the cleaned stream to the host (pinned) on a second stream, in pieces, under the
+    // screening / fine-sum work and the receiver's first segments
+    S_TRY(c->yh.alloc(sizeof(float) * (size_t)std::max<int64_t>(n, 1)));
+    if (!c->s2) {
+      S_TRY(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
+      S_TRY(hipEventCreateWithFlags(&c->ema_done, hipEventDisableTiming));
+      for (auto &e : c->piece) S_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    S_TRY(hipEventRecord(c->ema_done, s));
+    S_TRY(hipStreamWaitEvent(c->s2, c->ema_done, 0));
+    for (int q = 0; q < StreamCache::kPieces; ++q) {
+      const int64_t a = n * q / StreamCache::kPieces, b = n * (q + 1) / StreamCache::kPieces;
+      if (b > a)
+        S_TRY(hipMemcpyAsync(c->yh.p + a, c->d_y.as<float>() + a, sizeof(float) * (size_t)(b - a),
+                             hipMemcpyDeviceToHost, c->s2));
+      S_TRY(hipEventRecord(c->piece[q], c->s2));
+    }
+    S_TRY(hipStreamSynchronize(s));
     fixed = (int64_t)fx;
     // fine ranges (local positions): every position within 448 samples of a hot block
     const int64_t pad = 448;
@@ -363,39 +454,40 @@ struct Prepass {
       total += rhi - rlo + 1;
     };
     bool open = false;
-    for (int64_t b = 0; b < (int64_t)hot.size(); ++b) {
+    for (int64_t b = 0; b < nhot; ++b) {
       if (!hot[b]) continue;
       const int64_t za = 32 * b - pad, zb = 32 * b + 31 + pad;
       if (open && za <= rhi + 1) rhi = std::max(rhi, zb);
       else { if (open) flush(); rlo = za; rhi = zb; open = true; }
     }
     if (open) flush();
-    ft.corr_se.assign(2 * (size_t)total, 0.0);
+    // k_fine writes its metrics straight into mapped host memory (no copy queued behind
+    // the cleaned stream's transfer)
+    S_TRY(c->metric_h.alloc(sizeof(double) * (size_t)std::max<int64_t>(total, 1), true));
+    ft.metric = c->metric_h.as<double>();
     if (total) {
-      DBuf d_pre1, d_first, d_base, d_count, d_out;
       std::vector<float> p1(cfg->symbol_len);
       if (amod_preamble1(cfg, p1.data()) != AMOD_SUCCESS) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+      double p1e = 0.0; // this.pre1Energy (app.js:744-745)
+      for (float v : p1) p1e += (double)v * (double)v;
       const int nr = (int)first_loc.size();
-      S_TRY(d_pre1.alloc(sizeof(float) * p1.size()));
-      S_TRY(d_first.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_base.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_count.alloc(sizeof(int64_t) * nr));
-      S_TRY(d_out.alloc(sizeof(double) * 2 * (size_t)total));
-      S_TRY(hipMemcpyAsync(d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_first.p, first_loc.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(c->d_pre1.alloc(sizeof(float) * p1.size()));
+      S_TRY(c->d_first.alloc(sizeof(int64_t) * nr));
+      S_TRY(c->d_base.alloc(sizeof(int64_t) * nr));
+      S_TRY(c->d_count.alloc(sizeof(int64_t) * nr));
+      S_TRY(hipMemcpyAsync(c->d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(c->d_first.p, first_loc.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(c->d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
       for (int r0 = 0; r0 < nr; r0 += 65535) {
         const int k = std::min(65535, nr - r0);
-        S_TRY(amod_launch_fine(d_y.as<float>(), n, d_pre1.as<float>(), cfg->symbol_len, d_first.as<int64_t>() + r0,
-                               d_base.as<int64_t>() + r0, d_count.as<int64_t>() + r0, k, maxc, d_out.as<double2>(), s));
+        S_TRY(amod_launch_fine(c->d_y.as<float>(), n, c->d_pre1.as<float>(), cfg->symbol_len, p1e,
+                               c->d_first.as<int64_t>() + r0, c->d_base.as<int64_t>() + r0,
+                               c->d_count.as<int64_t>() + r0, k, maxc, (double *)c->metric_h.dp, s));
       }
-      S_TRY(hipMemcpyAsync(ft.corr_se.data(), d_out.p, sizeof(double) * 2 * (size_t)total, hipMemcpyDeviceToHost, s));
     }
     S_TRY(hipEventRecord(ev[2], s));
-    S_TRY(hipHostMalloc((void **)&yh.p, sizeof(float) * (size_t)std::max<int64_t>(n, 1), hipHostMallocDefault));
-    if (n) S_TRY(hipMemcpyAsync(yh.p, d_y.p, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s));
     S_TRY(hipStreamSynchronize(s));
     float ta = 0, tb = 0;
     S_TRY(hipEventElapsedTime(&ta, ev[0], ev[1]));
@@ -408,7 +500,17 @@ struct Prepass {
   Receiver receiver(const amod_cfg *cfg) const {
     Receiver rx;
     rx.cfg = cfg;
-    rx.lo = lo; rx.nloc = n; rx.y = yh.p; rx.fine = &ft;
+    rx.lo = lo; rx.nloc = n; rx.y = c->yh.p; rx.fine = &ft;
+    rx.wait_y = &wait_fn;
+    rx.avail = 0;
+    const int64_t nn = n;
+    rx.piece_end = [nn](int64_t g) { // end of the piece holding local sample g
+      for (int q = 0; q < StreamCache::kPieces; ++q) {
+        const int64_t b = nn * (q + 1) / StreamCache::kPieces;
+        if (g < b) return b;
+      }
+      return nn;
+    };
     rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
     rx.pre1.resize(cfg->symbol_len);
     amod_preamble1(cfg, rx.pre1.data());
@@ -420,7 +522,6 @@ struct Prepass {
 // Decodes frames' windows on the GPU (k_window peak normalisation + chunk-mode decode);
 // res[i] / payload row i for frame i (lost frames get AMOD_E_STREAM_LOST).
 struct WindowDecoder {
-  DBuf d_pos, d_len, d_woff, d_win, d_res, d_pay;
   std::vector<amod_result> res;
   std::vector<uint8_t> pay;
   int64_t stride = 16;
@@ -445,6 +546,8 @@ struct WindowDecoder {
     stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
     std::vector<amod_result> r(nw);
     std::vector<uint8_t> py((size_t)stride * nw);
+    StreamCache &c = *pp.c;
+    DBuf &d_pos = c.w_pos, &d_len = c.w_len, &d_woff = c.w_woff, &d_win = c.w_win, &d_res = c.w_res, &d_pay = c.w_pay;
     if (nw) {
       S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
@@ -456,7 +559,7 @@ struct WindowDecoder {
       S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
-      S_TRY(amod_launch_window(pp.d_y.as<float>(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
+      S_TRY(amod_launch_window(pp.y(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
                                d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
       int rc = amod_reserve(ctx, cfg, nw, maxlen);
       if (rc) return rc;
@@ -512,10 +615,42 @@ RxState from_state(const amod_stream_state &o) {
 
 } // namespace
 
-extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
-                                   amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
-                                   int64_t *nframes_out, int64_t *refine_fail, int64_t max_refine_fail,
-                                   amod_stream_stats *stats) {
+// processAudioBlock's DC removal (app.js:751-755) over a device buffer, from a zero EMA
+// state at x[0]: y = cleaned samples (device), *end_state = the state after x[n - 1]
+extern "C" int amod_dc_remove_device(amod_ctx *ctx, const float *x, int64_t n, float *y, double *end_state,
+                                     int64_t *chunks_fixed, void *stream) {
+  if (!ctx || n < 0 || (n && (!x || !y))) return amod_ctx_fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  if (n == 0) { if (end_state) *end_state = 0.0; if (chunks_fixed) *chunks_fixed = 0; return AMOD_SUCCESS; }
+  S_TRY(hipSetDevice(amod_ctx_device(ctx)));
+  hipStream_t s = stream ? (hipStream_t)stream : amod_ctx_stream(ctx);
+  const int64_t nch = (n + kEmaChunk - 1) / kEmaChunk;
+  DBuf warm, end, scr, list, apow, fixed;
+  S_TRY(warm.alloc(sizeof(double) * nch));
+  S_TRY(end.alloc(sizeof(double) * nch));
+  S_TRY(scr.alloc(sizeof(double) * nch));
+  S_TRY(list.alloc(sizeof(int64_t) * nch));
+  S_TRY(apow.alloc(sizeof(double) * kEmaChunk));
+  S_TRY(fixed.alloc(16));
+  std::vector<double> ap((size_t)kEmaChunk);
+  double a = 1.0;
+  for (auto &v : ap) { v = a; a *= 0.999; }
+  S_TRY(hipMemcpyAsync(apow.p, ap.data(), sizeof(double) * ap.size(), hipMemcpyHostToDevice, s));
+  S_TRY(amod_launch_ema(x, n, n, y, warm.as<double>(), end.as<double>(), scr.as<double>(), list.as<int64_t>(),
+                        apow.as<double>(), fixed.as<unsigned long long>(), s));
+  double e = 0.0;
+  unsigned long long fx = 0;
+  S_TRY(hipMemcpyAsync(&e, end.as<double>() + nch - 1, sizeof(double), hipMemcpyDeviceToHost, s));
+  S_TRY(hipMemcpyAsync(&fx, fixed.p, sizeof fx, hipMemcpyDeviceToHost, s));
+  S_TRY(hipStreamSynchronize(s));
+  if (end_state) *end_state = e;
+  if (chunks_fixed) *chunks_fixed = (int64_t)fx;
+  return AMOD_SUCCESS;
+}
+
+static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n, bool device,
+                          amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                          int64_t *nframes_out, int64_t *refine_fail, int64_t max_refine_fail,
+                          amod_stream_stats *stats) {
   using clk = std::chrono::steady_clock;
   const auto t_start = clk::now();
   if (!ctx || !cfg || n < 0 || (n && !samples) || (max_frames > 0 && !frames) || !nframes_out)
@@ -527,7 +662,7 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
   amod_stream_stats stt{};
   Prepass pp;
   {
-    const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s);
+    const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s, device);
     if (rc) return rc;
   }
   stt.ema_chunks_fixed = pp.fixed;
@@ -641,6 +776,21 @@ extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const flo
     *stats = stt;
   }
   return AMOD_SUCCESS;
+}
+
+extern "C" int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
+                                   amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                                   int64_t *nframes_out, int64_t *refine_fail, int64_t max_refine_fail,
+                                   amod_stream_stats *stats) {
+  return stream_receive(ctx, cfg, samples, n, false, assembler, frames, max_frames, nframes_out, refine_fail,
+                        max_refine_fail, stats);
+}
+extern "C" int amod_stream_receive_device(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
+                                          amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                                          int64_t *nframes_out, int64_t *refine_fail, int64_t max_refine_fail,
+                                          amod_stream_stats *stats) {
+  return stream_receive(ctx, cfg, samples, n, true, assembler, frames, max_frames, nframes_out, refine_fail,
+                        max_refine_fail, stats);
 }
 
 extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t lo, int64_t hi,

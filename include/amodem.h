@@ -298,9 +298,23 @@ typedef struct amod_stream_stats {
   int64_t fine_host_positions;                 /* refine positions outside the GPU precompute */
   double t_ema_ms, t_fine_ms, t_decode_ms, t_host_ms, t_total_ms;
 } amod_stream_stats;
+/* processAudioBlock's DC removal (app.js:751-755) over a device buffer x[0, n) from a zero
+ * EMA state: y (device) = f32(x - m) bit-exact, *end_state = the EMA state after x[n - 1],
+ * *chunks_fixed = EMA chunks whose parallel warm-up had to be recomputed (diagnostics).
+ * Either pointer may be NULL. stream 0: the context's stream; returns after it is done. */
+int amod_dc_remove_device(amod_ctx *ctx, const float *x, int64_t n, float *y, double *end_state,
+                          int64_t *chunks_fixed, void *stream);
+
 int amod_stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
                         amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
                         int64_t *nframes, int64_t *refine_fail, int64_t max_refine_fail, amod_stream_stats *stats);
+
+/* amod_stream_receive with the samples already in device memory (samples: a device
+ * pointer to n floats; the stream is not copied). */
+int amod_stream_receive_device(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, int64_t n,
+                               amod_assembler *assembler, amod_stream_frame *frames, int64_t max_frames,
+                               int64_t *nframes, int64_t *refine_fail, int64_t max_refine_fail,
+                               amod_stream_stats *stats);
 
 /* ---- sharded streaming receive (one process per GPU, SURVEY §8e raw single stream) ----
  * The receiver's state between blocks (StreamingReceiver fields): */

@@ -216,6 +216,17 @@ static double js_max(double a, double b) { /* Math.max: NaN-propagating */
   return b > a ? b : a;
 }
 
+/* StreamingReceiver.processAudioBlock's DC removal (app.js:751-755): the EMA state runs
+   on across calls (*state in / out) */
+void orc_dc_remove(const float *x, long n, float *out, double *state) {
+  double m = *state;
+  for (long i = 0; i < n; ++i) {
+    m = 0.999 * m + (1 - 0.999) * (double)x[i];
+    out[i] = (float)((double)x[i] - m);
+  }
+  *state = m;
+}
+
 void orc_preprocess(const float *x, int n, float *out, double *mean_o, double *mx_o) { /* 213-232 */
   double mean = 0.0;
   for (int i = 0; i < n; i++) mean += (double)x[i];

@@ -76,6 +76,7 @@ int orc_bits_to_bytes(const uint8_t *bits, int nbits, uint8_t *out);   /* modem.
 int orc_estimate_frame_samples(const orc_cfg *c, int payload, int mod, int rep); /* modem.js:863-874 */
 
 /* receive chain stages */
+void orc_dc_remove(const float *x, long n, float *out, double *state);
 void orc_preprocess(const float *x, int n, float *out, double *mean, double *mx); /* modem.js:213-232 */
 int orc_detect_preamble(const float *sig, int n, const orc_cfg *c);               /* modem.js:286-319 */
 int orc_fine_timing(const float *sig, int n, const orc_cfg *c, int coarse, double *best); /* modem.js:567-588 */

@@ -67,6 +67,7 @@ def lib():
             "orc_bits_to_bytes": (C.c_int, [u8p, C.c_int, u8p]),
             "orc_estimate_frame_samples": (C.c_int, [cfgp, C.c_int, C.c_int, C.c_int]),
             "orc_preprocess": (None, [f32p, C.c_int, f32p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+            "orc_dc_remove": (None, [f32p, C.c_long, f32p, C.POINTER(C.c_double)]),
             "orc_detect_preamble": (C.c_int, [f32p, C.c_int, cfgp]),
             "orc_fine_timing": (C.c_int, [f32p, C.c_int, cfgp, C.c_int, C.POINTER(C.c_double)]),
             "orc_estimate_channel": (None, [f32p, cfgp, f64p, f64p]),
@@ -190,6 +191,15 @@ def decode(c: Cfg, x: np.ndarray, mod: str, rep: int, chunk: bool):
     fn = lib().orc_decode_chunk if chunk else lib().orc_decode_received
     fn(C.byref(c), xx, n, MODS[mod], rep, C.byref(r), buf, cap)
     return r, buf[:max(0, min(r.nbytes, cap))].copy()
+
+
+def dc_remove(x: np.ndarray, state: float = 0.0):
+    """processAudioBlock's EMA DC removal (app.js:751-755) -> (cleaned, end state)."""
+    xx = _f32(x)
+    out = np.zeros(len(xx), np.float32)
+    st = C.c_double(state)
+    lib().orc_dc_remove(xx, len(x), out, C.byref(st))
+    return out[:len(x)], st.value
 
 
 def preprocess(x: np.ndarray):
