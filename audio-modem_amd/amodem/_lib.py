@@ -91,6 +91,11 @@ class StreamStats(C.Structure):
                                           "final_scan_pos", "ema_chunks_fixed", "fine_host_positions")] + \
                [(n, C.c_double) for n in ("t_ema_ms", "t_fine_ms", "t_decode_ms", "t_host_ms", "t_total_ms")]
 
+class LiveStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("total_written", "frames_decoded", "frame_errors", "refine_fails",
+                                          "last_refine_fail", "fine_host_positions")]
+
+
 # (restype, argtypes) for every symbol the header declares
 _P = C.c_void_p
 SIGNATURES = {
@@ -149,6 +154,11 @@ SIGNATURES = {
                                     C.POINTER(C.c_int64), _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_int64), _P,
                                     C.POINTER(StreamState)]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
+    "amod_live_open": (C.c_int, [_P, C.POINTER(Cfg), _P, C.POINTER(_P)]),
+    "amod_live_process_block": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_int32)]),
+    "amod_live_state": (C.c_int, [_P, C.POINTER(StreamState), C.POINTER(LiveStats)]),
+    "amod_live_refine_fails": (C.c_int64, [_P, _P, C.c_int64]),
+    "amod_live_close": (None, [_P]),
     "amod_dc_remove_device": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_double), C.POINTER(C.c_int64), _P]),
     "amod_synth_legacy_batch": (C.c_int64, [C.POINTER(Cfg), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                             C.c_int32, _P, _P, _P, C.c_int32]),

@@ -463,6 +463,56 @@ def _asm_check(rc):
     return rc
 
 
+class StreamingReceiver:
+    """app.js StreamingReceiver (706-998) driven live, one audio block per call
+    (processAudioBlock, 749-773): DC removal, ring buffer and one state-machine step on
+    the host, windows decoded on the GPU (decodeChunkFrame) and handed to the assembler.
+    process_audio_block returns the demodulated window's STREAM_FRAME_DTYPE record, or
+    None. Fed a recorded stream's blocks, the frames equal Demodulator.stream_receive's."""
+
+    def __init__(self, demodulator: "Demodulator", cfg: L.Cfg, assembler: "ChunkAssembler | None" = None):
+        self._L = L.load()
+        self._dm = demodulator
+        self.cfg = cfg
+        self.assembler = assembler if assembler is not None else ChunkAssembler()
+        h = C.c_void_p()
+        L.check(self._L.amod_live_open(demodulator.ctx, C.byref(cfg), self.assembler._h, C.byref(h)), demodulator.ctx)
+        self._h = h
+
+    def process_audio_block(self, samples) -> "np.ndarray | None":
+        x = np.ascontiguousarray(samples, np.float32)
+        rec = np.zeros(1, STREAM_FRAME_DTYPE)
+        has = C.c_int32()
+        with self._dm._lock:
+            L.check(self._L.amod_live_process_block(self._h, x.ctypes.data, len(x), rec.ctypes.data, C.byref(has)),
+                    self._dm.ctx)
+        return rec[0] if has.value else None
+
+    def state(self) -> dict:
+        st, ls = L.StreamState(), L.LiveStats()
+        L.check(self._L.amod_live_state(self._h, C.byref(st), C.byref(ls)))
+        out = {k: getattr(st, k) for k, _ in L.StreamState._fields_}
+        out.update({k: getattr(ls, k) for k, _ in L.LiveStats._fields_})
+        return out
+
+    def refine_fails(self) -> list:
+        n = self._L.amod_live_refine_fails(self._h, None, 0)
+        buf = np.zeros(max(n, 1), np.int64)
+        self._L.amod_live_refine_fails(self._h, buf.ctypes.data, n)
+        return buf[:n].tolist()
+
+    def close(self):
+        if self._h:
+            self._L.amod_live_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ChunkAssembler:
     """app.js ChunkAssembler (597-704) over libamodem's host assembler: same method
     names (snake_case), same state and the same thrown errors. directory: keep the

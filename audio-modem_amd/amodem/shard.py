@@ -259,5 +259,30 @@ def stream_receive_sharded(dm, cfg, samples_for, n: int, rank: int, world: int, 
     for g in gathered:
         g["events"] = [L.StreamEvent.from_buffer_copy(b) for b in g["events"]]
     traj, fails, warn = merge_trajectories(gathered)
+    # A metadata frame past phase A that changes the window length (metaReceived /
+    # chunkSize, app.js:889-896, 939-949) invalidates every later window the shards cut
+    # with the old length: rank 0 keeps the trajectory up to it and re-runs the rest of
+    # the stream from the receiver state right after it (updated), until no change is left.
+    npad = -(-n // BLOCK) * BLOCK
+    meta, chunk_now = bool(endA.meta_received), chunk
+    i = len(msg[1])  # events before it are phase A's (already applied)
+    while i < len(traj):
+        r = traj[i][0].frame.result
+        if r.status == 0 and r.frame_type == 0xFE and r.crc_valid:
+            new_meta = meta or r.total_chunks > -8  # apply_meta (stream.cpp): bitmap allocation throws at <= -8
+            new_chunk = r.chunk_size
+            if new_meta != meta or (new_meta and new_chunk != chunk_now):
+                st = L.StreamState.from_buffer_copy(bytes(traj[i][0].after))
+                st.meta_received, st.chunk_size = int(new_meta), int(new_chunk)
+                warn.append(f"metadata change at stream sample {traj[i][0].frame.pos}: "
+                            f"the rest re-run from there on rank 0")
+                own = st.block * BLOCK
+                lo2 = max(0, (own - EMA_WARM) // EMA_CHUNK * EMA_CHUNK)
+                # (payload rows as wide as the longest window: dispatch feeds them one by one)
+                ev2, pay2, fl2, _, _ = dm.stream_shard(cfg, samples_for(lo2, npad), lo2, npad, own, npad, start=st)
+                fails = [f for f in fails if f[0] < st.block] + [f for f in fl2 if f[0] >= st.block]
+                traj = traj[: i + 1] + list(zip(ev2, pay2))
+                meta, chunk_now = new_meta, new_chunk
+        i += 1
     counters = dispatch_events(traj, assembler) if assembler is not None else {}
     return traj, fails, counters, warn

@@ -732,6 +732,91 @@ static napi_value js_receive_stream(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* ------------------------------------------------- live receiver (processAudioBlock) */
+static void live_finalize(napi_env env, void *data, void *hint) {
+  (void)env; (void)hint;
+  amod_live_close((amod_live *)data);
+}
+
+static amod_live *get_live(napi_env env, napi_value v) {
+  void *p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "expected a live receiver handle");
+    return NULL;
+  }
+  return (amod_live *)p;
+}
+
+/* liveOpen(cfg, assemblerHandle, device) -> handle (closed when collected) */
+static napi_value js_live_open(napi_env env, napi_callback_info info) {
+  napi_value argv[3], out;
+  if (!get_args(env, info, 3, argv)) return NULL;
+  amod_cfg c;
+  if (!to_cfg(env, argv[0], &c)) return NULL;
+  amod_assembler *a = get_asm(env, argv[1]);
+  if (!a) return NULL;
+  int32_t dev = 0;
+  napi_get_value_int32(env, argv[2], &dev);
+  amod_ctx *ctx = get_ctx(env, dev);
+  if (!ctx) return NULL;
+  amod_live *lv;
+  if (amod_live_open(ctx, &c, a, &lv) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(ctx));
+  NAPI_TRY(env, napi_create_external(env, lv, live_finalize, NULL, &out));
+  return out;
+}
+
+/* liveProcess(handle, Float32Array) -> ArrayBuffer (one amod_stream_frame) | null */
+static napi_value js_live_process(napi_env env, napi_callback_info info) {
+  napi_value argv[2], out;
+  if (!get_args(env, info, 2, argv)) return NULL;
+  amod_live *lv = get_live(env, argv[0]);
+  if (!lv) return NULL;
+  float *x;
+  size_t n;
+  if (!typed(env, argv[1], napi_float32_array, (void **)&x, &n)) return throw_msg(env, "expected a Float32Array");
+  amod_stream_frame f;
+  int32_t has = 0;
+  if (amod_live_process_block(lv, x, (int64_t)n, &f, &has) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(NULL));
+  if (!has) {
+    NAPI_TRY(env, napi_get_null(env, &out));
+    return out;
+  }
+  void *p;
+  NAPI_TRY(env, napi_create_arraybuffer(env, sizeof f, &p, &out));
+  memcpy(p, &f, sizeof f);
+  return out;
+}
+
+/* liveState(handle) -> {state, acScanPos, preambleGlobalPos, expectedFrameEnd, metaReceived,
+   chunkSize, totalWritten, framesDecoded, frameErrors, refineFails} */
+static napi_value js_live_state(napi_env env, napi_callback_info info) {
+  napi_value argv[1], out, v;
+  if (!get_args(env, info, 1, argv)) return NULL;
+  amod_live *lv = get_live(env, argv[0]);
+  if (!lv) return NULL;
+  amod_stream_state st;
+  amod_live_stats ls;
+  amod_live_state(lv, &st, &ls);
+  NAPI_TRY(env, napi_create_object(env, &out));
+#define SETNUM(name, val)                                                               \
+  do {                                                                                  \
+    NAPI_TRY(env, napi_create_double(env, (double)(val), &v));                          \
+    NAPI_TRY(env, napi_set_named_property(env, out, name, v));                          \
+  } while (0)
+  SETNUM("state", st.state);
+  SETNUM("acScanPos", st.ac_pos);
+  SETNUM("preambleGlobalPos", st.pre_pos);
+  SETNUM("expectedFrameEnd", st.frame_end);
+  SETNUM("metaReceived", st.meta_received);
+  SETNUM("chunkSize", st.chunk_size);
+  SETNUM("totalWritten", ls.total_written);
+  SETNUM("framesDecoded", ls.frames_decoded);
+  SETNUM("frameErrors", ls.frame_errors);
+  SETNUM("refineFails", ls.refine_fails);
+#undef SETNUM
+  return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -754,6 +839,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"asmMissing", NULL, js_asm_missing, NULL, NULL, NULL, napi_enumerable, NULL},
       {"asmFile", NULL, js_asm_file, NULL, NULL, NULL, napi_enumerable, NULL},
       {"receiveStream", NULL, js_receive_stream, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"liveOpen", NULL, js_live_open, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"liveProcess", NULL, js_live_process, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"liveState", NULL, js_live_state, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof props / sizeof props[0], props) != napi_ok) return NULL;
   return exports;

@@ -109,13 +109,18 @@ struct Receiver {
   // there; a read past it waits for the piece that holds it
   const std::function<void(int64_t)> *wait_y = nullptr;
   mutable int64_t avail = INT64_MAX;
+  // live mode (amod_live): the reference's RingBuffer itself; getRange reads
+  // buffer[i mod capacity] for any i at or after the oldest sample (app.js:580-589)
+  const float *ring = nullptr;
+  int64_t tw_live = -1; // totalWritten (live mode)
   double S(int64_t i) const {
+    if (ring) { int64_t r = i % cap; if (r < 0) r += cap; return (double)ring[r]; }
     if (i < lo || i >= lo + nloc) return 0.0;
     if (i - lo >= avail) { (*wait_y)(i - lo + 1); avail = piece_end(i - lo); }
     return (double)y[i - lo];
   }
   std::function<int64_t(int64_t)> piece_end;
-  int64_t tw() const { return (st.block + 1) * kBlock; } // totalWritten after this block's write
+  int64_t tw() const { return tw_live >= 0 ? tw_live : (st.block + 1) * kBlock; } // totalWritten after this block's write
 
   // _scanForPreamble (app.js:775-847)
   void scan() {
@@ -893,4 +898,159 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
   }
   if (end) to_state(tr.end, *end);
   return AMOD_SUCCESS;
+}
+
+// ---------------------------------------------------------------- live receiver
+// StreamingReceiver.processAudioBlock (app.js:749-773) one block at a time, as an
+// AudioWorklet / ScriptProcessor callback drives it: EMA DC removal on the host (a
+// block is a few thousand samples), the reference's RingBuffer, one state-machine
+// step per call (the same Receiver code as the recorded-stream path), and a window
+// that completes is peak-normalised and decoded on the GPU (decodeChunkFrame), then
+// handed to the ChunkAssembler exactly as _demodulateFrame does (app.js:907-972).
+struct amod_live {
+  amod_ctx *ctx = nullptr;
+  amod_cfg cfg{};
+  amod_assembler *assembler = nullptr;
+  bool own_assembler = false;
+  std::vector<float> ring;
+  int64_t tw = 0, block = 0;
+  double dc_mean = 0.0;
+  Receiver rx;
+  std::vector<std::pair<int64_t, int64_t>> fails;
+  std::vector<float> win;
+  std::vector<uint8_t> pay;
+  int64_t frames_decoded = 0, frame_errors = 0;
+};
+
+extern "C" int amod_live_open(amod_ctx *ctx, const amod_cfg *cfg, amod_assembler *assembler, amod_live **out) {
+  if (!ctx || !cfg || !out) return amod_ctx_fail(ctx, "invalid argument", AMOD_ERR_ARG);
+  if (!amod_cfg_valid(cfg)) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  auto *lv = new amod_live;
+  lv->ctx = ctx;
+  lv->cfg = *cfg;
+  if (!assembler) {
+    if (amod_asm_open(nullptr, &lv->assembler) != AMOD_SUCCESS) { delete lv; return amod_ctx_fail(ctx, "assembler", AMOD_ERR_NOMEM); }
+    lv->own_assembler = true;
+  } else {
+    lv->assembler = assembler;
+  }
+  Receiver &rx = lv->rx;
+  rx.cfg = &lv->cfg;
+  rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer (app.js:711-715)
+  lv->ring.assign((size_t)rx.cap, 0.f);
+  rx.ring = lv->ring.data();
+  rx.tw_live = 0;
+  rx.pre1.resize(cfg->symbol_len);
+  amod_preamble1(cfg, rx.pre1.data());
+  for (float v : rx.pre1) rx.pre1_energy += (double)v * (double)v;
+  rx.fails = &lv->fails;
+  amod_asm_info inf;
+  amod_asm_state(lv->assembler, &inf);
+  rx.st.chunk_size = inf.chunk_size;
+  *out = lv;
+  return AMOD_SUCCESS;
+}
+
+extern "C" int amod_live_process_block(amod_live *lv, const float *samples, int64_t n, amod_stream_frame *frame,
+                                       int32_t *has_frame) {
+  if (!lv || n < 0 || (n && !samples) || !frame || !has_frame) return amod_ctx_fail(lv ? lv->ctx : nullptr, "invalid argument", AMOD_ERR_ARG);
+  *has_frame = 0;
+  Receiver &rx = lv->rx;
+  const int64_t cap = rx.cap;
+  // DC removal (app.js:751-755) and ringBuffer.write (571-577)
+  double m = lv->dc_mean;
+  for (int64_t i = 0; i < n; ++i) {
+    m = 0.999 * m + (1 - 0.999) * (double)samples[i];
+    lv->ring[(size_t)(lv->tw % cap)] = (float)((double)samples[i] - m);
+    ++lv->tw;
+  }
+  lv->dc_mean = m;
+  rx.tw_live = lv->tw;
+  rx.st.block = lv->block++;
+  switch (rx.st.state) {
+  case IDLE: rx.scan(); break;
+  case DETECTED: rx.refine(); break;
+  case COLLECTING:
+    if (lv->tw >= rx.st.frame_end) { // _checkFrameComplete -> _demodulateFrame
+      amod_stream_frame &f = *frame;
+      std::memset(&f, 0, sizeof f);
+      f.pos = rx.st.pre_pos;
+      f.end = rx.st.frame_end;
+      const int64_t len = rx.st.frame_end - rx.st.pre_pos;
+      amod_result &r = f.result;
+      if (rx.st.pre_pos < lv->tw - cap) { // getRange -> null: a frame error, nothing decoded
+        r.status = AMOD_E_STREAM_LOST; r.preamble_idx = -1; r.coarse_idx = -1; r.frame_type = -1;
+        f.window_len = 0;
+        ++lv->frame_errors;
+        rx.reset();
+      } else {
+        f.window_len = (int32_t)len;
+        lv->win.resize((size_t)len);
+        float mx = 0.f;
+        for (int64_t i = 0; i < len; ++i) {
+          const float v = (float)rx.S(rx.st.pre_pos + i);
+          lv->win[(size_t)i] = v;
+          mx = std::max(mx, std::fabs(v));
+        }
+        if ((double)mx > 1e-6) // per-window peak normalisation (app.js:918-925)
+          for (auto &v : lv->win) v = (float)((double)v / (double)mx);
+        const int64_t stride = amod_payload_stride(&lv->cfg, std::max<int64_t>(len, 1));
+        lv->pay.assign((size_t)stride, 0);
+        const int64_t off0 = 0;
+        const int32_t len32 = (int32_t)len;
+        const int rc = amod_decode_host(lv->ctx, &lv->cfg, AMOD_MODE_CHUNK, lv->win.data(), len, &off0, &len32, 1, &r,
+                                        lv->pay.data(), stride, 0);
+        if (rc) return rc;
+        rx.reset();
+        if (r.status != AMOD_OK) {
+          ++lv->frame_errors;
+        } else {
+          ++lv->frames_decoded;
+          const uint8_t *sl = lv->pay.data();
+          if (r.frame_type == 0xFE) {
+            if (!r.crc_valid) {
+              ++lv->frame_errors;
+            } else {
+              const int mr = amod_asm_metadata(lv->assembler, r.total_chunks, r.total_size, r.chunk_size, sl + r.name_off,
+                                               r.name_len);
+              if (mr == AMOD_ASM_RANGE_ERROR) ++lv->frame_errors;
+              apply_meta(r, rx.st);
+            }
+          } else if (r.frame_type == 0xFF) {
+            const int c = amod_asm_chunk(lv->assembler, r.seq_num, sl + r.data_off, r.data_len, r.crc_valid);
+            if (c < 0) return amod_ctx_fail(lv->ctx, "assembler store", c);
+          }
+        }
+      }
+      *has_frame = 1;
+    }
+    break;
+  }
+  return AMOD_SUCCESS;
+}
+
+extern "C" int amod_live_state(const amod_live *lv, amod_stream_state *state, amod_live_stats *stats) {
+  if (!lv) return amod_ctx_fail(nullptr, "invalid argument", AMOD_ERR_ARG);
+  if (state) { to_state(lv->rx.st, *state); state->block = lv->block; }
+  if (stats) {
+    stats->total_written = lv->tw;
+    stats->frames_decoded = lv->frames_decoded;
+    stats->frame_errors = lv->frame_errors;
+    stats->refine_fails = (int64_t)lv->fails.size();
+    stats->last_refine_fail = lv->fails.empty() ? -1 : lv->fails.back().second;
+    stats->fine_host_positions = lv->rx.fine_host;
+  }
+  return AMOD_SUCCESS;
+}
+
+extern "C" int64_t amod_live_refine_fails(const amod_live *lv, int64_t *pos, int64_t max) {
+  if (!lv) return -1;
+  for (size_t i = 0; i < lv->fails.size() && (int64_t)i < max; ++i) pos[i] = lv->fails[i].second;
+  return (int64_t)lv->fails.size();
+}
+
+extern "C" void amod_live_close(amod_live *lv) {
+  if (!lv) return;
+  if (lv->own_assembler) amod_asm_close(lv->assembler);
+  delete lv;
 }

@@ -437,38 +437,77 @@ const STREAM_REC = 24 + REC; // sizeof(amod_stream_frame)
 // (706-998) over a recorded stream fed in 4096-sample blocks (GPU pre-pass + decode,
 // host state machine); every demodulated window with decodeChunkFrame's outcome
 // (payload bytes go to the assembler, as _demodulateFrame does). Additive API.
+// one amod_stream_frame record -> {preambleGlobalPos, expectedFrameEnd, length, result}
+function streamFrame(view, b) {
+  const g = (k) => view.getInt32(b + 24 + 4 * k, true);
+  const status = g(0), frameType = g(3), aux = g(4);
+  let result;
+  if (status === 0 && frameType === FRAME_META) {
+    result = { frameType, totalChunks: g(11), totalFileSize: g(12), chunkSize: g(13), crcValid: g(16) !== 0 };
+  } else if (status === 0) {
+    result = { frameType, seqNum: g(10), dataLen: g(9), crcValid: g(16) !== 0 };
+  } else if (status === E_STREAM_LOST) {
+    result = { error: 'window left the ring buffer' };
+  } else if (status === E_INVALID_LEN) {
+    result = { error: `Invalid data length: ${aux}` };
+  } else if (status === E_UNKNOWN_TYPE) {
+    result = { error: `Unknown frame type: 0x${aux.toString(16)}`, frameType: aux };
+  } else {
+    result = { error: ERR[status] };
+  }
+  return {
+    preambleGlobalPos: Number(view.getBigInt64(b, true)), expectedFrameEnd: Number(view.getBigInt64(b + 8, true)),
+    length: view.getInt32(b + 16, true), result,
+  };
+}
+
 async function receiveStream(samples, modName, repetition, opts) {
   const o = opts || {};
   const asm = o.assembler || new ChunkAssembler();
   const r = native.receiveStream(asFloat32(samples), nativeCfg(modName, repetition), asm._h, o.device | 0);
   const view = new DataView(r.frames);
   const frames = [];
-  for (let i = 0; i < r.nframes; i++) {
-    const b = i * STREAM_REC, g = (k) => view.getInt32(b + 24 + 4 * k, true);
-    const status = g(0), frameType = g(3), aux = g(4);
-    let result;
-    if (status === 0 && frameType === FRAME_META) {
-      result = { frameType, totalChunks: g(11), totalFileSize: g(12), chunkSize: g(13), crcValid: g(16) !== 0 };
-    } else if (status === 0) {
-      result = { frameType, seqNum: g(10), dataLen: g(9), crcValid: g(16) !== 0 };
-    } else if (status === E_STREAM_LOST) {
-      result = { error: 'window left the ring buffer' };
-    } else if (status === E_INVALID_LEN) {
-      result = { error: `Invalid data length: ${aux}` };
-    } else if (status === E_UNKNOWN_TYPE) {
-      result = { error: `Unknown frame type: 0x${aux.toString(16)}`, frameType: aux };
-    } else {
-      result = { error: ERR[status] };
-    }
-    frames.push({
-      preambleGlobalPos: Number(view.getBigInt64(b, true)), expectedFrameEnd: Number(view.getBigInt64(b + 8, true)),
-      length: view.getInt32(b + 16, true), result,
-    });
-  }
+  for (let i = 0; i < r.nframes; i++) frames.push(streamFrame(view, i * STREAM_REC));
   return {
     frames, refineFail: Array.from(r.refineFail), framesDecoded: Number(r.framesDecoded),
     frameErrors: Number(r.frameErrors), assembler: asm,
   };
+}
+
+// app.js StreamingReceiver (706-998) driven live: processAudioBlock(inputSamples) once
+// per audio callback (app.js:1108-1112), as startStreamingReceive does. DC removal, ring
+// buffer and one state-machine step per call on the host; a completed window is decoded
+// on the GPU and handed to this.assembler before the call returns. Returns the
+// demodulated window ({preambleGlobalPos, expectedFrameEnd, length, result}) or null,
+// and calls opts.onFrame with it. Fields mirror the reference's (state, acScanPos, ...).
+const RECV_STATE = { IDLE: 0, PREAMBLE_DETECTED: 1, COLLECTING_FRAME: 2, DEMODULATING: 3 };
+class StreamingReceiver {
+  constructor(modName, repetition, opts) {
+    const o = opts || {};
+    this.modName = modName;
+    this.repetition = repetition;
+    this.assembler = o.assembler || new ChunkAssembler();
+    this.onFrame = o.onFrame || null;
+    this._h = native.liveOpen(nativeCfg(modName, repetition), this.assembler._h, o.device | 0);
+    this.startTime = Date.now();
+  }
+  processAudioBlock(inputSamples) {
+    const ab = native.liveProcess(this._h, asFloat32(inputSamples));
+    if (!ab) return null;
+    const frame = streamFrame(new DataView(ab), 0);
+    if (this.onFrame) this.onFrame(frame);
+    return frame;
+  }
+  _st() { return native.liveState(this._h); }
+  get state() { return this._st().state; }
+  get acScanPos() { return this._st().acScanPos; }
+  get preambleGlobalPos() { return this._st().preambleGlobalPos; }
+  get expectedFrameEnd() { return this._st().expectedFrameEnd; }
+  get metaReceived() { return this._st().metaReceived !== 0; }
+  get framesDecoded() { return this._st().framesDecoded; }
+  get frameErrors() { return this._st().frameErrors; }
+  get totalWritten() { return this._st().totalWritten; }
+  cleanup() { this.assembler.cleanup(); }
 }
 
 const api = {
@@ -476,6 +515,7 @@ const api = {
   decodeReceivedSignal, FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame, decodeChunkFrame,
   estimateFrameSamples, generateSweepTone, generateTestSignal, analyzeLoopback,
   decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native, ChunkAssembler, receiveStream,
+  StreamingReceiver, RECV_STATE,
 };
 
 module.exports = api;

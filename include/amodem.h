@@ -346,6 +346,30 @@ int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float *samples, 
                       uint8_t *payload, int64_t stride, int64_t *fails, int64_t max_fails, int64_t *nfails,
                       double *ema, amod_stream_state *end);
 
+/* ---- live streaming receive: StreamingReceiver.processAudioBlock (app.js:749-773) ----
+ * One call per audio callback block (any length; the reference's ScriptProcessor hands
+ * 4096 samples): DC removal, ring buffer, one step of the receiver's state machine.
+ * When the step demodulates a window (_demodulateFrame, app.js:907-972), *has_frame = 1
+ * and *frame holds it (decoded on the GPU, dispatched to the assembler before return).
+ * Fed the blocks of a recorded stream, the frames equal amod_stream_receive's. */
+typedef struct amod_live amod_live;
+typedef struct amod_live_stats {
+  int64_t total_written;       /* ringBuffer.totalWritten                             */
+  int64_t frames_decoded, frame_errors; /* the receiver's counters                    */
+  int64_t refine_fails;        /* _refineAndCollect false positives (back to idle)    */
+  int64_t last_refine_fail;    /* preambleGlobalPos of the last one, or -1            */
+  int64_t fine_host_positions; /* cross-correlation positions evaluated              */
+} amod_live_stats;
+/* assembler NULL: a private one (closed with the receiver) */
+int amod_live_open(amod_ctx *ctx, const amod_cfg *cfg, amod_assembler *assembler, amod_live **out);
+int amod_live_process_block(amod_live *lv, const float *samples, int64_t n, amod_stream_frame *frame,
+                            int32_t *has_frame);
+int amod_live_state(const amod_live *lv, amod_stream_state *state, amod_live_stats *stats);
+/* positions of the failed refinements so far (up to max); returns their count */
+int64_t amod_live_refine_fails(const amod_live *lv, int64_t *pos, int64_t max);
+void amod_live_close(amod_live *lv);
+
+
 /* deterministic synthetic payload (xorshift32, 4 bytes per step, little-endian) */
 void amod_synth_payload(uint32_t seed, int32_t len, uint8_t *out);
 /* nframes legacy frames of payload_len bytes each (seed 0x9E3779B9 ^ (first+i), name),

@@ -83,6 +83,24 @@ async function main() {
           };
           break;
         }
+        case 'live': { // processAudioBlock per 4096-sample block, as the audio callback drives it
+          const x = f32(j.file);
+          const rx = new M.StreamingReceiver(j.mod, j.rep);
+          const frames = [];
+          for (let b = 0; b < x.length; b += 4096) {
+            const f = rx.processAudioBlock(x.subarray(b, b + 4096));
+            if (f) frames.push(f);
+          }
+          const a = rx.assembler;
+          r = {
+            frames, framesDecoded: rx.framesDecoded, frameErrors: rx.frameErrors, acScanPos: rx.acScanPos,
+            state: rx.state, totalWritten: rx.totalWritten,
+            asm: { totalChunks: a.totalChunks, totalFileSize: a.totalFileSize, chunkSize: a.chunkSize,
+              fileName: a.fileName, receivedCount: a.receivedCount, crcErrors: a.crcErrors, complete: a.isComplete() },
+            file: a.totalChunks > 0 ? sha(await a.assembleFile()) : null,
+          };
+          break;
+        }
         default: throw new Error('unknown op ' + j.op);
       }
       out[j.id] = { ok: enc(r) };

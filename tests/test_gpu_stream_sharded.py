@@ -20,21 +20,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _stream(n_chunks, chunk=1024):
+def _stream(n_chunks, chunk=1024, second=None):
+    """Metadata + n_chunks data frames with varying gaps. second = (after, n2, chunk2):
+    after `after` chunks a second file starts mid-stream (its metadata frame changes
+    the chunk size, hence every later window length); data = the file the stream ends with."""
     import amodem
-    from amodem import _lib as L
     cfg = amodem.preset("standard", "QPSK", 1)
     data = amodem.synth_payload(0x5AD, n_chunks * chunk - 77)
     parts = [np.zeros(3000, np.float32), amodem.build_metadata_frame(n_chunks, len(data), chunk, "sh.bin", cfg=cfg)]
-    for i in range(n_chunks):
+    last = n_chunks if second is None else second[0]
+    for i in range(last):
         parts.append(amodem.build_data_chunk_frame(data[i * chunk:(i + 1) * chunk], i, cfg=cfg))
         parts.append(np.zeros((i * 1231) % 5000, np.float32))
+    if second is not None:
+        _, n2, c2 = second
+        data = amodem.synth_payload(0x5AE, n2 * c2 - 5)
+        parts.append(amodem.build_metadata_frame(n2, len(data), c2, "two.bin", cfg=cfg))
+        # the metadata frame's window is cut with the old (data-frame) length: silence
+        # after it, so the receiver does not resume past the next frame's preamble
+        parts.append(np.zeros(60000, np.float32))
+        for i in range(n2):
+            parts.append(amodem.build_data_chunk_frame(data[i * c2:(i + 1) * c2], i, cfg=cfg))
+            parts.append(np.zeros((i * 733) % 4000, np.float32))
     x = np.concatenate(parts + [np.zeros(30000, np.float32)])
     x = np.concatenate([x, np.zeros(-len(x) % 4096, np.float32)])
     return cfg, x, data
 
 
-def _worker(rank, world, port, out, n_chunks):
+def _worker(rank, world, port, out, n_chunks, second=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "audio-modem_amd"))
@@ -43,7 +56,7 @@ def _worker(rank, world, port, out, n_chunks):
     from amodem import shard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg, x, data = _stream(n_chunks)
+    cfg, x, data = _stream(n_chunks, second=second)
     dm = amodem.Demodulator(0)
     asm = amodem.ChunkAssembler() if rank == 0 else None
     res = shard.stream_receive_sharded(dm, cfg, lambda lo, hi: x[lo:hi], len(x), rank, world, assembler=asm)
@@ -99,3 +112,19 @@ def test_sharded_stream_equals_single(tmp_path, world, n_chunks):
     assert rec["n"] == n_chunks + 1 and rec["fails"] == rec["ref_fails"] and rec["warn"] == []
     assert [rec["counters"]["frames_decoded"], rec["counters"]["frame_errors"]] == rec["ref_counters"]
     assert rec["file_ok"] and rec["ref_file_ok"]
+
+
+def test_sharded_stream_second_file_mid_stream(tmp_path):
+    """A second metadata frame (a new file with a larger chunk size) lands inside rank 1's
+    shard: the windows the shards cut after it with the old length are dropped and rank 0
+    re-runs the rest with the new one; the merged trajectory still equals the
+    single-process receiver's, which rolls back the same way (stream.cpp)."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res.json")
+    mp.spawn(_worker, args=(2, _free_port(), out, 60, (40, 12, 2048)), nprocs=2, join=True)
+    rec = json.load(open(out))
+    assert rec["same_frames"], rec["diffs"]
+    assert rec["n"] == rec["n_ref"] == 40 + 1 + 12 + 1 and rec["fails"] == rec["ref_fails"]
+    assert [rec["counters"]["frames_decoded"], rec["counters"]["frame_errors"]] == rec["ref_counters"]
+    assert rec["file_ok"] and rec["ref_file_ok"]
+    assert any("metadata change" in w for w in rec["warn"])

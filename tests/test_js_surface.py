@@ -316,3 +316,39 @@ def test_receive_stream_through_js(tmp_path):
                                                                                  "fileName")], name
         if sp["offered"] is not None:
             assert g["file"] == sp["offered"]["sha256"], name
+
+
+@pytest.mark.gpu
+def test_live_receiver_through_js(tmp_path):
+    """StreamingReceiver.processAudioBlock from JS, one 4096-sample block per call (the
+    reference's audio callback, app.js:1108-1112), on the golden streams: the windows,
+    outcomes, counters, final scan position and assembled file equal the reference's."""
+    from test_gpu_stream import build_stream, streams
+    jobs, want = [], {}
+    for sp in streams():
+        _, x, _ = build_stream(sp)
+        p = tmp_path / f"{sp['name']}.f32"
+        x.astype(np.float32).tofile(p)
+        jobs.append({"op": "live", "file": str(p), "mod": sp["mod"], "rep": sp["rep"], "config": sp["config"],
+                     "id": sp["name"]})
+        want[sp["name"]] = sp
+    res = run(jobs, tmp_path)
+    for name, sp in want.items():
+        g = ok(res, name)
+        got = [{"pos": f["preambleGlobalPos"], "end": f["expectedFrameEnd"], "len": f["length"],
+                **({"error": f["result"]["error"]} if "error" in f["result"] else
+                   {k: v for k, v in f["result"].items() if k in ("frameType", "crcValid", "seqNum", "dataLen",
+                                                                   "totalChunks", "chunkSize")})}
+               for f in g["frames"]]
+        assert got == [{k: v for k, v in w.items() if k != "fileName"} for w in sp["frames"]], name
+        assert (g["framesDecoded"], g["frameErrors"]) == (sp["framesDecoded"], sp["frameErrors"]), name
+        assert (g["state"], g["acScanPos"]) == (sp["final"]["state"], sp["final"]["acScanPos"]), name
+        assert g["totalWritten"] == sp["n"], name
+        a = sp["assembler"]
+        assert [g["asm"][k] for k in ("totalChunks", "totalFileSize", "chunkSize", "receivedCount", "crcErrors",
+                                      "complete", "fileName")] == [a[k] for k in ("totalChunks", "totalFileSize",
+                                                                                 "chunkSize", "receivedCount",
+                                                                                 "crcErrors", "complete",
+                                                                                 "fileName")], name
+        if sp["offered"] is not None:
+            assert g["file"] == sp["offered"]["sha256"], name
