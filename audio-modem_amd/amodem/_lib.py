@@ -154,6 +154,12 @@ SIGNATURES = {
                                     C.POINTER(C.c_int64), _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_int64), _P,
                                     C.POINTER(StreamState)]),
     "amod_synth_legacy_packets": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32, _P, _P, _P]),
+    "amod_group_open": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
+    "amod_group_close": (C.c_int, [_P]),
+    "amod_group_size": (C.c_int32, [_P]),
+    "amod_group_context": (_P, [_P, C.c_int32]),
+    "amod_group_decode_host": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P, _P,
+                                         C.c_int64, C.c_uint32, _P]),
     "amod_live_open": (C.c_int, [_P, C.POINTER(Cfg), _P, C.POINTER(_P)]),
     "amod_live_process_block": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_int32)]),
     "amod_live_state": (C.c_int, [_P, C.POINTER(StreamState), C.POINTER(LiveStats)]),

@@ -463,6 +463,46 @@ def _asm_check(rc):
     return rc
 
 
+class DeviceGroup:
+    """Several GPUs from one process (amod_group_*): decode_batch cuts a batch into
+    contiguous frame ranges of about equal sample counts, one per device, decoded at once;
+    results come back in frame order. devices may repeat (two contexts on one GPU)."""
+
+    def __init__(self, devices):
+        self._L = L.load()
+        ids = np.ascontiguousarray(devices, np.int32)
+        h = C.c_void_p()
+        L.check(self._L.amod_group_open(ids.ctypes.data, len(ids), C.byref(h)))
+        self._h = h
+        self.devices = [int(d) for d in ids]
+
+    def decode_batch(self, samples, offsets, lengths, cfg: L.Cfg, mode: int = L.MODE_RECEIVED, options: int = 0):
+        """-> (RESULT_DTYPE records, payload uint8 [n, stride], frames per device)."""
+        x = np.ascontiguousarray(samples, np.float32)
+        off = np.ascontiguousarray(offsets, np.int64)
+        ln = np.ascontiguousarray(lengths, np.int32)
+        n = len(off)
+        stride = payload_stride(cfg, int(ln.max()) if n else 1)
+        rec = np.zeros(n, RESULT_DTYPE)
+        pay = np.zeros((n, stride), np.uint8)
+        split = np.zeros(len(self.devices), np.int32)
+        L.check(self._L.amod_group_decode_host(self._h, C.byref(cfg), mode, x.ctypes.data, len(x), off.ctypes.data,
+                                               ln.ctypes.data, n, rec.ctypes.data, pay.ctypes.data, stride, options,
+                                               split.ctypes.data))
+        return rec, pay, split.tolist()
+
+    def close(self):
+        if self._h:
+            self._L.amod_group_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class StreamingReceiver:
     """app.js StreamingReceiver (706-998) driven live, one audio block per call
     (processAudioBlock, 749-773): DC removal, ring buffer and one state-machine step on

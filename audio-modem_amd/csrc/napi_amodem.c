@@ -37,6 +37,7 @@
 
 #define MAX_DEVICES 16
 static amod_ctx *g_ctx[MAX_DEVICES];
+static amod_group *g_group[MAX_DEVICES + 1]; /* devices 0 .. n-1, opened on first use */
 
 #define NAPI_TRY(env, call)                                                 \
   do {                                                                      \
@@ -134,6 +135,7 @@ static int is_nullish(napi_env env, napi_value v) {
 typedef struct {
   amod_ctx *ctx;
   amod_cfg cfg;
+  amod_group *group; /* decodeBatch(..., {devices: n > 1}): the batch split across n GPUs */
   int32_t mode, nframes;
   uint32_t options;
   const float *samples;
@@ -154,11 +156,11 @@ typedef struct {
 
 /* parse args into a job; allocates offsets/lengths and the output ArrayBuffers */
 static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_value argv_out[3]) {
-  size_t argc = 7;
-  napi_value argv[7];
+  size_t argc = 8;
+  napi_value argv[8];
   memset(j, 0, sizeof *j);
   if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 6) {
-    napi_throw_type_error(env, NULL, "decode(samples, offsets, lengths, cfg, mode, options[, device])");
+    napi_throw_type_error(env, NULL, "decode(samples, offsets, lengths, cfg, mode, options[, device[, ndevices]])");
     return 0;
   }
   void *sp;
@@ -177,8 +179,26 @@ static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_va
   if (napi_get_value_uint32(env, argv[5], &j->options) != napi_ok) j->options = 0;
   int32_t device = 0;
   if (argc >= 7 && !is_nullish(env, argv[6]) && napi_get_value_int32(env, argv[6], &device) != napi_ok) device = 0;
-  j->ctx = get_ctx(env, device);
-  if (!j->ctx) return 0;
+  int32_t ndev = 1;
+  if (argc >= 8 && !is_nullish(env, argv[7]) && napi_get_value_int32(env, argv[7], &ndev) != napi_ok) ndev = 1;
+  if (ndev > 1) {
+    if (ndev > MAX_DEVICES) return napi_throw_range_error(env, NULL, "devices out of range"), 0;
+    if (!g_group[ndev]) {
+      int32_t ids[MAX_DEVICES];
+      for (int32_t i = 0; i < ndev; ++i) ids[i] = i;
+      /* AMODEM_GROUP_DEVICES="0,0": the device list to use instead (tests on one GPU) */
+      const char *lst = getenv("AMODEM_GROUP_DEVICES");
+      for (int32_t i = 0; lst && *lst && i < ndev; ++i) {
+        ids[i] = (int32_t)strtol(lst, (char **)&lst, 10);
+        if (*lst == ',') ++lst;
+      }
+      if (amod_group_open(ids, ndev, &g_group[ndev]) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(NULL)), 0;
+    }
+    j->group = g_group[ndev];
+  } else {
+    j->ctx = get_ctx(env, device);
+    if (!j->ctx) return 0;
+  }
 
   if (is_nullish(env, argv[1])) { /* one frame: the whole buffer */
     j->nframes = 1;
@@ -234,10 +254,15 @@ static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_va
 }
 
 static void run_decode(decode_job *j) {
-  j->rc = amod_decode_host(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths, j->nframes,
-                           (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options);
+  if (j->group)
+    j->rc = amod_group_decode_host(j->group, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths,
+                                   j->nframes, (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options,
+                                   NULL);
+  else
+    j->rc = amod_decode_host(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths, j->nframes,
+                             (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options);
   if (j->rc != AMOD_SUCCESS) {
-    const char *e = amod_last_error(j->ctx);
+    const char *e = amod_last_error(j->group ? NULL : j->ctx);
     snprintf(j->err, sizeof j->err, "libamodem error %d: %s", j->rc, e ? e : "");
   }
 }

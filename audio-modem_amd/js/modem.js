@@ -320,15 +320,18 @@ function decodeChunkFrame(frameSamples, modName, repetition) {
   return decodeOne(frameSamples, modName, repetition, MODE_CHUNK);
 }
 
-// decodeBatch(samples, frameOffsets, frameLens, modName, rep, {device, mode})
-// -> Promise<result[]>: many frames of one buffer in one GPU launch (additive API).
+// decodeBatch(samples, frameOffsets, frameLens, modName, rep, {device, devices, mode})
+// -> Promise<result[]>: many frames of one buffer in one GPU launch (additive API);
+// devices: n > 1 splits the batch into contiguous frame ranges over GPUs 0 .. n-1,
+// decoded concurrently (amod_group_decode_host), results in frame order.
 function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
   const o = opts || {};
   const mode = o.mode === 'chunk' || o.mode === MODE_CHUNK ? MODE_CHUNK : MODE_RECEIVED;
   const cfg = nativeCfg(modName, rep);
   const offs = frameOffsets instanceof Float64Array ? frameOffsets : Float64Array.from(frameOffsets);
   const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
-  return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0)
+  return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0,
+    Math.max(1, o.devices | 0))
     .then((out) => {
       const view = new DataView(out.results);
       const res = new Array(lens.length);

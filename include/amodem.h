@@ -275,6 +275,21 @@ int64_t amod_asm_name(const amod_assembler *a, uint8_t *out, int64_t cap);
 int64_t amod_asm_missing(const amod_assembler *a, int32_t *out, int64_t cap);
 int64_t amod_asm_file(const amod_assembler *a, uint8_t *out, int64_t cap);
 
+/* ---- several GPUs from one host process ----
+ * A group holds one context per listed device (a device may repeat). amod_group_decode_host
+ * decodes a batch like amod_decode_host, cut into contiguous frame ranges of about equal
+ * sample counts, one per device, all devices at once; every range's results and payload
+ * rows land in the caller's arrays at their frame index (per-device D2H, no gather step).
+ * frames_per_device (optional, group-size entries): the split used. */
+typedef struct amod_group amod_group;
+int amod_group_open(const int32_t *devices, int32_t ndev, amod_group **out);
+int amod_group_close(amod_group *g);
+int32_t amod_group_size(const amod_group *g);
+amod_ctx *amod_group_context(amod_group *g, int32_t i);
+int amod_group_decode_host(amod_group *g, const amod_cfg *cfg, int32_t mode, const float *samples, int64_t nsamples,
+                           const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
+                           uint8_t *payload, int64_t payload_stride, uint32_t options, int32_t *frames_per_device);
+
 /* ---- streaming receive: app.js StreamingReceiver (706-998) over a recorded stream ----
  * The stream is cut into 4096-sample blocks (the ScriptProcessor size; a last partial
  * block is completed with zeros) and run through the reference's receiver: EMA DC

@@ -48,7 +48,8 @@ async function main() {
         case 'decode': r = M.decodeReceivedSignal(f32(j.file), j.mod, j.rep); break;
         case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
         case 'loopback': r = M.analyzeLoopback(f32(j.file), j.mod, j.rep, Uint8Array.from(j.testData)); break;
-        case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { mode: j.mode }); break;
+        case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep,
+          { mode: j.mode, devices: j.devices }); break;
         case 'asm': {
           // one ChunkAssembler scenario (tests/golden/assembler.json ops); state after each op
           const a = new M.ChunkAssembler(j.directory ? { directory: j.directory } : undefined);

@@ -1,0 +1,55 @@
+"""Several GPUs from one process (amod_group_decode_host; decodeBatch {devices: n}): the
+batch is cut into contiguous frame ranges of about equal sample counts, one per context,
+decoded at once. On the one-GPU test box the group holds repeated contexts of device 0
+(separate streams and workspaces, the same code path as distinct devices). Results must
+equal the single-context decode frame for frame, in frame order, whatever the split."""
+import numpy as np
+import pytest
+
+import amodem
+from amodem import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch():
+    cfg = amodem.preset("standard", "QPSK", 1)
+    xs, offs, lens = [], [], []
+    base = 0
+    for k, plen in enumerate([64, 1024, 300, 2000, 17, 900] * 20):
+        x, o, l = amodem.synth_legacy_batch(cfg, 1, payload_len=plen, threads=1)
+        xs.append(x)
+        offs.append(base + int(o[0]))
+        lens.append(int(l[0]))
+        base += len(x)
+    return cfg, np.concatenate(xs), np.array(offs, np.int64), np.array(lens, np.int32)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_group_equals_single_context(devices):
+    cfg, x, offs, lens = _batch()
+    dm = amodem.Demodulator(0)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    dm.close()
+    g = amodem.DeviceGroup(devices)
+    rec, pay, split = g.decode_batch(x, offs, lens, cfg)
+    # frames out of buffer order (offsets permuted): the same results at the same indices
+    perm = np.random.default_rng(1).permutation(len(offs))
+    rec2, pay2, _ = g.decode_batch(x, offs[perm], lens[perm], cfg)
+    g.close()
+    assert sum(split) == len(offs) and len(split) == len(devices)
+    if len(devices) > 1:
+        assert min(split) > 0
+    # reference-visible fields (flags / coarse_idx / fine_metric / payload_valid say how the
+    # engine produced a result: they may follow the launch's workspace capacities)
+    vis = [n for n in amodem.RESULT_DTYPE.names
+           if n not in ("flags", "payload_valid", "fine_metric", "coarse_idx", "reserved")]
+    for n in vis:
+        assert (rec[n] == ref[n]).all(), n
+        assert (rec2[n] == ref[n][perm]).all(), n
+    for i in range(len(offs)):
+        k = min(int(ref["payload_valid"][i]), int(rec["payload_valid"][i]),
+                int(rec2["payload_valid"][np.nonzero(perm == i)[0][0]]))
+        assert pay[i, :k].tobytes() == rpay[i, :k].tobytes()
+        assert pay2[np.nonzero(perm == i)[0][0], :k].tobytes() == rpay[i, :k].tobytes()
+    assert (ref["status"] == 0).all()

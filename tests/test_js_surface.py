@@ -34,12 +34,13 @@ GLOBALS = ["fft", "OFDM_CONFIGS", "OFDM", "setOFDMConfig", "Constellations", "ge
            "generateTestSignal", "analyzeLoopback"]
 
 
-def run(jobs, tmp_path, timeout=600):
+def run(jobs, tmp_path, timeout=600, env=None):
     for i, j in enumerate(jobs):
         j.setdefault("id", str(i))
     p = tmp_path / "jobs.json"
     p.write_text(json.dumps(jobs))
-    out = subprocess.run([NODE, DRIVER, str(p)], capture_output=True, text=True, timeout=timeout)
+    out = subprocess.run([NODE, DRIVER, str(p)], capture_output=True, text=True, timeout=timeout,
+                         env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stderr[-2000:]
     return json.loads(out.stdout)
 
@@ -352,3 +353,27 @@ def test_live_receiver_through_js(tmp_path):
                                                                                  "fileName")], name
         if sp["offered"] is not None:
             assert g["file"] == sp["offered"]["sha256"], name
+
+
+@pytest.mark.gpu
+def test_decode_batch_devices_through_js(tmp_path):
+    """decodeBatch(..., {devices: 2}) splits the batch over two GPU contexts
+    (amod_group_decode_host; on the one-GPU box both on device 0 via AMODEM_GROUP_DEVICES):
+    the reference result objects, in frame order, as with one device."""
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["rep"] == 1
+           and f["mod"] in ("QPSK", "BPSK")]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    groups = {}
+    for f in sel:
+        groups.setdefault(f["mod"], []).append(sel.index(f))
+    jobs = []
+    for mod, idx in groups.items():
+        jobs.append({"op": "decode_batch", "config": "standard", "file": str(fn), "offsets": [offs[i] for i in idx],
+                     "lengths": [len(xs[i]) for i in idx], "mod": mod, "rep": 1, "devices": 2, "id": mod})
+    res = run(jobs, tmp_path, env={"AMODEM_GROUP_DEVICES": "0,0"})
+    for mod, idx in groups.items():
+        assert ok(res, mod) == [sel[i]["result"] for i in idx], mod
