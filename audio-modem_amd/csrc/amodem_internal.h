@@ -251,31 +251,44 @@ __device__ inline uint32_t voted_byte(const uint32_t *raw, int i, int rep) {
 // nbytes bytes, given that the first `avail` are known. The answer only ever
 // grows as more bytes become known; the parse is final once it is <= avail.
 // Reads exactly the bytes parse_stream branches on (modem.js:607-640, 793-849).
-__device__ inline int parse_need(const uint32_t *raw, int rep, int avail, int nbytes, int mode) {
+// *final: the value no longer depends on bytes past `avail` (the header is decoded)
+__device__ inline int parse_need(const uint32_t *raw, int rep, int avail, int nbytes, int mode, bool *final = nullptr) {
+  bool fin = true;
+  int r;
   const int min_bytes = mode == AMOD_MODE_CHUNK ? 6 : 10;
-  if (nbytes < min_bytes) return 0;
-  if (avail < 1) return 1;
-  const int t = (int)voted_byte(raw, 0, rep);
-  if (t == 0xFE) {
-    if (nbytes < 16) return 1;
-    if (avail < 12) return 12;
-    const int nl = (int)voted_byte(raw, 11, rep);
-    return 12 + nl + 4 > nbytes ? 12 : 12 + nl + 4;
+  if (nbytes < min_bytes) r = 0;
+  else if (avail < 1) { r = 1; fin = false; }
+  else {
+    const int t = (int)voted_byte(raw, 0, rep);
+    if (t == 0xFE) {
+      if (nbytes < 16) r = 1;
+      else if (avail < 12) { r = 12; fin = false; }
+      else {
+        const int nl = (int)voted_byte(raw, 11, rep);
+        r = 12 + nl + 4 > nbytes ? 12 : 12 + nl + 4;
+      }
+    } else if (t == 0xFF) {
+      if (nbytes < 11) r = 1;
+      else if (avail < 7) { r = 7; fin = false; }
+      else {
+        const int dl = (int)((voted_byte(raw, 5, rep) << 8) | voted_byte(raw, 6, rep));
+        r = 7 + dl + 4 > nbytes ? 7 : 7 + dl + 4;
+      }
+    } else if (mode == AMOD_MODE_CHUNK) {
+      r = 1;
+    } else {
+      const int nl = t;
+      if (1 + nl + 8 > nbytes) r = 1;
+      else if (avail < 1 + nl + 4) { r = 1 + nl + 4; fin = false; }
+      else {
+        int32_t dl = 0;
+        for (int q = 0; q < 4; ++q) dl = (int32_t)(((uint32_t)dl << 8) | voted_byte(raw, 1 + nl + q, rep));
+        r = (dl <= 0 || (int64_t)1 + nl + 4 + dl + 4 > nbytes) ? 1 + nl + 4 : 1 + nl + 4 + dl + 4;
+      }
+    }
   }
-  if (t == 0xFF) {
-    if (nbytes < 11) return 1;
-    if (avail < 7) return 7;
-    const int dl = (int)((voted_byte(raw, 5, rep) << 8) | voted_byte(raw, 6, rep));
-    return 7 + dl + 4 > nbytes ? 7 : 7 + dl + 4;
-  }
-  if (mode == AMOD_MODE_CHUNK) return 1;
-  const int nl = t;
-  if (1 + nl + 8 > nbytes) return 1;
-  if (avail < 1 + nl + 4) return 1 + nl + 4;
-  int32_t dl = 0;
-  for (int q = 0; q < 4; ++q) dl = (int32_t)(((uint32_t)dl << 8) | voted_byte(raw, 1 + nl + q, rep));
-  if (dl <= 0 || (int64_t)1 + nl + 4 + dl + 4 > nbytes) return 1 + nl + 4;
-  return 1 + nl + 4 + dl + 4;
+  if (final) *final = fin;
+  return r;
 }
 
 // Workgroup CRC-32 (modem.js:443-457) of bytes [0, L) of stream v.

@@ -54,7 +54,8 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone)
 #endif
 #ifndef AMOD_DEMOD_WPE
-#define AMOD_DEMOD_WPE 5                     // k_demod: 96 registers, no spills
+#define AMOD_DEMOD_WPE 4                     // k_demod: 112 registers, no VGPR spills (at 5 waves /
+                                             // 96 registers it spilled 37: -13 % chain time)
 #endif
 
 // Dynamic LDS of k_detect, sized per launch (amod_fast_lds_bytes): one region reused
@@ -1309,6 +1310,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
 
   // next frame on the demodulation path at or after wave-iteration k (frames last-first)
   auto next_frame = [&](int k, FrameS &F) -> int {
+    FRESH_ARGS;
     for (; k < nfr; k += wstride) {
       const int f = w.f1 - 1 - k;
       const DetRec d = sload(w.det + f);
@@ -1348,20 +1350,24 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   int sflags = 0;  // DEMAP / PHASE of flag_sym and later: only if the parse reads them
   const int rep = cfg.rep;
   // bytes the parse reads once `dsym` data symbols are demodulated (-1: more needed)
-  auto eval_need = [&](const FrameS &F, int dsym) -> int {
+  // (-1 - need: more bytes needed; with *hdr = 1 the header is decoded, so `need` is final)
+  auto eval_need = [&](const FrameS &F, int dsym, int *hdr = nullptr) -> int {
     const int nbits = F.M * per_sym;
-    int need = 0;
+    int need = 0, fin = 0;
     if (lane == 0) {
       const int avail = (min(dsym * per_sym, nbits) / rep) >> 3;
-      need = parse_need(bits, rep, avail, (nbits / rep) >> 3, cfg.mode);
+      bool f = false;
+      need = parse_need(bits, rep, avail, (nbits / rep) >> 3, cfg.mode, &f);
+      fin = f;
       if (need > avail) need = -1 - need;
     }
+    if (hdr) *hdr = __builtin_amdgcn_readfirstlane(fin);
     return __builtin_amdgcn_readfirstlane(need);
   };
   // one job of frame `cur` (jcur = 0 starts the frame; a frame without data symbols has
   // one empty job, so every frame passes through its frame end)
-  // c1 / c2: the job's samples; issue_next() refills them with the next job's once the
-  // FFT has consumed them, so those loads fly under this job's equalise / demap / finish
+  // c1 / c2: the job's samples; issue_next() refills them with the next job's once they
+  // are folded into the FFT input, so those loads fly under this job's FFT, equalise, demap, finish
   auto run_job = [&](const FrameS &cur, const int jcur, float (&c1)[8], float (&c2)[8], auto &&issue_next) {
 #define DSTAMP(k, cond)                                                                   \
   do {                                                                                  \
@@ -1398,8 +1404,9 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       const bool const1 = __ballot(ne1) == 0, const2 = __ballot(ne2) == 0;
       if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
       DSTAMP(16, jcur == 1);
+      DSTAMP(27, jcur == 2); // (job 2 samples ready: minus mark 21 = the wait for its loads)
+      issue_next(); // the samples are in v: the next job's loads fly under this FFT too
       fft512_wave(v, X2, tw1, tw2);
-      issue_next();
       DSTAMP(17, jcur == 1);
       int ln = lane;
       asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
@@ -1561,15 +1568,27 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
         const int dsym = jcur == 0 ? 1 : min(2 * jcur + 1, cur.T);
         // (the job count only ever shrinks, once the answer is final: the next job was
         // chosen before this one ran, so a frame whose count grew would lose jobs)
-        const int need = eval_need(cur, dsym);
+        int hdr = 0;
+        int need = eval_need(cur, dsym, &hdr);
+        if (need < 0 && hdr) need = -1 - need; // header decoded: the byte count is final
         if (need >= 0) {
-          fneed = need;
-          fnj = jcur + 1;
+          // jobs holding the last data symbol the parse reads (job j: symbols 2j-1, 2j)
+          const int ls = need > 0 ? (int)(((int64_t)need * 8 * rep + per_sym - 1) / per_sym) - 1 : 0;
+          const int jn = ls <= 0 ? 1 : (ls + 1) / 2 + 1;
+          const int availT = (min(cur.T * per_sym, cur.M * per_sym) / rep) >> 3;
+          if (need > availT) {
+            wflags |= AMOD_FLAG_SPAN; // past the demodulated symbols: the exact kernel
+            fnj = jcur + 1;
+          } else {
+            fneed = need;
+            fnj = min(fnj, max(jcur + 1, jn));
+          }
         }
       }
     }
     // ---------------------------------------------------------------- frame end
     if (jcur + 1 >= fnj) {
+      FRESH_ARGS; // the finish's tables and outputs: scalar loads here, not held across the loop
       DSTAMP(22, true);
       const int nbits = cur.M * per_sym;
       const int decoded = cur.T * per_sym;
@@ -1649,7 +1668,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   // every load is unconditional (a frame without data symbols reads its CE window, the
   // last job re-reads its own samples), so the in-order vmcnt accounting stays exact
   auto loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) { job_loads(F, j, r1, r2); };
-  // the sample registers are refilled with the next job right after each FFT
+  // the sample registers are refilled with the next job as soon as the FFT input is formed
   FrameS fa, fb;
   int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
   if (ka >= nfr) return;

@@ -548,7 +548,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   for (auto &e : ctx->chunk_ev)
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  const int xslots = std::min(ctx->nslots, nframes);
+  // exact-kernel grid: persistent workgroups over the listed frames (usually none: the
+  // launch then costs its dispatch, so two per CU, not one per slot)
+  const int xslots = std::min({ctx->nslots, nframes, 2 * std::max(1, ctx->cu_count)});
   HIP_TRY(mark(0));
   if (nchunk == 1) {
     w.f0 = 0; w.f1 = nframes;

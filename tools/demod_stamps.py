@@ -46,6 +46,11 @@ def main():
                       f"  p90 {np.percentile(d, 90):8.0f}")
     ok = (st[:, 21] != 0) & (st[:, 16] != 0)
     print("job 1 total median", np.median(st[ok, 21] - st[ok, 16]))
+    ok = (st[:, 21] != 0) & (st[:, 27] != 0)
+    if ok.any():
+        d = st[ok, 27] - st[ok, 21]
+        print(f"job 1 end -> job 2 samples ready: median {np.median(d):.0f} p10 {np.percentile(d, 10):.0f} "
+              f"p90 {np.percentile(d, 90):.0f}")
     ok = (st[:, 28] != 0) & (st[:, 29] != 0)
     if ok.any():
         a, b = st[ok, 28], st[ok, 29]
