@@ -441,7 +441,7 @@ __device__ inline void init_result(amod_result &r) {
 extern "C" {
 hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s); // k_detect / k_chunk_prep
 hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s);
-int amod_demod_blocks_per_cu(int mod, int lds);
+int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds);
 void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_words, int *vote_off);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);

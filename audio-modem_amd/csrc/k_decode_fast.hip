@@ -89,6 +89,39 @@ struct Smem {  // fixed part (static LDS)
 
 __device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 operator-(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// packed-pair forms the demodulator needs (one v_pk_* each, halves picked by op_sel)
+// (a.x + b.x, a.y - b.y)
+__device__ __forceinline__ f2v pk_add_conj(f2v a, f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// (a.y + b.y, b.x - a.x)
+__device__ __forceinline__ f2v pk_add_swap_neg(f2v a, f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// phase derotation (e.x + ph e.y, e.y - ph e.x), ph wave-uniform
+__device__ __forceinline__ f2v pk_derot(f2v e, f2v ph) {
+  f2v r;
+  asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(e), "s"(ph));
+  return r;
+}
+// (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
+__device__ __forceinline__ f2v pk_cmul(f2v a, f2v b) {
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+// QPSK (Gray, modem.js:107-150) decision as its two stream bits at bits 31, 30:
+// [im < 0], [re < 0] xor [im < 0] from the sign bits (a +-0 component lies on a decision
+// boundary, where the margin test lists the frame for the exact kernel anyway)
+__device__ __forceinline__ uint32_t qpsk_bits(float cr, float ci) {
+  const uint32_t a = __float_as_uint(cr), b = __float_as_uint(ci);
+  return (b & 0x80000000u) | (((a ^ b) >> 31) << 30);
+}
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
@@ -115,45 +148,54 @@ __device__ __forceinline__ void dft8(float2 (&v)[8]) {
   v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
 }
 
-// exchange-2 column swizzle and the final spectrum placement (bank-conflict free)
-__device__ __forceinline__ int swz2(int q, int l1, int p1) {
-  return 8 * ((l1 ^ q) & 7) + ((p1 ^ ((q & 3) + 4 * (l1 >> 2))) & 7);
-}
+// Per-wave exchange buffer of the 512-pt FFT (float2 units): exchanges 1 and 2 use 8 rows
+// of XROW = 72 (row q at 72 q), exchange 2 columns at 9 p1 + l1; the spectrum is left at
+// spec_idx(n). Every access of a pass is a per-lane base plus an immediate offset (no
+// per-access address arithmetic), and the row pad makes each pattern conflict-free:
+// ds_read_b64 serves lanes in two groups of 32 with banks (a / 4) mod 64, ds_write_b64 in
+// four groups of 16 with banks (a / 4) mod 32 (MI355X_MICROARCH.md, LDS), and
+// 72 q2 + l1 resp. 72 q2 + 9 p1 (q2 < 4 inside a group) are distinct mod 32.
+constexpr int XROW = 72;
+constexpr int XCH_F2 = 8 * XROW; // float2 per wave
 __device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2); }
 
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); X[n] is
-// left in the wave's 512-entry LDS exchange buffer X2 at spec_idx(n).
+// left in the wave's exchange buffer X2 at spec_idx(n).
 // tw1: rows 1-7 of e^{-2 pi i l q / 512} (row q at tw1[64 q]); tw2: [8][8] pass-2 twiddles
 __device__ void fft512_wave(float2 (&v)[8], float2 *const X2, const float2 *__restrict__ tw1,
                             const float2 *__restrict__ tw2) {
   int l = wave_lane();
-  asm volatile("" : "+v"(l)); // keep lane-derived swizzles inside the job loop
+  asm volatile("" : "+v"(l)); // keep lane-derived bases inside the job loop
+  const int l1 = l & 7, q2 = l >> 3;
   dft8(v);
 #pragma unroll
   for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], tw1[q * 64 + l]);
-  // exchange 1: row q, col l ^ (q<<3)
+  // exchange 1: Y1[q][l] at row q, column l
+  float2 *const w1 = X2 + l;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) X2[q * 64 + (l ^ (q << 3))] = v[q];
+  for (int q = 0; q < 8; ++q) w1[q * XROW] = v[q];
   __builtin_amdgcn_wave_barrier();
-  const int l1 = l & 7, q2 = l >> 3; // pass-2 lane = (l1, q)
-  const int r2 = q2 * 64;
+  // pass 2, lane (l1, q2): the 64-pt DFT of row q2 over l = l1 + 8 l2, radix-8 over l2
+  float2 *const r1 = X2 + q2 * XROW + l1;
 #pragma unroll
-  for (int l2 = 0; l2 < 8; ++l2) v[l2] = X2[r2 + l1 + 8 * (l2 ^ q2)];
+  for (int l2 = 0; l2 < 8; ++l2) v[l2] = r1[8 * l2];
   dft8(v);
 #pragma unroll
   for (int p1 = 1; p1 < 8; ++p1) v[p1] = cmul(v[p1], tw2[p1 * 8 + l1]);
   __builtin_amdgcn_wave_barrier();
-  // exchange 2: lane (l1, q) writes U[p1] at row q, col swz2(q, l1, p1)
+  // exchange 2: U[p1] of lane (l1, q2) at row q2, column 9 p1 + l1 (same base as r1)
 #pragma unroll
-  for (int p1 = 0; p1 < 8; ++p1) X2[r2 + swz2(q2, l1, p1)] = v[p1];
+  for (int p1 = 0; p1 < 8; ++p1) r1[9 * p1] = v[p1];
   __builtin_amdgcn_wave_barrier();
-  const int p1 = l & 7; // pass-3 lane = (p1, q), same row as pass 2
+  const int p1 = l & 7; // pass-3 lane = (p1, q2), same row as pass 2
+  const float2 *const r2 = X2 + q2 * XROW + 9 * p1;
 #pragma unroll
-  for (int a = 0; a < 8; ++a) v[a] = X2[r2 + swz2(q2, a, p1)];
+  for (int a = 0; a < 8; ++a) v[a] = r2[a];
   dft8(v); // v[p2] = X[q2 + 8 p1 + 64 p2]
   __builtin_amdgcn_wave_barrier();
+  float2 *const w3 = X2 + spec_idx(q2 + 8 * p1); // spec_idx(n + 64 p2) = spec_idx(n) + 64 p2
 #pragma unroll
-  for (int p2 = 0; p2 < 8; ++p2) X2[spec_idx(q2 + 8 * p1 + 64 * p2)] = v[p2];
+  for (int p2 = 0; p2 < 8; ++p2) w3[64 * p2] = v[p2];
   __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ float2 spec_read(const float2 *X2, int n) { return X2[spec_idx(n & 511)]; }
@@ -1215,19 +1257,44 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   }
   return r;
 }
+// one slice-by-4 step: the register after message word `word` (little-endian bytes)
+__device__ __forceinline__ uint32_t crc_step(uint32_t c, uint32_t word, const uint32_t *t4) {
+  c ^= word;
+  return t4[768 + (c & 0xFF)] ^ t4[512 + ((c >> 8) & 0xFF)] ^ t4[256 + ((c >> 16) & 0xFF)] ^ t4[c >> 24];
+}
+// t4: the slice-by-4 tables. Lane l takes chunks l and l + 64 of each 128 in lockstep (two
+// independent register chains), so a message of up to 128 chunks costs one 4-step chain
+// of latency.
 __device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4) {
   const int lane = wave_lane();
   constexpr int BLOCKB = kCrcMats * kCrcChunk; // bytes per block
+  static_assert(kCrcChunk == 16, "four words per chunk");
   uint32_t reg = 0xFFFFFFFFu; // carried between blocks (uniform)
   for (int p0 = 0; p0 < L; p0 += BLOCKB) {
     const int plen = min(BLOCKB, L - p0);
     const int nch = (plen + kCrcChunk - 1) / kCrcChunk; // chunks, right-aligned
     uint32_t acc = 0;
-    for (int j = lane; j < nch; j += 64) {
-      const int end = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
-      const int beg = max(0, end - kCrcChunk);
-      const uint32_t c = crc_chunk(v, p0 + beg, p0 + end, j == 0 ? reg : 0u, t4);
-      acc ^= crc_shift(t.crc_mat, nch - 1 - j, c);
+    for (int j = lane; j < nch; j += 128) {
+      const int jb = j + 64;
+      const bool hb = jb < nch;
+      const int end_a = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
+      const int beg_a = max(0, end_a - kCrcChunk);
+      const int beg_b = plen - (nch - 1 - jb) * kCrcChunk - kCrcChunk; // chunk jb is whole
+      uint32_t ca = j == 0 ? reg : 0u, cb = 0u;
+      if (end_a - beg_a == kCrcChunk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t wa = le_word_at(v, p0 + beg_a + 4 * k);
+          const uint32_t wb = hb ? le_word_at(v, p0 + beg_b + 4 * k) : 0u;
+          ca = crc_step(ca, wa, t4);
+          cb = crc_step(cb, wb, t4);
+        }
+      } else { // the short first chunk (lane 0 only)
+        ca = crc_chunk(v, p0 + beg_a, p0 + end_a, ca, t4);
+        if (hb) cb = crc_chunk(v, p0 + beg_b, p0 + beg_b + kCrcChunk, 0u, t4);
+      }
+      acc ^= crc_shift(t.crc_mat, nch - 1 - j, ca);
+      if (hb) acc ^= crc_shift(t.crc_mat, nch - 1 - jb, cb);
     }
     reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
   }
@@ -1255,16 +1322,22 @@ __device__ inline void wave_vote(const uint32_t *bits, int nbits, int rep, uint3
   }
 }
 
-struct FrameS {  // wave-uniform facts of one frame on the demodulation path
-  int f, T, M, nj, start, coarse;
-  float A, B, fbest;
+// the longest prefix parse_need reads: a legacy header (1 + 255 + 4 bytes)
+constexpr int kHeaderMaxBytes = 1 + 255 + 4;
+
+struct FrameS {  // wave-uniform facts of one frame on the demodulation path (SGPRs: the
+                // frame-end-only fields are re-read from the detection record there)
+  int f, T, M, start;
+  float A, B;
   const float *X;
 };
+__device__ __forceinline__ int frame_jobs(const FrameS &F) { return F.T > 0 ? 1 + F.T / 2 : 0; }
 
 // MOD: the launch's modulation as a template argument (decisions and packing unroll)
-template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
+// NS: band slots per lane, ceil(nband / 64) (slot rr < NS - 1 is full on every lane)
+template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop() {
   constexpr int BPS = MOD == AMOD_BPSK ? 1 : (MOD == AMOD_QPSK ? 2 : 4);
-  __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][512];
+  __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][XCH_F2];
   __shared__ float2 twl[512];   // tw1 rows 1-7 (row q at 64 (q - 1)), then tw2[64]
   FRESH_ARGS;
   const int tid = ltid();
@@ -1282,41 +1355,46 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   const bool chunk_mode = cfg.mode == AMOD_MODE_CHUNK;
   const float guard = cfg.guard;
   const int nfr = w.f1 - w.f0; // frames [f0, f1) of this launch
-  const int wstride = (int)gridDim.x * NWAVE;
   // the wave's bit stream (and voted stream) in dynamic LDS
   uint32_t *const bits = LDS_U + wave * w.stream_words;
   uint32_t *const voted = bits + w.vote_off;
   float2 *const X2 = xch[wave];
   const float2 *const tw1 = twl - 64, *const tw2 = twl + 7 * 64;
-  // per-lane band facts for its 4 subcarriers b = lane + 64 rr: data index (-1 pilot, -2 none)
+  // per-lane band facts for its 4 subcarriers b = lane + 64 rr: the bit offset of its
+  // decision in a symbol, di * BPS (-1 pilot, -2 none; di = data index)
   // (two 16-bit fields per register: registers bound k_demod's occupancy)
   uint32_t di_pk[2] = {0u, 0u};
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int di = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
-    di_pk[rr >> 1] |= ((uint32_t)di & 0xFFFFu) << (16 * (rr & 1));
+    const int dib = di >= 0 ? di * BPS : di;
+    di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
   }
-  auto di_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
+  auto dib_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
   // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
   // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
   int prr = -1, npl = 0;
 #pragma unroll
   for (int rr = 3; rr >= 0; --rr)
-    if (di_of(rr) == -1) { prr = rr; ++npl; }
+    if (dib_of(rr) == -1) { prr = rr; ++npl; }
   const bool pil_multi = __ballot(npl > 1) != 0;
   uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(lane + 64 * rr < nband && cfg.t.known[lane + 64 * rr] < 0.f) << rr;
 
-  // next frame on the demodulation path at or after wave-iteration k (frames last-first)
+  // next frame on the demodulation path at or after wave-iteration k (frames last-first).
+  // A static stride: the dispatcher places the grid's workgroups round-robin over the CUs,
+  // so every SIMD gets within one frame of the mean (a claim counter measured slower: its
+  // atomics' returns hold up the in-order vmcnt waits of the sample loads)
+  const int wstride = (int)gridDim.x * NWAVE;
   auto next_frame = [&](int k, FrameS &F) -> int {
     FRESH_ARGS;
     for (; k < nfr; k += wstride) {
       const int f = w.f1 - 1 - k;
       const DetRec d = sload(w.det + f);
       if (d.route != ROUTE_DEMOD) continue;
-      F.f = f; F.T = d.T; F.M = d.M; F.nj = d.T > 0 ? 1 + d.T / 2 : 0; F.start = d.start; F.coarse = d.coarse;
-      F.A = d.A; F.B = d.B; F.fbest = d.fbest;
+      F.f = f; F.T = d.T; F.M = d.M; F.start = d.start;
+      F.A = d.A; F.B = d.B;
       F.X = w.samples + sload(w.off + f);
       return k;
     }
@@ -1351,13 +1429,22 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   const int rep = cfg.rep;
   // bytes the parse reads once `dsym` data symbols are demodulated (-1: more needed)
   // (-1 - need: more bytes needed; with *hdr = 1 the header is decoded, so `need` is final)
+  // (rep > 1: the known prefix, up to the longest header parse_need reads, is voted by the
+  // whole wave first, so lane 0 parses a plain byte stream)
   auto eval_need = [&](const FrameS &F, int dsym, int *hdr = nullptr) -> int {
     const int nbits = F.M * per_sym;
+    const int known = min(dsym * per_sym, nbits);
+    const int avail = (known / rep) >> 3;
+    const uint32_t *src = bits;
+    if (rep > 1) {
+      wave_vote(bits, min(known, kHeaderMaxBytes * 8 * rep), rep, voted);
+      __builtin_amdgcn_wave_barrier();
+      src = voted;
+    }
     int need = 0, fin = 0;
     if (lane == 0) {
-      const int avail = (min(dsym * per_sym, nbits) / rep) >> 3;
       bool f = false;
-      need = parse_need(bits, rep, avail, (nbits / rep) >> 3, cfg.mode, &f);
+      need = parse_need(src, 1, avail, (nbits / rep) >> 3, cfg.mode, &f);
       fin = f;
       if (need > avail) need = -1 - need;
     }
@@ -1378,7 +1465,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
     if (jcur == 0) { // a new frame: clear its bit stream
       const int nwz = (cur.T * per_sym + 31) / 32 + 2;
       for (int i = lane; i < nwz; i += 64) bits[i] = 0u;
-      live_f = f; fnj = max(cur.nj, 1); fneed = -1; flag_sym = 0x7fffffff;
+      live_f = f; fnj = max(frame_jobs(cur), 1); fneed = -1; flag_sym = 0x7fffffff;
       wflags = 0; sflags = 0;
     } else if (jcur >= fnj) { // prefetched before the header showed the frame was complete
       issue_next();
@@ -1390,15 +1477,18 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       int s1, s2;
       job_syms(cur, jcur, s1, s2);
       const bool ce = s1 == -2;
-      const float f1v = rlane(c1[0], 0), f2v = rlane(c2[0], 0);
+      const float first1 = rlane(c1[0], 0), first2 = rlane(c2[0], 0);
       int ne1 = 0, ne2 = 0, nf = 0;
       float2 v[8];
+      // no second symbol: A = B = 0 zeroes the imaginary half (its samples are finite: the
+      // last job re-reads the first symbol's, checked below in chunk mode)
+      const float A2 = s2 >= 0 ? cur.A : 0.f, B2 = s2 >= 0 ? cur.B : 0.f;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        ne1 |= c1[m] != f1v;
-        ne2 |= c2[m] != f2v;
+        ne1 |= c1[m] != first1;
+        ne2 |= c2[m] != first2;
         if (chunk_mode) nf |= !isfinite(c1[m]) || !isfinite(c2[m]); // received: stage 0 saw them
-        v[m] = make_float2(fmaf(c1[m], cur.A, cur.B), s2 >= 0 ? fmaf(c2[m], cur.A, cur.B) : 0.f);
+        v[m] = make_float2(fmaf(c1[m], cur.A, cur.B), fmaf(c2[m], A2, B2));
       }
       // a window is constant iff every raw sample equals its first one (all-zero spectrum)
       const bool const1 = __ballot(ne1) == 0, const2 = __ballot(ne2) == 0;
@@ -1410,23 +1500,36 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       DSTAMP(17, jcur == 1);
       int ln = lane;
       asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
+      // per-job copies of the lane's slot facts: their comparisons are made where they are
+      // used instead of held as lane masks across the loop (SGPR pairs that spill)
+      asm volatile("" : "+v"(prr), "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg));
+      // the band: slot rr of lane ln is subcarrier b = ln + 64 rr, bins k = k0 + 64 rr and
+      // 512 - k (spec_idx(n +- 64) = spec_idx(n) +- 64: one base per side, immediate offsets)
+      const int k0 = sub_start + ln;
+      const f2v *const zkp = reinterpret_cast<const f2v *>(X2 + spec_idx(k0));
+      const f2v *const znp = reinterpret_cast<const f2v *>(X2 + spec_idx(kFft - 192 - k0));
       float zm = 0.f;
-      float2 x1[4], x2[4];
+      // twice the reference's X1, X2 (Z = x1 + i x2: X1 = (Z[k] + conj Z[-k]) / 2,
+      // X2 = (Z[k] - conj Z[-k]) / 2i); the 1/2 is folded into G below (exact: powers of 2)
+      f2v x1[4], x2[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int b = ln + 64 * rr;
-        x1[rr] = x2[rr] = make_float2(0.f, 0.f);
-        if (b < nband) {
-          const int k = sub_start + b;
-          const float2 zk = spec_read(X2, k), zn = spec_read(X2, kFft - k);
-          zm = fmaxf(zm, fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y)));
-          // Z = x1 + i x2:  X1 = (Z[k] + conj Z[-k]) / 2,  X2 = (Z[k] - conj Z[-k]) / 2i
-          x1[rr] = make_float2(0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y));
-          x2[rr] = make_float2(0.5f * (zk.y + zn.y), 0.5f * (zn.x - zk.x));
+        x1[rr] = x2[rr] = f2v{0.f, 0.f};
+        if (rr >= NS) continue; // no subcarrier in this slot
+        const f2v zk = zkp[64 * rr], zn = znp[64 * (3 - rr)];
+        f2v a = pk_add_conj(zk, zn), c = pk_add_swap_neg(zk, zn);
+        float zz = fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y));
+        if (rr == NS - 1) { // the last slot may be partly filled
+          const bool in = ln + 64 * rr < nband;
+          a = in ? a : f2v{0.f, 0.f};
+          c = in ? c : f2v{0.f, 0.f};
+          zz = in ? zz : 0.f;
         }
+        x1[rr] = a; x2[rr] = c; zm = fmaxf(zm, zz);
       }
       if (ce) {
-        // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438)
+        // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438).
+        // Here h = 2H and g = G / 2 (so x g = X G); |h|^2 = 4 |H|^2 against 4 x the thresholds
         zce = wmax_nn(zm);
         float gm = 0.f;
         int ch = 0;
@@ -1437,65 +1540,63 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
           const float2 h = const1 ? make_float2(0.f, 0.f) : make_float2(x1[rr].x * kn, x1[rr].y * kn);
           const float m2 = h.x * h.x + h.y * h.y;
           float2 g;
-          if (m2 > 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the 2e-6 eq bound
-          else g = make_float2(1.f, 0.f);
+          if (m2 > 4.f * 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the eq bound
+          else g = make_float2(0.5f, 0.f); // G = 1 (passthrough)
           // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
-          ch |= b < nband && !const1 && m2 < 1e-6f;
+          ch |= b < nband && !const1 && m2 < 4.f * 1e-6f;
           gl[rr] = g;
           if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
-          if (DBG && b < nband) { D->h_re[b] = h.x; D->h_im[b] = h.y; }
+          if (DBG && b < nband) { D->h_re[b] = 0.5f * h.x; D->h_im[b] = 0.5f * h.y; }
         }
-        gmax = wmax_nn(gm);
+        gmax = wmax_nn(gm); // half of max |G|
         if (__ballot(ch)) wflags |= AMOD_FLAG_CHANNEL;
       }
-      // equalise both halves (the CE half of job 0 is not a data symbol)
-      float2 e1[4], e2[4];
-      float em1 = 0.f, em2 = 0.f;
+      // equalise both halves (the CE half of job 0 is not a data symbol); em bounds |eq| of
+      // both symbols of the job
+      f2v e1[4], e2[4];
+      float em = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        e1[rr] = cmul(x1[rr], gl[rr]);
-        e2[rr] = cmul(x2[rr], gl[rr]);
-        em1 = fmaxf(em1, fabsf(e1[rr].x) + fabsf(e1[rr].y));
-        em2 = fmaxf(em2, fabsf(e2[rr].x) + fabsf(e2[rr].y));
+        const f2v g = f2v{gl[rr].x, gl[rr].y};
+        e1[rr] = pk_cmul(x1[rr], g);
+        e2[rr] = pk_cmul(x2[rr], g);
+        em = fmaxf(em, fmaxf(fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y)));
         const int b = ln + 64 * rr;
         if (DBG && b < nband && (s1 == 0 || s2 == 0)) {
           const bool one = s1 == 0;
-          const float2 xx = one ? x1[rr] : x2[rr], ee = one ? e1[rr] : e2[rr];
+          const f2v xx = one ? x1[rr] : x2[rr], ee = one ? e1[rr] : e2[rr];
           const bool c = one ? const1 : const2;
-          D->x_re[b] = c ? 0.f : xx.x; D->x_im[b] = c ? 0.f : xx.y;
+          D->x_re[b] = c ? 0.f : 0.5f * xx.x; D->x_im[b] = c ? 0.f : 0.5f * xx.y;
           D->eq_re[b] = c ? 0.f : ee.x; D->eq_im[b] = c ? 0.f : ee.y;
         }
       }
       DSTAMP(18, jcur == 1);
-      // error bound of eq per symbol (fp32 FFT + channel estimate), DESIGN.md "guards"
-      const float gsc = 2e-6f * guard * gmax;
-      float d1 = gsc * (zm + em1 * zce), d2 = gsc * (zm + em2 * zce);
-      d1 = wmax_nn(d1); d2 = wmax_nn(d2);
-      d1 += 1e-12f; d2 += 1e-12f;
+      // error bound of eq for both symbols (fp32 FFT + channel estimate), DESIGN.md "guards"
+      // (gmax is half of max |G|, hence 4e-6)
+      float d = 4e-6f * guard * gmax * (zm + em * zce);
+      d = wmax_nn(d) + 1e-12f;
       const bool live1 = !ce && !const1, live2 = s2 >= 0 && !const2;
-      // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405)
-      float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f, pc1 = 0.f, pc2 = 0.f;
-      int pflag1 = 0, pflag2 = 0;
-      auto pilot = [&](bool pil, float2 q1e, float2 q2e) {
+      // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405);
+      // per lane its pilot (at most one per lane: pil_multi takes the per-slot loop)
+      float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f;
+      int pc1 = 0, pc2 = 0, pflag1 = 0, pflag2 = 0;
+      auto pilot = [&](bool pil, f2v q1e, f2v q2e) {
         const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
-        // 0/1 weights in VGPRs (no lane masks kept live)
-        const float w1 = (pil && a1 > 1e-6f) ? 1.f : 0.f, w2 = (pil && a2 > 1e-6f) ? 1.f : 0.f;
-        // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below;
-        // signed 1/eqRe, finite for every lane (weight 0 where the reference skips)
-        const float q1 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a1, 1e-30f), q1e.x));
-        const float q2 = __builtin_amdgcn_rcpf(copysignf(fmaxf(a2, 1e-30f), q2e.x));
-        const float r1 = fabsf(q1), r2 = fabsf(q2);
-        ps1 = fmaf(w1 * q1, q1e.y, ps1);
-        ps2 = fmaf(w2 * q2, q2e.y, ps2);
-        pe1 = fmaf(w1 * r1, fmaf(fabsf(q1e.y), r1, 1.f), pe1);
-        pe2 = fmaf(w2 * r2, fmaf(fabsf(q2e.y), r2, 1.f), pe2);
-        pc1 += w1;
-        pc2 += w2;
-        pflag1 |= pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d1 + 1e-7f;
-        pflag2 |= pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d2 + 1e-7f;
+        const bool w1 = pil && a1 > 1e-6f, w2 = pil && a2 > 1e-6f;
+        pc1 += __popcll(__ballot(w1));
+        pc2 += __popcll(__ballot(w2));
+        // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below
+        const float q1 = w1 ? __builtin_amdgcn_rcpf(q1e.x) : 0.f;
+        const float q2 = w2 ? __builtin_amdgcn_rcpf(q2e.x) : 0.f;
+        ps1 = fmaf(q1, q1e.y, ps1);
+        ps2 = fmaf(q2, q2e.y, ps2);
+        pe1 = fmaf(fabsf(q1), fmaf(fabsf(q1e.y), fabsf(q1), 1.f), pe1);
+        pe2 = fmaf(fabsf(q2), fmaf(fabsf(q2e.y), fabsf(q2), 1.f), pe2);
+        pflag1 |= pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f;
+        pflag2 |= pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f;
       };
       if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
-        float2 p1 = e1[0], p2 = e2[0];
+        f2v p1 = e1[0], p2 = e2[0];
 #pragma unroll
         for (int rr = 1; rr < 4; ++rr) {
           p1 = prr == rr ? e1[rr] : p1;
@@ -1504,17 +1605,17 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
         pilot(prr >= 0, p1, p2);
       } else {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) pilot(di_of(rr) == -1, e1[rr], e2[rr]);
+        for (int rr = 0; rr < 4; ++rr) pilot(dib_of(rr) == -1, e1[rr], e2[rr]);
       }
-      ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); pc1 = wsum_b(pc1); pc2 = wsum_b(pc2);
+      ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2);
       // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
       const bool ph_unc1 = __ballot(pflag1) != 0, ph_unc2 = __ballot(pflag2) != 0;
-      const float ip1 = pc1 > 0.f ? __builtin_amdgcn_rcpf(pc1) : 0.f;
-      const float ip2 = pc2 > 0.f ? __builtin_amdgcn_rcpf(pc2) : 0.f;
+      const float ip1 = pc1 > 0 ? __builtin_amdgcn_rcpf((float)pc1) : 0.f;
+      const float ip2 = pc2 > 0 ? __builtin_amdgcn_rcpf((float)pc2) : 0.f;
       const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
-      const float dp1 = d1 * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d2 * pe2 * ip2 + 1e-6f * fabsf(ph2);
-      const float tau1 = 4.f * (d1 * (1.f + fabsf(ph1)) + em1 * dp1) + 1e-9f;
-      const float tau2 = 4.f * (d2 * (1.f + fabsf(ph2)) + em2 * dp2) + 1e-9f;
+      const float dp1 = d * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d * pe2 * ip2 + 1e-6f * fabsf(ph2);
+      const float tau1 = 4.f * (d * (1.f + fabsf(ph1)) + em * dp1) + 1e-9f;
+      const float tau2 = 4.f * (d * (1.f + fabsf(ph2)) + em * dp2) + 1e-9f;
       DSTAMP(19, jcur == 1);
       if (DBG && ln == 0) {
         if (s1 >= 0 && s1 < AMOD_DBG_SYMS) D->phase[s1] = const1 ? 0.f : ph1;
@@ -1523,30 +1624,38 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
       // a constant FFT window has an all-zero spectrum in the reference: every data
       // subcarrier takes the origin decision (ties resolve to the first point).
       // Each decision is OR-ed straight into the frame's MSB-first stream (LDS atomic OR;
-      // BPS divides 32, so a decision never straddles a word)
+      // BPS divides 32, so a decision never straddles a word): its bits are placed at the
+      // top of a word and shifted right by the stream position (v_lshrrev takes it mod 32)
+      const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
       int dflag1 = 0, dflag2 = 0;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int b = ln + 64 * rr;
-        const int di = di_of(rr);
-        const bool dat = b < nband && di >= 0;
+      for (int which = 0; which < 2; ++which) {
+        const int sidx = which == 0 ? s1 : s2;
+        if (sidx < 0) continue; // wave-uniform
+        const bool live = which == 0 ? live1 : live2;
+        const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
+        const float tau = which == 0 ? tau1 : tau2;
+        const int sbase = sidx * per_sym;
+        int unc_any = 0;
 #pragma unroll
-        for (int which = 0; which < 2; ++which) {
-          const int sidx = which == 0 ? s1 : s2;
-          if (sidx < 0) continue; // wave-uniform
-          const bool live = which == 0 ? live1 : live2;
-          const float2 e = which == 0 ? e1[rr] : e2[rr];
-          const float ph = which == 0 ? ph1 : ph2;
-          const float cr = fmaf(e.y, ph, e.x);
-          const float ci = fmaf(-e.x, ph, e.y);
+        for (int rr = 0; rr < 4; ++rr) {
+          if (rr >= NS) continue;
+          const int dib = dib_of(rr);
+          const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
+          uint32_t db;
           float margin;
-          const int dec = decide(MOD, cr, ci, margin);
-          const int idx = live ? dec : origin_idx;
-          const int unc = dat && live && margin <= (which == 0 ? tau1 : tau2);
-          if (which == 0) dflag1 |= unc; else dflag2 |= unc;
-          const int pos = sidx * per_sym + di * BPS;
-          if (dat && idx) atomicOr(bits + (pos >> 5), (uint32_t)idx << (32 - BPS - (pos & 31)));
+          if (MOD == AMOD_QPSK) {
+            db = qpsk_bits(c.x, c.y);
+            margin = fminf(fabsf(c.x), fabsf(c.y));
+          } else {
+            db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
+          }
+          db = live ? db : org_bits;
+          unc_any |= dib >= 0 && live && margin <= tau;
+          const int pos = sbase + dib;
+          if (dib >= 0) atomicOr(bits + (pos >> 5), db >> (pos & 31));
         }
+        if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
       }
       {
         const bool d1u = __ballot(dflag1) != 0, d2u = __ballot(dflag2) != 0;
@@ -1615,7 +1724,10 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
           amod_result r;
           init_result(r);
           r.nbits = nbits;
-          if (cfg.mode == AMOD_MODE_RECEIVED) { r.fine_metric = cur.fbest; r.coarse_idx = cur.coarse; r.preamble_idx = cur.start; }
+          if (cfg.mode == AMOD_MODE_RECEIVED) {
+            const DetRec dr = sload(w.det + f);
+            r.fine_metric = dr.fbest; r.coarse_idx = dr.coarse; r.preamble_idx = cur.start;
+          }
           const int nbytes = (nbits / rep) >> 3;
           const int crc_len = parse_stream(v, nbytes, cfg.mode, r); // every lane: the same bytes
           if (cfg.mode == AMOD_MODE_RECEIVED) {
@@ -1658,7 +1770,7 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   };
   // the job after (F, k, j): the frame's next, or the next frame's first; false at the end
   auto advance = [&](FrameS &F, int &k, int &j) -> bool {
-    if (j + 1 < (F.f == live_f ? fnj : max(F.nj, 1))) { ++j; return true; }
+    if (j + 1 < (F.f == live_f ? fnj : max(frame_jobs(F), 1))) { ++j; return true; }
     FrameS nf;
     const int kn = next_frame(k + wstride, nf);
     if (kn >= nfr) return false;
@@ -1685,21 +1797,30 @@ template <bool DBG, int MOD> __device__ __forceinline__ void demod_loop() {
   }
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
 }
-template <int MOD> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {
+template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  demod_loop<false, MOD>();
+  demod_loop<false, MOD, NS>();
 }
-template <int MOD> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
+template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
-  demod_loop<true, MOD>();
+  demod_loop<true, MOD, NS>();
 }
 typedef void (*demod_fn)(const DevCfg, const DevWork);
-__host__ demod_fn demod_kernel(int mod, bool dbg) {
-  if (mod == AMOD_BPSK) return dbg ? k_demod_dbg<AMOD_BPSK> : k_demod<AMOD_BPSK>;
-  if (mod == AMOD_QPSK) return dbg ? k_demod_dbg<AMOD_QPSK> : k_demod<AMOD_QPSK>;
-  return dbg ? k_demod_dbg<AMOD_QAM16> : k_demod<AMOD_QAM16>;
+template <int MOD> __host__ demod_fn demod_kernel_ns(int ns, bool dbg) {
+  switch (ns) {
+  case 1: return dbg ? k_demod_dbg<MOD, 1> : k_demod<MOD, 1>;
+  case 2: return dbg ? k_demod_dbg<MOD, 2> : k_demod<MOD, 2>;
+  case 3: return dbg ? k_demod_dbg<MOD, 3> : k_demod<MOD, 3>;
+  default: return dbg ? k_demod_dbg<MOD, 4> : k_demod<MOD, 4>;
+  }
+}
+__host__ demod_fn demod_kernel(const DevCfg &cfg, bool dbg) {
+  const int ns = (cfg.nband + 63) / 64; // validate(): 1 <= nband <= 255
+  if (cfg.mod == AMOD_BPSK) return demod_kernel_ns<AMOD_BPSK>(ns, dbg);
+  if (cfg.mod == AMOD_QPSK) return demod_kernel_ns<AMOD_QPSK>(ns, dbg);
+  return demod_kernel_ns<AMOD_QAM16>(ns, dbg);
 }
 
 
@@ -1737,14 +1858,14 @@ extern "C" hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::De
 }
 extern "C" hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s) {
   if (w.f1 <= w.f0 || nblocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::demod_kernel(cfg.mod, w.dbg != nullptr), dim3(nblocks), dim3(amod::WG),
+  hipLaunchKernelGGL(amod::demod_kernel(cfg, w.dbg != nullptr), dim3(nblocks), dim3(amod::WG),
                      (unsigned)(4 * amod::NWAVE * w.stream_words), s, cfg, w);
   return hipGetLastError();
 }
 // k_demod blocks resident at once on one CU for a dynamic LDS of lds bytes
-extern "C" int amod_demod_blocks_per_cu(int mod, int lds) {
+extern "C" int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, amod::demod_kernel(mod, false), amod::WG, lds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, amod::demod_kernel(cfg, false), amod::WG, lds) != hipSuccess ||
       n <= 0)
     n = 4;
   return n;

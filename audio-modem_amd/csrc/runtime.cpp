@@ -239,7 +239,7 @@ struct amod_ctx {
   DevBuf det;          // fast path: per-frame detection records (k_detect -> k_demod)
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
-  int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_bpc = 0;
+  int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0;
   void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
   void (*ext_free[4])(void *) = {nullptr, nullptr, nullptr, nullptr};
   int64_t soft_stride = 0;
@@ -529,8 +529,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // d.stop_after (diagnostics, AMOD_STOP_AFTER): <= 2 stops after detection
   const bool demod = d.stop_after >= 3;
   const int lds = 4 * 4 * w.stream_words; // k_demod: 4 waves per block
-  if (ctx->demod_lds != lds || ctx->demod_mod != d.mod) {
-    ctx->demod_lds = lds; ctx->demod_mod = d.mod; ctx->demod_bpc = amod_demod_blocks_per_cu(d.mod, lds);
+  if (ctx->demod_lds != lds || ctx->demod_mod != d.mod || ctx->demod_nband != d.nband) {
+    ctx->demod_lds = lds; ctx->demod_mod = d.mod; ctx->demod_nband = d.nband;
+    ctx->demod_bpc = amod_demod_blocks_per_cu(d, lds);
   }
   int64_t per_cu = ctx->demod_bpc;
   if (const char *g = getenv("AMOD_DEMOD_BPC")) per_cu = std::max(1, atoi(g)); // diagnostics: grid size
