@@ -126,26 +126,56 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
 
-// 4-point DFT, W4 = -i
-__device__ __forceinline__ void dft4(float2 &a0, float2 &a1, float2 &a2, float2 &a3) {
-  const float2 s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = a1 - a3;
+// Radix-8 step on packed pairs (f2v = (re, im) in an aligned register pair): every
+// complex add and every multiply by -i or W8 is one v_pk_* with its halves picked by
+// op_sel / negated by neg_lo / neg_hi, so no operand is moved between registers. 8-point
+// DFT in natural order, v[q] <- sum_m v[m] W8^{mq}: two 4-point DFTs (W4 = -i) after the
+// first butterfly, W8 = (1 - i) / sqrt 2 and W8^3 applied as (x + y, y - x) r.
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ f2v pk_add_mi(f2v a, f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ f2v pk_sub_mi(f2v a, f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// (b.x + b.y, b.y - b.x): W8 b / r
+__device__ __forceinline__ f2v pk_w8u(f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b));
+  return r;
+}
+// (b.y - b.x, -b.x - b.y): W8^3 b / r
+__device__ __forceinline__ f2v pk_w83u(f2v b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(b));
+  return r;
+}
+__device__ __forceinline__ void pk_dft4(f2v &a0, f2v &a1, f2v &a2, f2v &a3) {
+  const f2v s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = a1 - a3;
   a0 = s02 + s13;
   a2 = s02 - s13;
-  a1 = make_float2(d02.x + d13.y, d02.y - d13.x);
-  a3 = make_float2(d02.x - d13.y, d02.y + d13.x);
+  a1 = pk_add_mi(d02, d13);
+  a3 = pk_sub_mi(d02, d13);
 }
-// 8-point DFT in natural order: v[q] <- sum_m v[m] W8^{mq}
-__device__ __forceinline__ void dft8(float2 (&v)[8]) {
-  const float r = 0.70710678118654752f;
-  float2 a0 = v[0] + v[4], a1 = v[1] + v[5], a2 = v[2] + v[6], a3 = v[3] + v[7];
-  float2 b0 = v[0] - v[4], b1 = v[1] - v[5], b2 = v[2] - v[6], b3 = v[3] - v[7];
-  b1 = make_float2((b1.x + b1.y) * r, (b1.y - b1.x) * r);
-  b2 = make_float2(b2.y, -b2.x);
-  b3 = make_float2((b3.y - b3.x) * r, -(b3.x + b3.y) * r);
-  dft4(a0, a1, a2, a3);
-  dft4(b0, b1, b2, b3);
+__device__ __forceinline__ void pk_dft8(f2v (&v)[8]) {
+  const f2v r = {0.70710678118654752f, 0.70710678118654752f};
+  f2v a0 = v[0] + v[4], a1 = v[1] + v[5], a2 = v[2] + v[6], a3 = v[3] + v[7];
+  f2v b0 = v[0] - v[4], b1 = v[1] - v[5], b2 = v[2] - v[6], b3 = v[3] - v[7];
+  b1 = pk_w8u(b1) * r;
+  b3 = pk_w83u(b3) * r;
+  pk_dft4(a0, a1, a2, a3);
+  // dft4 of (b0, -i b2 folded into the adds, b1, b3)
+  const f2v s02 = pk_add_mi(b0, b2), d02 = pk_sub_mi(b0, b2), s13 = b1 + b3, d13 = b1 - b3;
   v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
-  v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
+  v[1] = s02 + s13;
+  v[5] = s02 - s13;
+  v[3] = pk_add_mi(d02, d13);
+  v[7] = pk_sub_mi(d02, d13);
 }
 
 // Per-wave exchange buffer of the 512-pt FFT (float2 units): exchanges 1 and 2 use 8 rows
@@ -162,38 +192,40 @@ __device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); X[n] is
 // left in the wave's exchange buffer X2 at spec_idx(n).
 // tw1: rows 1-7 of e^{-2 pi i l q / 512} (row q at tw1[64 q]); tw2: [8][8] pass-2 twiddles
-__device__ void fft512_wave(float2 (&v)[8], float2 *const X2, const float2 *__restrict__ tw1,
-                            const float2 *__restrict__ tw2) {
+__device__ void fft512_wave(f2v (&v)[8], float2 *const X2f, const float2 *__restrict__ tw1f,
+                            const float2 *__restrict__ tw2f) {
+  f2v *const X2 = reinterpret_cast<f2v *>(X2f);
+  const f2v *const tw1 = reinterpret_cast<const f2v *>(tw1f), *const tw2 = reinterpret_cast<const f2v *>(tw2f);
   int l = wave_lane();
   asm volatile("" : "+v"(l)); // keep lane-derived bases inside the job loop
   const int l1 = l & 7, q2 = l >> 3;
-  dft8(v);
+  pk_dft8(v);
 #pragma unroll
-  for (int q = 1; q < 8; ++q) v[q] = cmul(v[q], tw1[q * 64 + l]);
+  for (int q = 1; q < 8; ++q) v[q] = pk_cmul(v[q], tw1[q * 64 + l]);
   // exchange 1: Y1[q][l] at row q, column l
-  float2 *const w1 = X2 + l;
+  f2v *const w1 = X2 + l;
 #pragma unroll
   for (int q = 0; q < 8; ++q) w1[q * XROW] = v[q];
   __builtin_amdgcn_wave_barrier();
   // pass 2, lane (l1, q2): the 64-pt DFT of row q2 over l = l1 + 8 l2, radix-8 over l2
-  float2 *const r1 = X2 + q2 * XROW + l1;
+  f2v *const r1 = X2 + q2 * XROW + l1;
 #pragma unroll
   for (int l2 = 0; l2 < 8; ++l2) v[l2] = r1[8 * l2];
-  dft8(v);
+  pk_dft8(v);
 #pragma unroll
-  for (int p1 = 1; p1 < 8; ++p1) v[p1] = cmul(v[p1], tw2[p1 * 8 + l1]);
+  for (int p1 = 1; p1 < 8; ++p1) v[p1] = pk_cmul(v[p1], tw2[p1 * 8 + l1]);
   __builtin_amdgcn_wave_barrier();
   // exchange 2: U[p1] of lane (l1, q2) at row q2, column 9 p1 + l1 (same base as r1)
 #pragma unroll
   for (int p1 = 0; p1 < 8; ++p1) r1[9 * p1] = v[p1];
   __builtin_amdgcn_wave_barrier();
   const int p1 = l & 7; // pass-3 lane = (p1, q2), same row as pass 2
-  const float2 *const r2 = X2 + q2 * XROW + 9 * p1;
+  const f2v *const r2 = X2 + q2 * XROW + 9 * p1;
 #pragma unroll
   for (int a = 0; a < 8; ++a) v[a] = r2[a];
-  dft8(v); // v[p2] = X[q2 + 8 p1 + 64 p2]
+  pk_dft8(v); // v[p2] = X[q2 + 8 p1 + 64 p2]
   __builtin_amdgcn_wave_barrier();
-  float2 *const w3 = X2 + spec_idx(q2 + 8 * p1); // spec_idx(n + 64 p2) = spec_idx(n) + 64 p2
+  f2v *const w3 = X2 + spec_idx(q2 + 8 * p1); // spec_idx(n + 64 p2) = spec_idx(n) + 64 p2
 #pragma unroll
   for (int p2 = 0; p2 < 8; ++p2) w3[64 * p2] = v[p2];
   __builtin_amdgcn_wave_barrier();
@@ -1257,44 +1289,19 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   }
   return r;
 }
-// one slice-by-4 step: the register after message word `word` (little-endian bytes)
-__device__ __forceinline__ uint32_t crc_step(uint32_t c, uint32_t word, const uint32_t *t4) {
-  c ^= word;
-  return t4[768 + (c & 0xFF)] ^ t4[512 + ((c >> 8) & 0xFF)] ^ t4[256 + ((c >> 16) & 0xFF)] ^ t4[c >> 24];
-}
-// t4: the slice-by-4 tables. Lane l takes chunks l and l + 64 of each 128 in lockstep (two
-// independent register chains), so a message of up to 128 chunks costs one 4-step chain
-// of latency.
 __device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4) {
   const int lane = wave_lane();
   constexpr int BLOCKB = kCrcMats * kCrcChunk; // bytes per block
-  static_assert(kCrcChunk == 16, "four words per chunk");
   uint32_t reg = 0xFFFFFFFFu; // carried between blocks (uniform)
   for (int p0 = 0; p0 < L; p0 += BLOCKB) {
     const int plen = min(BLOCKB, L - p0);
     const int nch = (plen + kCrcChunk - 1) / kCrcChunk; // chunks, right-aligned
     uint32_t acc = 0;
-    for (int j = lane; j < nch; j += 128) {
-      const int jb = j + 64;
-      const bool hb = jb < nch;
-      const int end_a = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
-      const int beg_a = max(0, end_a - kCrcChunk);
-      const int beg_b = plen - (nch - 1 - jb) * kCrcChunk - kCrcChunk; // chunk jb is whole
-      uint32_t ca = j == 0 ? reg : 0u, cb = 0u;
-      if (end_a - beg_a == kCrcChunk) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t wa = le_word_at(v, p0 + beg_a + 4 * k);
-          const uint32_t wb = hb ? le_word_at(v, p0 + beg_b + 4 * k) : 0u;
-          ca = crc_step(ca, wa, t4);
-          cb = crc_step(cb, wb, t4);
-        }
-      } else { // the short first chunk (lane 0 only)
-        ca = crc_chunk(v, p0 + beg_a, p0 + end_a, ca, t4);
-        if (hb) cb = crc_chunk(v, p0 + beg_b, p0 + beg_b + kCrcChunk, 0u, t4);
-      }
-      acc ^= crc_shift(t.crc_mat, nch - 1 - j, ca);
-      if (hb) acc ^= crc_shift(t.crc_mat, nch - 1 - jb, cb);
+    for (int j = lane; j < nch; j += 64) {
+      const int end = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
+      const int beg = max(0, end - kCrcChunk);
+      const uint32_t c = crc_chunk(v, p0 + beg, p0 + end, j == 0 ? reg : 0u, t4);
+      acc ^= crc_shift(t.crc_mat, nch - 1 - j, c);
     }
     reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
   }
@@ -1405,17 +1412,14 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     if (j == 0) { s1 = -2; s2 = 0; }
     else { s1 = 2 * j - 1; s2 = 2 * j < F.T ? 2 * j : -1; }
   };
-  auto job_loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) {
+  auto job_loads = [&](const FrameS &F, int j, f2v (&r)[8]) {
     int s1, s2;
     job_syms(F, j, s1, s2);
     const int data0 = F.start + 3 * SYM;
     const int p1 = (s1 == -2 ? F.start + 2 * SYM : data0 + s1 * SYM) + CP;
     const int p2 = s2 >= 0 ? data0 + s2 * SYM + CP : p1;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      r1[m] = F.X[p1 + lane + 64 * m];
-      r2[m] = F.X[p2 + lane + 64 * m];
-    }
+    for (int m = 0; m < 8; ++m) r[m] = f2v{F.X[p1 + lane + 64 * m], F.X[p2 + lane + 64 * m]};
   };
 
   float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
@@ -1455,7 +1459,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // one empty job, so every frame passes through its frame end)
   // c1 / c2: the job's samples; issue_next() refills them with the next job's once they
   // are folded into the FFT input, so those loads fly under this job's FFT, equalise, demap, finish
-  auto run_job = [&](const FrameS &cur, const int jcur, float (&c1)[8], float (&c2)[8], auto &&issue_next) {
+  auto run_job = [&](const FrameS &cur, const int jcur, f2v (&c)[8], auto &&issue_next) {
 #define DSTAMP(k, cond)                                                                   \
   do {                                                                                  \
     if (w.stamps && (cond) && lane == 0) w.stamps[(int64_t)cur.f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -1477,18 +1481,18 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       int s1, s2;
       job_syms(cur, jcur, s1, s2);
       const bool ce = s1 == -2;
-      const float first1 = rlane(c1[0], 0), first2 = rlane(c2[0], 0);
+      const float first1 = rlane(c[0].x, 0), first2 = rlane(c[0].y, 0);
       int ne1 = 0, ne2 = 0, nf = 0;
-      float2 v[8];
+      f2v v[8];
       // no second symbol: A = B = 0 zeroes the imaginary half (its samples are finite: the
       // last job re-reads the first symbol's, checked below in chunk mode)
-      const float A2 = s2 >= 0 ? cur.A : 0.f, B2 = s2 >= 0 ? cur.B : 0.f;
+      const f2v Av = {cur.A, s2 >= 0 ? cur.A : 0.f}, Bv = {cur.B, s2 >= 0 ? cur.B : 0.f};
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        ne1 |= c1[m] != first1;
-        ne2 |= c2[m] != first2;
-        if (chunk_mode) nf |= !isfinite(c1[m]) || !isfinite(c2[m]); // received: stage 0 saw them
-        v[m] = make_float2(fmaf(c1[m], cur.A, cur.B), fmaf(c2[m], A2, B2));
+        ne1 |= c[m].x != first1;
+        ne2 |= c[m].y != first2;
+        if (chunk_mode) nf |= !isfinite(c[m].x) || !isfinite(c[m].y); // received: stage 0 saw them
+        v[m] = __builtin_elementwise_fma(c[m], Av, Bv);
       }
       // a window is constant iff every raw sample equals its first one (all-zero spectrum)
       const bool const1 = __ballot(ne1) == 0, const2 = __ballot(ne2) == 0;
@@ -1779,19 +1783,19 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   };
   // every load is unconditional (a frame without data symbols reads its CE window, the
   // last job re-reads its own samples), so the in-order vmcnt accounting stays exact
-  auto loads = [&](const FrameS &F, int j, float (&r1)[8], float (&r2)[8]) { job_loads(F, j, r1, r2); };
+  auto loads = [&](const FrameS &F, int j, f2v (&r)[8]) { job_loads(F, j, r); };
   // the sample registers are refilled with the next job as soon as the FFT input is formed
   FrameS fa, fb;
   int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
   if (ka >= nfr) return;
   const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
-  float r1[8], r2[8];
-  loads(fa, ja, r1, r2);
+  f2v r[8];
+  loads(fa, ja, r);
   for (;;) {
     fb = fa; kb = ka; jb = ja;
     const bool hb = advance(fb, kb, jb);
-    run_job(fa, ja, r1, r2, [&] { if (hb) loads(fb, jb, r1, r2); });
+    run_job(fa, ja, r, [&] { if (hb) loads(fb, jb, r); });
     if (!hb) break;
     fa = fb; ka = kb; ja = jb;
   }
