@@ -54,8 +54,8 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone)
 #endif
 #ifndef AMOD_DEMOD_WPE
-#define AMOD_DEMOD_WPE 4                     // k_demod: 112 registers, no VGPR spills (at 5 waves /
-                                             // 96 registers it spilled 37: -13 % chain time)
+#define AMOD_DEMOD_WPE 4                     // k_demod: 104 registers, no VGPR spills; LDS (FFT exchange
+                                             // rows, twiddles, bit streams) allows 4 workgroups per CU on C2 anyway
 #endif
 
 // Dynamic LDS of k_detect, sized per launch (amod_fast_lds_bytes): one region reused
