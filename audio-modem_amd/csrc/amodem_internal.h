@@ -456,6 +456,7 @@ hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sy
                             int64_t maxcount, double *out, hipStream_t s);
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,
                               int nwin, float *out, hipStream_t s);
+hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s);
 // runtime.cpp: a context's device and stream for the host-side orchestrators
 int amod_ctx_device(const amod_ctx *ctx);
 hipStream_t amod_ctx_stream(const amod_ctx *ctx);

@@ -21,6 +21,8 @@
 //                sum seg[i]^2 in the reference's order, then corr / sqrt(sEnergy E),
 //                one lane per position, IEEE double (f32 x f32 products are exact in
 //                double; sqrt and the quotient correctly rounded).
+//   k_gather     the granules of the cleaned stream the host state machine reads (its
+//                scan and refine regions), packed for one device-to-host copy
 //   k_window     _demodulateFrame's per-window peak normalisation (app.js:916-925):
 //                mx = max |x|, x / mx when mx > 1e-6 (f32 of the double quotient).
 // Built with -ffp-contract=off.
@@ -278,6 +280,15 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
   out[base[r] + j] = denom > 0.001 ? corr / denom : __builtin_nan("");
 }
 
+// the host's sparse copy of the cleaned stream: compact granule j (1024 samples) is stream
+// granule src[j]; one workgroup per granule, float4 per thread, coalesced both ways
+__global__ __launch_bounds__(256) void k_gather(const float *__restrict__ y, const int32_t *__restrict__ src,
+                                                float *__restrict__ out) {
+  const int64_t j = blockIdx.x;
+  const float4 *const a = reinterpret_cast<const float4 *>(y + (int64_t)src[j] * 1024);
+  reinterpret_cast<float4 *>(out + j * 1024)[threadIdx.x] = a[threadIdx.x];
+}
+
 __global__ __launch_bounds__(256) void k_window(const float *__restrict__ y, int64_t n, const int64_t *__restrict__ pos,
                                                 const int32_t *__restrict__ len, const int64_t *__restrict__ woff,
                                                 float *__restrict__ out) {
@@ -334,6 +345,11 @@ hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sy
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
   hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
                      pre1_energy, first, base, count, nranges, out);
+  return hipGetLastError();
+}
+hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s) {
+  if (ng <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amod::k_gather, dim3(ng), dim3(256), 0, s, y, src, out);
   return hipGetLastError();
 }
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,

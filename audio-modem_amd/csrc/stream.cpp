@@ -25,11 +25,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -40,6 +43,7 @@ namespace {
 constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
 const int64_t kEmaChunk = amod_ema_chunk(); // k_ema chunk (EMA end states are reported per chunk)
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
+constexpr int kGranLog = 10, kGran = 1 << kGranLog; // sparse host copy granule (samples)
 enum { IDLE = 0, DETECTED = 1, COLLECTING = 2 };
 
 struct DBuf {
@@ -104,6 +108,9 @@ struct Receiver {
   std::vector<std::pair<int64_t, int64_t>> *fails = nullptr; // (block, preambleGlobalPos) of failed refinements
   int64_t fine_host = 0; // positions the host had to correlate itself
   size_t cursor = 0;     // FineTable lookup cursor
+  // diagnostics (AMOD_STREAM_DIAG): scan positions stepped, time spent waiting for pieces
+  int64_t scanned = 0;
+  mutable double wait_ms = 0;
 
   // the host copy of the cleaned stream arrives in pieces: local samples [0, avail) are
   // there; a read past it waits for the piece that holds it
@@ -113,10 +120,29 @@ struct Receiver {
   // buffer[i mod capacity] for any i at or after the oldest sample (app.js:580-589)
   const float *ring = nullptr;
   int64_t tw_live = -1; // totalWritten (live mode)
+  // sparse host copy (SparseCopy below): local granule g (kGran samples) is at gptr[g], or
+  // not on the host yet (null: present(g) brings it and returns its pointer)
+  std::atomic<const float *> *gptr = nullptr;
+  const std::function<const float *(int64_t)> *present = nullptr;
+  const std::function<const float *(int64_t)> *copied = nullptr; // granule g if it is (being) copied, else null
+  const float *granule(int64_t g) const {
+    const float *p = gptr[g].load(std::memory_order_acquire);
+    return p ? p : (*present)(g);
+  }
+  const float *peek(int64_t g) const { // granule g if on the host or on its way (never fetched)
+    const float *p = gptr[g].load(std::memory_order_acquire);
+    return p ? p : (*copied)(g);
+  }
   double S(int64_t i) const {
     if (ring) { int64_t r = i % cap; if (r < 0) r += cap; return (double)ring[r]; }
     if (i < lo || i >= lo + nloc) return 0.0;
-    if (i - lo >= avail) { (*wait_y)(i - lo + 1); avail = piece_end(i - lo); }
+    if (gptr) return (double)granule((i - lo) >> kGranLog)[(i - lo) & (kGran - 1)];
+    if (i - lo >= avail) {
+      const auto t0 = std::chrono::steady_clock::now();
+      (*wait_y)(i - lo + 1);
+      avail = piece_end(i - lo);
+      wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     return (double)y[i - lo];
   }
   std::function<int64_t(int64_t)> piece_end;
@@ -139,6 +165,34 @@ struct Receiver {
     const double min_e = 0.001;
     double best = 0;
     int64_t best_pos = -1;
+    // sparse host copy: positions whose reads lie in one contiguous run of granules on the
+    // host are stepped straight from the array, the others one at a time through S()
+    // (which brings their granule); only granules the scan actually reads are fetched
+    if (!ring && gptr && st.ac_pos >= lo && total <= lo + nloc) {
+      while (st.ac_pos <= scan_end) {
+        const int64_t g0 = (st.ac_pos - lo) >> kGranLog, glim = (total - 1 - lo) >> kGranLog;
+        const float *p0 = granule(g0);
+        int64_t g = g0 + 1;
+        while (g <= glim && peek(g) == p0 + (g - g0) * kGran) ++g;
+        const int64_t lim = std::min(scan_end, lo + g * kGran - 2 * half - 1); // reads pos + 512 < run end
+        const bool det = lim >= st.ac_pos ? scan_direct(p0 - (lo + g0 * kGran), lim, scan_end, min_e, best, best_pos)
+                                          : scan_step(scan_end, min_e, best, best_pos);
+        if (det) return;
+      }
+      if (best > 0.5 && best_pos >= 0) { st.pre_pos = best_pos; st.state = DETECTED; }
+      return;
+    }
+    // the whole host copy: every sample this call can read, [ac_pos, total), is there
+    if (!ring && !gptr && st.ac_pos >= lo && total <= lo + nloc && total > st.ac_pos) {
+      (void)S(total - 1); // waits for the piece holding the last one
+      if (total - lo <= avail) {
+        if (!scan_direct(y - lo, scan_end, scan_end, min_e, best, best_pos) && best > 0.5 && best_pos >= 0) {
+          st.pre_pos = best_pos;
+          st.state = DETECTED;
+        }
+        return;
+      }
+    }
     // p^2 < 0.49 ra rb (rounded products, relative error ~1e-16) proves the rounded
     // quotient is below 0.5: the division is only evaluated where it can matter
     while (st.ac_pos <= scan_end) {
@@ -156,12 +210,72 @@ struct Receiver {
         st.ac_rb += b_in * b_in - mid * mid;
       }
       st.ac_pos++;
+      ++scanned;
       if (best > 0.5 && best_pos >= 0 && st.ac_ra > min_e && st.ac_rb > min_e) {
         const double cur = (st.ac_p * st.ac_p) / (st.ac_ra * st.ac_rb);
         if (cur < best * 0.7) { st.pre_pos = best_pos; st.state = DETECTED; return; }
       }
     }
     if (best > 0.5 && best_pos >= 0) { st.pre_pos = best_pos; st.state = DETECTED; }
+  }
+
+  // the scan loop above over a plain array yy (yy[i] = stream sample i), positions up to
+  // lim (<= scan_end): the same operations in the same order; true when it detected
+  bool scan_direct(const float *yy, int64_t lim, int64_t scan_end, double min_e, double &best, int64_t &best_pos) {
+    const int64_t half = 256;
+    double p = st.ac_p, ra = st.ac_ra, rb = st.ac_rb;
+    int64_t pos = st.ac_pos;
+    while (pos <= lim) {
+      if (ra > min_e && rb > min_e) {
+        const double pp = p * p, rr = ra * rb;
+        if (pp >= 0.49 * rr) {
+          const double metric = pp / rr;
+          if (metric > 0.5 && metric > best) { best = metric; best_pos = pos; }
+        }
+      }
+      if (pos < scan_end) {
+        const double a_out = yy[pos], mid = yy[pos + half], b_in = yy[pos + 2 * half];
+        p += mid * b_in - a_out * mid;
+        ra += mid * mid - a_out * a_out;
+        rb += b_in * b_in - mid * mid;
+      }
+      pos++;
+      ++scanned;
+      if (best > 0.5 && best_pos >= 0 && ra > min_e && rb > min_e) {
+        const double cur = (p * p) / (ra * rb);
+        if (cur < best * 0.7) {
+          st.ac_p = p; st.ac_ra = ra; st.ac_rb = rb; st.ac_pos = pos;
+          st.pre_pos = best_pos; st.state = DETECTED;
+          return true;
+        }
+      }
+    }
+    st.ac_p = p; st.ac_ra = ra; st.ac_rb = rb; st.ac_pos = pos;
+    return false;
+  }
+  // one position of the scan loop through S(); true when it detected
+  bool scan_step(int64_t scan_end, double min_e, double &best, int64_t &best_pos) {
+    const int64_t half = 256;
+    if (st.ac_ra > min_e && st.ac_rb > min_e) {
+      const double pp = st.ac_p * st.ac_p, rr = st.ac_ra * st.ac_rb;
+      if (pp >= 0.49 * rr) {
+        const double metric = pp / rr;
+        if (metric > 0.5 && metric > best) { best = metric; best_pos = st.ac_pos; }
+      }
+    }
+    if (st.ac_pos < scan_end) {
+      const double a_out = S(st.ac_pos), mid = S(st.ac_pos + half), b_in = S(st.ac_pos + 2 * half);
+      st.ac_p += mid * b_in - a_out * mid;
+      st.ac_ra += mid * mid - a_out * a_out;
+      st.ac_rb += b_in * b_in - mid * mid;
+    }
+    st.ac_pos++;
+    ++scanned;
+    if (best > 0.5 && best_pos >= 0 && st.ac_ra > min_e && st.ac_rb > min_e) {
+      const double cur = (st.ac_p * st.ac_p) / (st.ac_ra * st.ac_rb);
+      if (cur < best * 0.7) { st.pre_pos = best_pos; st.state = DETECTED; return true; }
+    }
+    return false;
   }
 
   // _refineAndCollect (app.js:849-898)
@@ -276,6 +390,7 @@ void run_blocks(Receiver &rx, const RxState &start, int64_t stop, bool first_onl
 // speculative segment demodulated from the identical post-reset state, and adopts the
 // segment's trajectory from there (or covers the whole segment itself).
 Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, int nthreads, int64_t &fine_host) {
+  const auto t_par0 = std::chrono::steady_clock::now();
   const int64_t span = nblocks - start.block;
   const char *ms = getenv("AMOD_STREAM_MINSEG"); // tests: force short speculative segments
   const int64_t minseg = ms ? std::max(1, atoi(ms)) : 64;
@@ -300,6 +415,7 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
     });
   }
   for (auto &t : th) t.join();
+  const auto t_threads = std::chrono::steady_clock::now();
   Traj total = std::move(seg[0]);
   Receiver rx = proto;
   for (int k = 1; k < T; ++k) {
@@ -320,6 +436,16 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
   }
   fine_host += rx.fine_host;
   for (auto &r : rxs) fine_host += r.fine_host;
+  if (getenv("AMOD_STREAM_DIAG")) {
+    int64_t sc = rx.scanned;
+    double wmax = 0;
+    for (auto &r : rxs) { sc += r.scanned; wmax = std::max(wmax, r.wait_ms); }
+    fprintf(stderr, "[stream] run_parallel: %d segments, threads %.3f ms (max wait %.3f ms), merge %.3f ms (wait %.3f), "
+            "scanned %lld positions, frames %zu\n", T,
+            std::chrono::duration<double, std::milli>(t_threads - t_par0).count(), wmax,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_threads).count(), rx.wait_ms,
+            (long long)sc, total.frames.size());
+  }
   return total;
 }
 
@@ -345,15 +471,20 @@ struct StreamCache {
   DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
   DBuf d_pre1, d_first, d_base, d_count, d_out;
   DBuf w_pos, w_len, w_woff, w_win, w_res, w_pay;
-  Pinned yh, hot_h, metric_h;
+  DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
+  Pinned yh, yc, hot_h, metric_h;
+  Pinned w_res_h, w_pay_h;                  // window decoder: results and payload rows (pinned D2H)
   bool apow_ready = false;
   hipStream_t s2 = nullptr;                 // the cleaned stream's device-to-host copy
   static constexpr int kPieces = 16;
-  hipEvent_t ema_done = nullptr, piece[kPieces] = {};
+  hipEvent_t ema_done = nullptr, gathered = nullptr, piece[kPieces] = {}, cpiece[kPieces] = {};
   ~StreamCache() {
     if (s2) { (void)hipStreamSynchronize(s2); (void)hipStreamDestroy(s2); }
     if (ema_done) (void)hipEventDestroy(ema_done);
+    if (gathered) (void)hipEventDestroy(gathered);
     for (auto e : piece)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : cpiece)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -375,13 +506,156 @@ struct Prepass {
   double t_ema = 0, t_fine = 0;
   const float *y() const { return c->d_y.as<float>(); }
   std::function<void(int64_t)> wait_fn = [this](int64_t g) { wait_y(g); };
+  // sparse: only the first piece of the cleaned stream is copied to the host at once (the
+  // metadata phase reads the stream's start); the state machine's parallel phase then gets
+  // just the granules it reads (sparse_setup), and a read past the first piece before that
+  // starts the full copy
+  bool sparse = false;
+  mutable bool full_started = false;
+  mutable std::mutex mu;
+  hipStream_t s_main = nullptr;
   // the host copy of the cleaned stream holds local samples [0, g)
   void wait_y(int64_t g) const {
+    if (g > n / StreamCache::kPieces) start_full();
     for (int q = 0; q < StreamCache::kPieces; ++q) {
       const int64_t a = n * q / StreamCache::kPieces;
       if (a >= g) break;
       (void)hipEventSynchronize(c->piece[q]);
     }
+  }
+  // pieces [q0, kPieces) of the full copy (q0 = 1: the rest after the first)
+  hipError_t enqueue_pieces(int q0) const {
+    for (int q = q0; q < StreamCache::kPieces; ++q) {
+      const int64_t a = n * q / StreamCache::kPieces, b = n * (q + 1) / StreamCache::kPieces;
+      if (b > a) {
+        const hipError_t e = hipMemcpyAsync(c->yh.p + a, c->d_y.as<float>() + a, sizeof(float) * (size_t)(b - a),
+                                            hipMemcpyDeviceToHost, c->s2);
+        if (e != hipSuccess) return e;
+      }
+      const hipError_t e = hipEventRecord(c->piece[q], c->s2);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  void start_full() const {
+    std::lock_guard<std::mutex> lk(mu);
+    if (full_started) return;
+    (void)enqueue_pieces(1);
+    full_started = true;
+  }
+
+  // ---- sparse copy of the cleaned stream (the parallel phase's reads)
+  int64_t ng = 0, first_g = 0; // granules; those inside the first piece
+  std::vector<int32_t> cidx;   // granule -> packed index (-1: not packed)
+  std::unique_ptr<std::atomic<const float *>[]> gptr;
+  std::unique_ptr<std::atomic<bool>[]> cready; // packed piece q has landed
+  std::atomic<bool> first_ready{false};
+  mutable std::atomic<int64_t> fallbacks{0};
+  int64_t npacked = 0;
+  std::function<const float *(int64_t)> present_fn = [this](int64_t g) { return present(g); };
+  std::function<const float *(int64_t)> copied_fn = [this](int64_t g) -> const float * {
+    return g < first_g || cidx[g] >= 0 ? present(g) : nullptr;
+  };
+  // granule g on the host: the first piece, the packed copy, or fetched now (16 granules)
+  const float *present(int64_t g) {
+    const float *p;
+    if (g < first_g) {
+      if (!first_ready.load(std::memory_order_acquire)) {
+        (void)hipEventSynchronize(c->piece[0]);
+        first_ready.store(true, std::memory_order_release);
+      }
+      p = c->yh.as<float>() + g * kGran;
+    } else if (cidx[g] >= 0) {
+      const int q = (int)(cidx[g] * (int64_t)StreamCache::kPieces / std::max<int64_t>(npacked, 1));
+      if (!cready[q].load(std::memory_order_acquire)) {
+        (void)hipEventSynchronize(c->cpiece[q]);
+        cready[q].store(true, std::memory_order_release);
+      }
+      p = c->yc.as<float>() + (int64_t)cidx[g] * kGran;
+    } else {
+      std::lock_guard<std::mutex> lk(mu);
+      if ((p = gptr[g].load(std::memory_order_acquire))) return p;
+      const int64_t g1 = std::min(ng, g + 16);
+      (void)hipMemcpy(c->yh.as<float>() + g * kGran, c->d_y.as<float>() + g * kGran,
+                      sizeof(float) * (size_t)((g1 - g) * kGran), hipMemcpyDeviceToHost);
+      fallbacks += g1 - g;
+      for (int64_t k = g + 1; k < g1; ++k)
+        if (!gptr[k].load(std::memory_order_acquire) && cidx[k] < 0)
+          gptr[k].store(c->yh.as<float>() + k * kGran, std::memory_order_release);
+      p = c->yh.as<float>() + g * kGran;
+    }
+    gptr[g].store(p, std::memory_order_release);
+    return p;
+  }
+  // Marks the granules the state machine reads from `start` on (the scan from each frame's
+  // end through the next hot region and its block, the refine windows, the start of every
+  // speculative segment), packs them on the GPU and copies them to the host in pieces.
+  // Reads outside them still work (present() fetches). Returns false when the full copy
+  // is (or was) used instead.
+  bool sparse_setup(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int nthreads) {
+    if (!sparse || full_started) return false;
+    ng = n >> kGranLog;
+    first_g = (n / StreamCache::kPieces) >> kGranLog;
+    std::vector<uint8_t> need((size_t)ng, 0);
+    auto mark = [&](int64_t a, int64_t b) { // local samples [a, b)
+      a = std::max<int64_t>(a, first_g * kGran);
+      b = std::min<int64_t>(b, n);
+      for (int64_t g = a >> kGranLog; a < b && g <= (b - 1) >> kGranLog; ++g) need[(size_t)g] = 1;
+    };
+    // hot regions (local), blocks less than 2 K samples apart merged
+    std::vector<std::pair<int64_t, int64_t>> reg;
+    const uint8_t *hot = c->hot_h.as<uint8_t>();
+    for (int64_t b = 0; b < n / 32; ++b) {
+      if (!hot[b]) continue;
+      if (!reg.empty() && 32 * b <= reg.back().second + 2048) reg.back().second = 32 * b + 32;
+      else reg.push_back({32 * b, 32 * b + 32});
+    }
+    const int32_t maxp = start.meta_received ? (start.chunk_size ? start.chunk_size : 4096) + 11 : 280;
+    const int64_t F = amod_estimate_frame_samples(cfg, maxp);
+    const int64_t R = 3 * (int64_t)cfg->cp_len + cfg->symbol_len + 64; // refine radius + correlation
+    const int64_t W = 2048;                                             // the metric's drop after the plateau
+    // the scan from local position p to the detection in the first hot region after it
+    auto scan_from = [&](int64_t p) {
+      auto it = std::lower_bound(reg.begin(), reg.end(), std::make_pair(p, (int64_t)0));
+      mark(p - 1024, it == reg.end() ? p + F + W : it->first);
+    };
+    for (size_t k = 0; k < reg.size(); ++k) {
+      mark(reg[k].first - R - 1024, reg[k].second + R + W);
+      scan_from(reg[k].first - R + F); // the scan after the frame detected in region k
+    }
+    scan_from(start.ac_pos - lo);
+    const int64_t span = nblocks - start.block; // run_parallel's speculative segments
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, span / 64));
+    for (int k = 1; k < T; ++k) scan_from((start.block + span * k / T) * kBlock - 511 - lo - 1024);
+    std::vector<int32_t> src;
+    cidx.assign((size_t)ng, -1);
+    for (int64_t g = first_g; g < ng; ++g)
+      if (need[(size_t)g]) { cidx[(size_t)g] = (int32_t)src.size(); src.push_back((int32_t)g); }
+    if (2 * (int64_t)src.size() > ng - first_g) { start_full(); return false; } // not worth it
+    npacked = (int64_t)src.size();
+    gptr.reset(new std::atomic<const float *>[(size_t)ng]);
+    for (int64_t g = 0; g < ng; ++g) gptr[g].store(nullptr, std::memory_order_relaxed);
+    cready.reset(new std::atomic<bool>[StreamCache::kPieces]);
+    for (int q = 0; q < StreamCache::kPieces; ++q) cready[q].store(npacked == 0, std::memory_order_relaxed);
+    if (npacked) {
+      if (c->d_c.alloc(sizeof(float) * (size_t)npacked * kGran) || c->d_gsrc.alloc(sizeof(int32_t) * src.size()) ||
+          c->yc.alloc(sizeof(float) * (size_t)npacked * kGran)) { start_full(); return false; }
+      if (!c->gathered) (void)hipEventCreateWithFlags(&c->gathered, hipEventDisableTiming);
+      for (auto &e : c->cpiece)
+        if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      bool ok = hipMemcpyAsync(c->d_gsrc.p, src.data(), sizeof(int32_t) * src.size(), hipMemcpyHostToDevice, s_main) == hipSuccess &&
+                amod_launch_gather(c->d_y.as<float>(), c->d_gsrc.as<int32_t>(), (int)npacked, c->d_c.as<float>(), s_main) == hipSuccess &&
+                hipEventRecord(c->gathered, s_main) == hipSuccess && hipStreamWaitEvent(c->s2, c->gathered, 0) == hipSuccess;
+      for (int q = 0; ok && q < StreamCache::kPieces; ++q) {
+        const int64_t a = npacked * q / StreamCache::kPieces, b = npacked * (q + 1) / StreamCache::kPieces;
+        if (b > a)
+          ok = hipMemcpyAsync(c->yc.as<float>() + a * kGran, c->d_c.as<float>() + a * kGran,
+                              sizeof(float) * (size_t)((b - a) * kGran), hipMemcpyDeviceToHost, c->s2) == hipSuccess;
+        ok = ok && hipEventRecord(c->cpiece[q], c->s2) == hipSuccess;
+      }
+      if (!ok) { (void)hipStreamSynchronize(c->s2); start_full(); return false; }
+    }
+    return true;
   }
 
   // samples: host memory, or device memory when `device` (read for [0, nvalid); the
@@ -440,12 +714,16 @@ struct Prepass {
     }
     S_TRY(hipEventRecord(c->ema_done, s));
     S_TRY(hipStreamWaitEvent(c->s2, c->ema_done, 0));
-    for (int q = 0; q < StreamCache::kPieces; ++q) {
-      const int64_t a = n * q / StreamCache::kPieces, b = n * (q + 1) / StreamCache::kPieces;
-      if (b > a)
-        S_TRY(hipMemcpyAsync(c->yh.p + a, c->d_y.as<float>() + a, sizeof(float) * (size_t)(b - a),
-                             hipMemcpyDeviceToHost, c->s2));
-      S_TRY(hipEventRecord(c->piece[q], c->s2));
+    s_main = s;
+    full_started = false;
+    if (sparse) { // the first piece now, the rest on demand (sparse_setup / start_full)
+      const int64_t b = n / StreamCache::kPieces;
+      if (b > 0)
+        S_TRY(hipMemcpyAsync(c->yh.p, c->d_y.as<float>(), sizeof(float) * (size_t)b, hipMemcpyDeviceToHost, c->s2));
+      S_TRY(hipEventRecord(c->piece[0], c->s2));
+    } else {
+      S_TRY(enqueue_pieces(0));
+      full_started = true;
     }
     S_TRY(hipStreamSynchronize(s));
     fixed = (int64_t)fx;
@@ -527,17 +805,21 @@ struct Prepass {
 // Decodes frames' windows on the GPU (k_window peak normalisation + chunk-mode decode);
 // res[i] / payload row i for frame i (lost frames get AMOD_E_STREAM_LOST).
 struct WindowDecoder {
-  std::vector<amod_result> res;
-  std::vector<uint8_t> pay;
+  std::vector<amod_result> res; // frame i - a of the last run
+  std::vector<int> slot;         // its row in the pinned payload (-1: lost)
+  const uint8_t *ph = nullptr;   // pinned payload rows
+  std::vector<uint8_t> zero_row;
   int64_t stride = 16;
   double t_ms = 0;
+  // payload row of frame i - a of the last run (zeros for a lost window)
+  const uint8_t *row(size_t k) const { return slot[k] < 0 ? zero_row.data() : ph + (size_t)stride * slot[k]; }
 
   int run(amod_ctx *ctx, const amod_cfg *cfg, const Prepass &pp, const std::vector<FrameEv> &fr, size_t a, size_t b,
           hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<int64_t> pos, woff;
     std::vector<int32_t> len;
-    std::vector<int> slot(b - a, -1);
+    slot.assign(b - a, -1);
     int64_t tot = 0, maxlen = 0;
     for (size_t i = a; i < b; ++i) {
       if (fr[i].lost) continue;
@@ -549,10 +831,13 @@ struct WindowDecoder {
     }
     const int nw = (int)pos.size();
     stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
-    std::vector<amod_result> r(nw);
-    std::vector<uint8_t> py((size_t)stride * nw);
+    zero_row.assign((size_t)stride, 0);
     StreamCache &c = *pp.c;
     DBuf &d_pos = c.w_pos, &d_len = c.w_len, &d_woff = c.w_woff, &d_win = c.w_win, &d_res = c.w_res, &d_pay = c.w_pay;
+    S_TRY(c.w_res_h.alloc(sizeof(amod_result) * (size_t)std::max(nw, 1)));
+    S_TRY(c.w_pay_h.alloc((size_t)stride * std::max(nw, 1)));
+    const amod_result *rh = c.w_res_h.as<amod_result>();
+    ph = c.w_pay_h.as<uint8_t>();
     if (nw) {
       S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
@@ -571,19 +856,18 @@ struct WindowDecoder {
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
                               nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
       if (rc) return rc;
-      S_TRY(hipMemcpyAsync(r.data(), d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
-      S_TRY(hipMemcpyAsync(py.data(), d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
+      S_TRY(hipMemcpyAsync(c.w_res_h.p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
+      S_TRY(hipMemcpyAsync(c.w_pay_h.p, d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
       S_TRY(hipStreamSynchronize(s));
     }
-    res.assign(b - a, amod_result{});
-    pay.assign((size_t)stride * (b - a), 0);
+    res.resize(b - a);
     for (size_t i = a; i < b; ++i) {
       amod_result &o = res[i - a];
       if (slot[i - a] < 0) {
+        o = amod_result{};
         o.status = AMOD_E_STREAM_LOST; o.preamble_idx = -1; o.coarse_idx = -1; o.frame_type = -1;
       } else {
-        o = r[slot[i - a]];
-        std::memcpy(pay.data() + (size_t)stride * (i - a), py.data() + (size_t)stride * slot[i - a], (size_t)stride);
+        o = rh[slot[i - a]];
       }
     }
     t_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -666,6 +950,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
   amod_stream_stats stt{};
   Prepass pp;
+  pp.sparse = !getenv("AMOD_STREAM_FULLCOPY"); // (diagnostics: the whole cleaned stream to the host)
   {
     const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s, device);
     if (rc) return rc;
@@ -682,8 +967,9 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     assembler = own;
   }
   struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
-  const Receiver proto = pp.receiver(cfg);
+  Receiver proto = pp.receiver(cfg);
   const int nthreads = receiver_threads();
+  bool sparse_done = false;
   int64_t nfr = 0, frames_decoded = 0, frame_errors = 0, fine_host = 0;
   std::vector<int64_t> fails_out;
   WindowDecoder wd;
@@ -708,7 +994,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
         ++nfr;
         if (r.status != AMOD_OK) { ++frame_errors; continue; }
         ++frames_decoded;
-        const uint8_t *sl = wd.pay.data() + (size_t)wd.stride * (i - c0);
+        const uint8_t *sl = wd.row(i - c0);
         if (r.frame_type == 0xFE) {
           if (!r.crc_valid) { ++frame_errors; continue; }
           const int m = amod_asm_metadata(assembler, r.total_chunks, r.total_size, r.chunk_size, sl + r.name_off,
@@ -744,11 +1030,22 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
       run_blocks(rx, st, nblocks, true, nullptr, tr, nullptr);
       fine_host += rx.fine_host;
     } else {
+      if (!sparse_done) { // from here on the state machine reads only where frames start
+        sparse_done = true;
+        if (pp.sparse_setup(cfg, st, nblocks, nthreads)) {
+          proto.gptr = pp.gptr.get(); proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
+        }
+      }
       tr = run_parallel(proto, st, nblocks, nthreads, fine_host);
     }
     int64_t chg = -1;
+    const auto t_dd = clk::now();
     const int rc = decode_dispatch(tr.frames, 0, tr.frames.size(), chg);
     if (rc) return rc;
+    if (getenv("AMOD_STREAM_DIAG"))
+      fprintf(stderr, "[stream] decode_dispatch of %zu frames: %.3f ms (since prepass %.3f ms)\n", tr.frames.size(),
+              std::chrono::duration<double, std::milli>(clk::now() - t_dd).count(),
+              std::chrono::duration<double, std::milli>(t_dd - t_gpu_pre).count());
     if (chg >= 0) {
       // keep what happened up to that frame; re-run the rest with the new window length
       const RxState after = tr.frames[chg].after;
@@ -775,6 +1072,9 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     stt.final_state = final_state.state;
     stt.final_scan_pos = final_state.ac_pos;
     stt.fine_host_positions = fine_host;
+    if (getenv("AMOD_STREAM_DIAG"))
+      fprintf(stderr, "[stream] sparse copy: %lld of %lld granules packed, %lld fetched on demand, full copy %d\n",
+              (long long)pp.npacked, (long long)pp.ng, (long long)pp.fallbacks.load(), (int)pp.full_started);
     stt.t_decode_ms = wd.t_ms;
     stt.t_total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
     stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - wd.t_ms;
@@ -851,7 +1151,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       apply_meta(wd.res[0], t1.frames[0].after);
       tr.frames.push_back(t1.frames[0]);
       res.push_back(wd.res[0]);
-      pay.insert(pay.end(), wd.pay.begin(), wd.pay.begin() + std::min<int64_t>(wd.stride, stride));
+      pay.insert(pay.end(), wd.row(0), wd.row(0) + std::min<int64_t>(wd.stride, stride));
       if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
       st = t1.frames[0].after;
       tr.end = st;
@@ -874,7 +1174,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       if (rc) return rc;
       res.insert(res.end(), wd.res.begin(), wd.res.end());
       for (size_t i = c0; i < c1; ++i) { // rows at the caller's stride
-        const uint8_t *row = wd.pay.data() + (size_t)wd.stride * (i - c0);
+        const uint8_t *row = wd.row(i - c0);
         pay.insert(pay.end(), row, row + std::min<int64_t>(wd.stride, stride));
         if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
       }
