@@ -1163,6 +1163,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
       const int tact = (act_end - data0 + SYM - 1) / SYM;
       T = min(M, max(min(M, FIRST_SYMS), tact));
     }
+    T = min(T, w.mcap); // the k_demod bit stream's capacity (a parse past it: exact path)
     DetRec d;
     d.route = ROUTE_DEMOD; d.flags = 0; d.start = start; d.M = M; d.T = T; d.coarse = sm.coarse;
     d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
@@ -1231,7 +1232,7 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
     return;
   }
   DetRec d;
-  d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = d.M; d.coarse = -1;
+  d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = min(d.M, w.mcap); d.coarse = -1;
   d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
   w.det[f] = d;
   if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);

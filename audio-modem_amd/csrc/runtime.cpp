@@ -502,7 +502,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   rc = ensure_chain(ctx, nframes);
   if (rc) return rc;
   w.nb_cap = dims.nb_cap; w.fine_cap = dims.fine_cap; w.mcap = dims.mcap; w.fast_len = dims.fast_len;
-  amod_demod_stream_words(d, dims.mcap, &w.stream_words, &w.vote_off);
+  if (const char *mc = getenv("AMOD_DEMOD_MCAP")) w.mcap = std::min(w.mcap, std::max(1, atoi(mc))); // experiments
+  amod_demod_stream_words(d, w.mcap, &w.stream_words, &w.vote_off);
   w.det = (amod::DetRec *)ctx->det.p;
   if (!ctx->cu_count) {
     hipDeviceProp_t prop;
