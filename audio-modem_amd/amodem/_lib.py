@@ -25,6 +25,7 @@ OK = 0
 E_CAPACITY = 100
 FLAG_SPAN = 1 << 9
 FLAG_SOFT = 1 << 10
+FLAG_REPLAY = 1 << 11
 FLAG_EXACT = 1 << 15
 
 

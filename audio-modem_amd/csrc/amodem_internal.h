@@ -74,10 +74,11 @@ struct DevTxWork {
 };
 
 // k_detect / k_chunk_prep -> k_demod: one record per frame
-enum { ROUTE_DEMOD = 0, ROUTE_DONE = 1, ROUTE_EXACT = 2 };
+enum { ROUTE_DEMOD = 0, ROUTE_DONE = 1, ROUTE_EXACT = 2, ROUTE_REPLAY = 3 };
 struct DetRec {
-  int32_t route;   // ROUTE_DEMOD: demodulate; ROUTE_DONE: result written; ROUTE_EXACT: listed
-  int32_t flags;   // reserved (0)
+  int32_t route;   // ROUTE_DEMOD: demodulate; ROUTE_DONE: result written; ROUTE_EXACT: listed;
+                   // ROUTE_REPLAY: detection replayed by the exact kernel, for k_demod's list launch
+  int32_t flags;   // 0; a replayed detection: AMOD_FLAG_REPLAY | the flags that listed it
   int32_t start;   // preambleIdx (fine timing); 0 in chunk mode
   int32_t M, T;    // whole data symbols (demodulateOFDM numSym); symbols demodulated (prefix)
   int32_t coarse;  // Schmidl-Cox index (in the plateau)
@@ -117,6 +118,13 @@ struct DevWork {
   DetRec *det;        // [nframes] detection records
   float *soft;        // exact kernel, AMOD_OPT_SOFT_COMBINE: per-slot soft bit values
   int64_t soft_stride;// floats per slot
+  // detection replay: the exact kernel appends frames listed only for detection-stage
+  // guards (COARSE / FINE / THRESH) to this list once its fp64 detection is done, with
+  // their detection record, and leaves the demodulation to a k_demod launch over the list
+  int32_t *rp_count;  // exact kernel: the list it fills (null: demodulate every frame itself)
+  int32_t *rp_list;
+  const int32_t *dm_count; // k_demod: frames dm_list[0 .. *dm_count) instead of [f0, f1)
+  const int32_t *dm_list;
 };
 
 // AMOD_OPT_SOFT_COMBINE applies to repeated BPSK / QPSK frames

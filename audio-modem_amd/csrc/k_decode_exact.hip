@@ -40,7 +40,8 @@ struct alignas(16) XSmem {
   int ri[XT / 64 + 4];
   uint32_t ru[16];
   double mean, mx, best, phase;
-  int coarse, start, status;
+  float xmn, xmx;
+  int coarse, start, status, nonfin;
 };
 
 __device__ __forceinline__ double or_zero(float v) { return (v != v || v == 0.0f) ? 0.0 : (double)v; } // `x || 0`
@@ -86,6 +87,35 @@ template <typename F> __device__ __forceinline__ void strided8(const float *__re
     for (int u = 0; u < 8; ++u) fn(i + u * XT, v[u]);
   }
   for (; i < N; i += XT) fn(i, p[i]);
+}
+
+// fn(i, p[i]) for every i < N, as aligned float4 loads (a frame starts anywhere): one
+// workgroup streams a whole frame with 8 x 16 B in flight per thread. Each thread sees its
+// samples in no particular order (its callers only take order-free sums and extremes, or
+// write sample i itself).
+template <typename F> __device__ __forceinline__ void stream4(const float *__restrict__ p, int N, F &&fn) {
+  const int ph = (int)((reinterpret_cast<uintptr_t>(p) >> 2) & 3);
+  const float4 *const b = reinterpret_cast<const float4 *>(p - ph);
+  const int nvec = (N + ph + 3) >> 2;
+  auto use = [&](int v, const float4 t) {
+    const int i0 = 4 * v - ph;
+    if (i0 >= 0 && i0 + 3 < N) { fn(i0, t.x); fn(i0 + 1, t.y); fn(i0 + 2, t.z); fn(i0 + 3, t.w); }
+    else {
+      if (i0 >= 0 && i0 < N) fn(i0, t.x);
+      if (i0 + 1 >= 0 && i0 + 1 < N) fn(i0 + 1, t.y);
+      if (i0 + 2 >= 0 && i0 + 2 < N) fn(i0 + 2, t.z);
+      if (i0 + 3 < N) fn(i0 + 3, t.w);
+    }
+  };
+  int v = threadIdx.x;
+  for (; v + 7 * XT < nvec; v += 8 * XT) {
+    float4 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = b[v + u * XT];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) use(v + u * XT, t[u]);
+  }
+  for (; v < nvec; v += XT) use(v, b[v]);
 }
 
 __device__ __forceinline__ double js_max(double a, double b) { // Math.max, NaN-propagating
@@ -187,18 +217,29 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
     // soft combining already has a proven preambleIdx: the replica runs preprocess +
     // demodulation only.
     const bool demod_only = cfg.mode == AMOD_MODE_RECEIVED && w.det && flags0 != 0 &&
-        (flags0 & ~(AMOD_FLAG_DEMAP | AMOD_FLAG_PHASE | AMOD_FLAG_CHANNEL | AMOD_FLAG_SPAN | AMOD_FLAG_SOFT)) == 0;
+        (flags0 & ~(AMOD_FLAG_DEMAP | AMOD_FLAG_PHASE | AMOD_FLAG_CHANNEL | AMOD_FLAG_SPAN | AMOD_FLAG_SOFT |
+                    AMOD_FLAG_REPLAY)) == 0;
+    // A frame listed only for detection-stage guards (and not for soft combining) replays
+    // the detection here and goes back to k_demod (w.rp_count: the caller launches it)
+    const bool replay = w.rp_count && w.det && !D && cfg.mode == AMOD_MODE_RECEIVED && flags0 != 0 &&
+        (flags0 & ~(AMOD_FLAG_COARSE | AMOD_FLAG_FINE | AMOD_FLAG_THRESH)) == 0 &&
+        !soft_combine_applies(w.options, cfg.rep, cfg.mod);
     if (cfg.mode != AMOD_MODE_CHUNK) {
       // ---- preprocessSignal: the mean is a sequential double sum (modem.js:215-217).
       // Every partial sum of floats is a multiple of 2^emin (the smallest sample ulp) and
       // at most sum|x| in magnitude; when sum|x| < 2^(emin + 53) no partial sum rounds, in
       // any order, so the parallel sum is bit-equal to the sequential one. Otherwise (or
       // with non-finite samples) the sum runs sequentially.
+      // (one pass: the parallel sum and its certificate, and the extremes, from which
+      // the peak below follows without a pass of its own)
       double ps = 0.0, pa = 0.0;
       int emin = 1 << 20, nonfin = 0;
-      strided8(xr, N, [&](int, float x) {
+      float xmn = INFINITY, xmx = -INFINITY;
+      stream4(xr, N, [&](int, float x) {
         ps += (double)x;
         pa += fabs((double)x);
+        xmn = fminf(xmn, x);
+        xmx = fmaxf(xmx, x);
         const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
         if (e == 0xFFu) nonfin = 1;
         else if (x != 0.0f) emin = min(emin, e == 0 ? -149 : (int)e - 150);
@@ -208,15 +249,22 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         pa += __shfl_xor(pa, o, 64);
         emin = min(emin, __shfl_xor(emin, o, 64));
         nonfin |= __shfl_xor(nonfin, o, 64);
+        xmn = fminf(xmn, __shfl_xor(xmn, o, 64));
+        xmx = fmaxf(xmx, __shfl_xor(xmx, o, 64));
       }
       if (lane == 0) { sm.rd[wave] = ps; sm.ri[wave] = emin; sm.ri[XT / 64 + wave] = nonfin; }
-      if (lane == 0) sm.er[wave] = pa;
+      if (lane == 0) { sm.er[wave] = pa; sm.rf[wave] = xmn; sm.ei[wave] = (double)xmx; }
       __syncthreads();
       bool exact_par = true;
       if (tid == 0) {
         double S = 0.0, PA = 0.0;
         int EM = 1 << 20, NF = 0;
-        for (int i = 0; i < XT / 64; ++i) { S += sm.rd[i]; PA += sm.er[i]; EM = min(EM, sm.ri[i]); NF |= sm.ri[XT / 64 + i]; }
+        float MN = INFINITY, MX = -INFINITY;
+        for (int i = 0; i < XT / 64; ++i) {
+          S += sm.rd[i]; PA += sm.er[i]; EM = min(EM, sm.ri[i]); NF |= sm.ri[XT / 64 + i];
+          MN = fminf(MN, sm.rf[i]); MX = fmaxf(MX, (float)sm.ei[i]);
+        }
+        sm.xmn = MN; sm.xmx = MX; sm.nonfin = NF;
         // non-finite samples: NaN, or +-Inf, whatever the order (finite sums stay finite)
         exact_par = NF || EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53);
         sm.mean = S / (double)N;
@@ -228,63 +276,38 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       if (!exact_par) {
         // Segments of G samples, certified one by one along the sequential order. A
         // segment whose sum|x| < 2^(em + 53) (em: its smallest sample ulp exponent) has
-        // exact internal sums in any order, so its total and the extremes pmax / pmin of
-        // its sequential prefix sums P_j come out exact from a parallel scan. With S the
-        // running (sequential) sum at its start and q the smaller of em and the exponent
-        // of S's lowest set bit, every partial sum S + P_j is a multiple of 2^q inside
-        // [S + pmin, S + pmax]; below 2^(q + 53) in magnitude none of them rounds and S +
-        // total is the sequential result. A segment failing either test (a sample far
-        // below the running sum's ulp, or a partial sum that could round) is summed
-        // sample by sample.
-        constexpr int SEGCAP = 3 * SCH / 5;
-        double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_hi = sm.sc + 2 * SEGCAP,
-                     *const seg_lo = sm.sc + 3 * SEGCAP, *const seg_e = sm.sc + 4 * SEGCAP;
+        // exact internal sums in any order, so its total comes out exact from one thread's
+        // running sum. With S the running (sequential) sum at its start and q the smaller
+        // of em and the exponent of S's lowest set bit, every partial sum S + P_j is a
+        // multiple of 2^q no larger than |S| + sum|x| in magnitude; below 2^(q + 53) none
+        // of them rounds and S + total is the sequential result. A segment failing either
+        // test (a sample far below the running sum's ulp, or a partial sum that could
+        // round) is summed sample by sample. One thread per segment (the frame is
+        // L2-resident after the pass above): no cross-lane scans.
+        constexpr int SEGCAP = SCH;
+        double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_e = sm.sc + 2 * SEGCAP;
         const int G = 256 * max(1, (N + 256 * SEGCAP - 1) / (256 * SEGCAP));
         const int nseg = (N + G - 1) / G;
-        constexpr int NW = XT / 64;
-        for (int sg0 = wave; sg0 < nseg; sg0 += 4 * NW) {
-          float v[4][4]; // four segments' first 256 samples in flight at once
+        for (int sg = tid; sg < nseg; sg += XT) {
+          const int b0 = sg * G, e1 = min(N, b0 + G);
+          double ss = 0.0, sa = 0.0;
+          int em = 1 << 20;
+          auto add = [&](float x) {
+            ss += (double)x;
+            sa += fabs((double)x);
+            const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
+            if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
+          };
+          int i = b0;
+          for (; i + 8 <= e1; i += 8) {
+            float v[8];
 #pragma unroll
-          for (int g = 0; g < 4; ++g)
+            for (int u = 0; u < 8; ++u) v[u] = xr[i + u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int sg = sg0 + g * NW, i = sg * G + lane + 64 * u;
-              v[g][u] = sg < nseg && i < min(N, (sg + 1) * G) ? xr[i] : 0.f;
-            }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int sg = sg0 + g * NW;
-            if (sg >= nseg) break; // wave-uniform
-            double carry = 0.0, sa = 0.0, pmax = 0.0, pmin = 0.0;
-            int em = 1 << 20;
-            const int e1 = min(N, (sg + 1) * G);
-            for (int r = 0; sg * G + 64 * r < e1; ++r) { // rows of 64 samples, in order
-              const int i = sg * G + 64 * r + lane;
-              const float x = r < 4 ? v[g][r] : (i < e1 ? xr[i] : 0.f);
-              sa += fabs((double)x);
-              const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
-              if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
-              double c = (double)x; // inclusive scan over the row
-#pragma unroll
-              for (int o = 1; o < 64; o <<= 1) {
-                const double t = __shfl_up(c, o, 64);
-                if (lane >= o) c += t;
-              }
-              const double P = carry + c;
-              pmax = fmax(pmax, P);
-              pmin = fmin(pmin, P);
-              carry += __shfl(c, 63, 64);
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-              sa += __shfl_xor(sa, o, 64);
-              pmax = fmax(pmax, __shfl_xor(pmax, o, 64));
-              pmin = fmin(pmin, __shfl_xor(pmin, o, 64));
-              em = min(em, __shfl_xor(em, o, 64));
-            }
-            if (lane == 0) {
-              seg_s[sg] = carry; seg_a[sg] = sa; seg_hi[sg] = pmax; seg_lo[sg] = pmin; seg_e[sg] = (double)em;
-            }
+            for (int u = 0; u < 8; ++u) add(v[u]);
           }
+          for (; i < e1; ++i) add(xr[i]);
+          seg_s[sg] = ss; seg_a[sg] = sa; seg_e[sg] = (double)em;
         }
         __syncthreads();
         if (wave == 0) { // the chain along the segments: wave-uniform S on every lane
@@ -301,8 +324,10 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
               qs = (be ? be : 1) - 1075 + __builtin_ctzll(m);
             }
             const int q = min(em, qs);
-            const bool inner = seg_a[sg] * (1.0 + 0x1p-40) < ldexp(1.0, em + 53);
-            const double reach = fmax(fabs(S + seg_hi[sg]), fabs(S + seg_lo[sg])) * (1.0 + 0x1p-50);
+            // (sum|x| in fp64 over G terms: relative error below G 2^-53)
+            const double slack = 1.0 + ldexp((double)G, -52);
+            const bool inner = seg_a[sg] * slack < ldexp(1.0, em + 53);
+            const double reach = (fabs(S) + seg_a[sg]) * slack;
             if (inner && reach < ldexp(1.0, q + 53)) {
               S += seg_s[sg];
             } else { // sample by sample: 64 coalesced loads, then lane by lane in order
@@ -320,24 +345,38 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       __syncthreads();
       const double mean = sm.mean;
       double mx = 0.0;
-      strided8(xr, N, [&](int i, float x) {
-        const float o = (float)((double)x - mean);
-        xs[i] = o;
-        mx = js_max(mx, fabs((double)o));
-      });
-      for (int o = 32; o > 0; o >>= 1) mx = js_max(mx, __shfl_xor(mx, o, 64));
-      if (lane == 0) sm.rd[wave] = mx;
-      __syncthreads();
-      if (tid == 0) {
-        double m = 0.0;
-        for (int i = 0; i < XT / 64; ++i) m = js_max(m, sm.rd[i]);
-        sm.mx = m;
-        if (D) { D->mean = mean; D->mx = m; }
-      }
-      __syncthreads();
-      mx = sm.mx;
-      if (mx > 1e-6) {
-        strided8(xs, N, [&](int i, float o) { xs[i] = (float)((double)o / mx); }); // own indices only
+      if (!sm.nonfin) {
+        // finite samples: max |f32(x - mean)| is reached at an extreme (fl64(x - mean) and
+        // the f32 rounding are monotone in x), so the peak is known before the one pass
+        // that writes the normalised samples
+        if (tid == 0) {
+          const double m = N == 0 ? 0.0 : js_max(js_max(0.0, fabs((double)(float)((double)sm.xmx - mean))),
+                                                 fabs((double)(float)((double)sm.xmn - mean)));
+          sm.mx = m;
+          if (D) { D->mean = mean; D->mx = m; }
+        }
+        __syncthreads();
+        mx = sm.mx;
+        if (mx > 1e-6) stream4(xr, N, [&](int i, float x) { xs[i] = (float)((double)(float)((double)x - mean) / mx); });
+        else stream4(xr, N, [&](int i, float x) { xs[i] = (float)((double)x - mean); });
+      } else { // NaN / Inf: Math.max's NaN propagation over every sample, then the division
+        stream4(xr, N, [&](int i, float x) {
+          const float o = (float)((double)x - mean);
+          xs[i] = o;
+          mx = js_max(mx, fabs((double)o));
+        });
+        for (int o = 32; o > 0; o >>= 1) mx = js_max(mx, __shfl_xor(mx, o, 64));
+        if (lane == 0) sm.rd[wave] = mx;
+        __syncthreads();
+        if (tid == 0) {
+          double m = 0.0;
+          for (int i = 0; i < XT / 64; ++i) m = js_max(m, sm.rd[i]);
+          sm.mx = m;
+          if (D) { D->mean = mean; D->mx = m; }
+        }
+        wg_global_sync(); // (the pass below reads samples other threads wrote)
+        mx = sm.mx;
+        if (mx > 1e-6) stream4(xs, N, [&](int i, float o) { xs[i] = (float)((double)o / mx); }); // own indices only
       }
       wg_global_sync();
       sig = xs;
@@ -350,6 +389,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       if (demod_only) {
         // the fast path's detection record: preambleIdx proven by its guards
         const DetRec dr = w.det[f];
+        r.flags |= dr.flags; // a replayed detection's flags (0 for k_detect's records)
         r.coarse_idx = dr.coarse;
         r.fine_metric = dr.fbest;
         r.preamble_idx = start = dr.start;
@@ -525,6 +565,25 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         r.status = status;
         if (!loop) r.preamble_idx = -1;
         w.res[f] = r;
+      }
+      __syncthreads();
+      continue;
+    }
+    if (replay) {
+      // detection replay: preambleIdx (and the coarse index and fine metric the result
+      // reports) now equal the reference's; the demodulation is k_demod's, under its own
+      // guards (a frame they list comes back here, demodulation only). The record carries
+      // the normalisation of the replica's exact mean and peak, as k_detect's does.
+      if (tid == 0) {
+        const double mean = sm.mean, mx = sm.mx;
+        DetRec d;
+        d.route = ROUTE_REPLAY; d.flags = flags0 | AMOD_FLAG_REPLAY; d.start = start;
+        d.M = (N - (start + 3 * SYM)) / SYM; d.T = min(d.M, w.mcap); d.coarse = r.coarse_idx;
+        if (mx > 1e-6) { d.A = (float)(1.0 / mx); d.B = (float)(-mean / mx); }
+        else { d.A = 1.f; d.B = (float)(-mean); }
+        d.fbest = r.fine_metric; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
+        w.det[f] = d;
+        w.rp_list[atomicAdd(w.rp_count, 1)] = f;
       }
       __syncthreads();
       continue;

@@ -1362,7 +1362,9 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   const int ndata = cfg.ndata, per_sym = ndata * BPS, origin_idx = cfg.origin_idx;
   const bool chunk_mode = cfg.mode == AMOD_MODE_CHUNK;
   const float guard = cfg.guard;
-  const int nfr = w.f1 - w.f0; // frames [f0, f1) of this launch
+  // frames [f0, f1) of this launch, or the list of frames whose detection the exact
+  // kernel replayed
+  const int nfr = w.dm_list ? __builtin_amdgcn_readfirstlane(*w.dm_count) : w.f1 - w.f0;
   // the wave's bit stream (and voted stream) in dynamic LDS
   uint32_t *const bits = LDS_U + wave * w.stream_words;
   uint32_t *const voted = bits + w.vote_off;
@@ -1398,9 +1400,9 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   auto next_frame = [&](int k, FrameS &F) -> int {
     FRESH_ARGS;
     for (; k < nfr; k += wstride) {
-      const int f = w.f1 - 1 - k;
+      const int f = w.dm_list ? __builtin_amdgcn_readfirstlane(w.dm_list[k]) : w.f1 - 1 - k;
       const DetRec d = sload(w.det + f);
-      if (d.route != ROUTE_DEMOD) continue;
+      if (d.route != (w.dm_list ? ROUTE_REPLAY : ROUTE_DEMOD)) continue; // (the list launch: replayed frames)
       F.f = f; F.T = d.T; F.M = d.M; F.start = d.start;
       F.A = d.A; F.B = d.B;
       F.X = w.samples + sload(w.off + f);
@@ -1628,9 +1630,23 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       }
       // a constant FFT window has an all-zero spectrum in the reference: every data
       // subcarrier takes the origin decision (ties resolve to the first point).
-      // Each decision is OR-ed straight into the frame's MSB-first stream (LDS atomic OR;
-      // BPS divides 32, so a decision never straddles a word): its bits are placed at the
-      // top of a word and shifted right by the stream position (v_lshrrev takes it mod 32)
+      // The job's decisions (symbols s1, s2: a contiguous run [gs, ge) of the frame's
+      // decision sequence) go to the exchange buffer, free again once the band is in
+      // registers: one dword per decision (conflict-free ds_write_b32, consecutive data
+      // indices on consecutive lanes), its bits already at their place in the stream word
+      // (BPS divides 32, so a decision never straddles a word; v_lshrrev takes the
+      // position mod 32). Word wfirst + i of the stream is then the OR of dwords
+      // [DPW i, DPW i + DPW), one lane per word, one ds_or into the stream (the first
+      // word's top bits belong to the previous job).
+      constexpr int DPW = 32 / BPS; // decisions per stream word
+      uint32_t *const dec = reinterpret_cast<uint32_t *>(X2);
+      const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
+      const int wfirst = gs / DPW, g0 = wfirst * DPW, gend = (ge + DPW - 1) / DPW * DPW;
+      asm volatile("" ::: "memory"); // (the band reads above are float2 accesses of the same LDS)
+      if (ln < DPW) { // the first and last words' dwords outside [gs, ge)
+        if (g0 + ln < gs) dec[ln] = 0u;
+        if (ge + ln < gend) dec[ge - g0 + ln] = 0u;
+      }
       const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
       int dflag1 = 0, dflag2 = 0;
 #pragma unroll
@@ -1658,10 +1674,23 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           db = live ? db : org_bits;
           unc_any |= dib >= 0 && live && margin <= tau;
           const int pos = sbase + dib;
-          if (dib >= 0) atomicOr(bits + (pos >> 5), db >> (pos & 31));
+          if (dib >= 0) dec[pos / BPS - g0] = db >> (pos & 31);
         }
         if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
       }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      for (int i = ln; i < (gend - g0) / DPW; i += 64) {
+        const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
+        uint32_t word = 0u;
+#pragma unroll
+        for (int k = 0; k < DPW / 4; ++k) {
+          const uint4 t = q[k];
+          word |= (t.x | t.y) | (t.z | t.w);
+        }
+        atomicOr(bits + wfirst + i, word);
+      }
+      asm volatile("" ::: "memory"); // (the next FFT rewrites the buffer)
       {
         const bool d1u = __ballot(dflag1) != 0, d2u = __ballot(dflag2) != 0;
         if (s1 >= 0 && (d1u || ph_unc1)) {
@@ -1732,6 +1761,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           if (cfg.mode == AMOD_MODE_RECEIVED) {
             const DetRec dr = sload(w.det + f);
             r.fine_metric = dr.fbest; r.coarse_idx = dr.coarse; r.preamble_idx = cur.start;
+            r.flags = dr.flags; // AMOD_FLAG_REPLAY (+ why) for a replayed detection, else 0
           }
           const int nbytes = (nbits / rep) >> 3;
           const int crc_len = parse_stream(v, nbytes, cfg.mode, r); // every lane: the same bytes

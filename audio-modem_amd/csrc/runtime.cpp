@@ -434,13 +434,13 @@ int ensure_chain(amod_ctx *ctx, int32_t nframes) {
 
 int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
   if (max_len < 0) { // device path: keep what amod_reserve set up, or size from a default
-    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 4 * (size_t)std::max(nframes, 1))));
+    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 5 * (size_t)std::max(nframes, 1))));
     if (ctx->nslots > 0) return AMOD_SUCCESS;
     max_len = 65536;
   }
   const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
       std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
-  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 4 * (size_t)std::max(nframes, 1))));
+  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 5 * (size_t)std::max(nframes, 1))));
   // grow-only: a later, smaller reservation never shrinks a stride or the slot count that
   // earlier (longer) frames were sized for
   const int64_t words = (max_bits_for(c, max_len) + 31) / 32;
@@ -481,7 +481,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.samples = samples; w.off = offsets; w.len = lengths; w.nframes = nframes;
   w.res = results; w.payload = payload; w.stride = payload_stride; w.dbg = debug;
   int32_t *fb = (int32_t *)ctx->fb.p;
-  // two exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod
+  // exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod;
+  // list C (fb[2]): frames whose detection the exact kernel replayed, for k_demod
   w.fb_count = fb; w.fb_list = fb + 64; w.fb_flags = fb + 64 + nframes;
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
@@ -553,6 +554,23 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // exact-kernel grid: persistent workgroups over the listed frames (usually none: the
   // launch then costs its dispatch, so two per CU, not one per slot)
   const int xslots = std::min({ctx->nslots, nframes, 2 * std::max(1, ctx->cu_count)});
+  // list A's exact kernel, then (detection replay) k_demod over the frames it only
+  // detected: a frame listed for COARSE / FINE / THRESH alone gets its preambleIdx from
+  // the fp64 replica and its symbols from the fast path (AMOD_NO_REPLAY: diagnostics)
+  const bool replay = demod && !debug && mode == AMOD_MODE_RECEIVED && !getenv("AMOD_NO_REPLAY");
+  auto exact_a = [&](hipStream_t st) -> int {
+    amod::DevWork wa = w;
+    wa.f0 = 0; wa.f1 = nframes;
+    if (replay) { wa.rp_count = fb + 2; wa.rp_list = fb + 64 + 4 * nframes; }
+    HIP_TRY(amod_launch_exact(d, wa, xslots, st));
+    if (replay) {
+      amod::DevWork wc = wb; // its guards list into B
+      wc.f0 = 0; wc.f1 = nframes;
+      wc.dm_count = fb + 2; wc.dm_list = fb + 64 + 4 * nframes;
+      HIP_TRY(amod_launch_demod(d, wc, std::min(demod_blocks(nframes), std::max(1, ctx->cu_count)), st));
+    }
+    return AMOD_SUCCESS;
+  };
   HIP_TRY(mark(0));
   if (nchunk == 1) {
     w.f0 = 0; w.f1 = nframes;
@@ -565,11 +583,13 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       if (getenv("AMOD_EXACT_SERIAL")) {
         wb.f0 = 0; wb.f1 = nframes;
         HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
-        HIP_TRY(amod_launch_exact(d, w, xslots, s));
+        rc = exact_a(s);
+        if (rc) return rc;
       } else {
       HIP_TRY(hipEventRecord(ctx->chunk_ev[0], s));
       HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[0], 0));
-      HIP_TRY(amod_launch_exact(d, w, xslots, ctx->aux));
+      rc = exact_a(ctx->aux);
+      if (rc) return rc;
       HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
       wb.f0 = 0; wb.f1 = nframes;
       HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
@@ -590,7 +610,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     HIP_TRY(mark(1)); // every k_detect done (on s)
     HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
     HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0));
-    HIP_TRY(amod_launch_exact(d, w, xslots, s));
+    rc = exact_a(s);
+    if (rc) return rc;
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(2));

@@ -178,7 +178,7 @@ def main():
         st = np.zeros(F * 32, dtype=np.uint64)
         n = L.load().amod_debug_stamps(dm.ctx, st.ctypes.data, st.size)
         st = st[:n].reshape(-1, 32).astype(np.int64)
-        for i in np.nonzero(rec["flags"] & L.FLAG_EXACT)[0][:32]:
+        for i in np.nonzero(rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY))[0][:32]:
             print("listed", i, hex(int(rec["flags"][i])), int(rec["coarse_idx"][i]),
                   [int(st[i, b] - st[i, a]) if st[i, a] and st[i, b] else None
                    for a, b in ((8, 9), (9, 10), (10, 11), (11, 12))], file=sys.stderr)
@@ -333,7 +333,7 @@ def main():
 
 
 FLAG_NAMES = {0: "FORCED", 1: "NONFINITE", 2: "BIG", 3: "COARSE", 4: "FINE", 5: "CHANNEL", 6: "PHASE", 7: "DEMAP",
-              8: "THRESH", 9: "SPAN", 10: "SOFT"}
+              8: "THRESH", 9: "SPAN", 10: "SOFT", 11: "REPLAY"}
 PAYLOAD_C5 = 256
 
 

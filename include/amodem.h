@@ -91,6 +91,9 @@ extern "C" {
                                         path demodulated (signal energy ended early)   */
 #define AMOD_FLAG_SOFT (1 << 10)     /* AMOD_OPT_SOFT_COMBINE: demodulated by the exact
                                         kernel after the fast path's detection         */
+#define AMOD_FLAG_REPLAY (1 << 11)   /* preambleIdx from the exact replica's detection
+                                        (COARSE / FINE / THRESH), symbols demodulated
+                                        by the fast path under its guards              */
 #define AMOD_FLAG_EXACT (1 << 15)    /* result produced by the exact-replica kernel */
 
 /* OFDM parameters + modulation; mirrors OFDM (modem.js:69-98) */

@@ -51,9 +51,10 @@ def _check_against_oracle(cfg_name, mod, rep, x, offs, lens, rec, pay):
         ref = ref_dict(struct_to_dict(r), rp.tobytes(), via_legacy=True)
         got = as_golden(amodem.to_reference(rec[i], pay[i].tobytes(), via_legacy=True))
         assert got == ref, (i, fl)
-        if fl & L.FLAG_EXACT and fl & ~(L.FLAG_EXACT | DEMOD_FLAGS):
+        if fl & (L.FLAG_EXACT | L.FLAG_REPLAY) and fl & ~(L.FLAG_EXACT | L.FLAG_REPLAY | DEMOD_FLAGS):
             # the replica's own Schmidl-Cox argmax and fine metric (demodulation-only
-            # frames keep the fast path's plateau index, pinned in test_gpu_parity)
+            # frames keep the fast path's plateau index, pinned in test_gpu_parity); a
+            # replayed detection (REPLAY: demodulated by k_demod) reports the replica's too
             assert int(rec["coarse_idx"][i]) == r.coarse_idx, (i, fl)
             if r.coarse_idx >= 0:
                 assert float(rec["fine_metric"][i]) == float(np.float32(r.fine_metric)), (i, fl)
@@ -69,17 +70,33 @@ def test_forced_exact_matches_oracle_under_noise(snr_db, tiny):
     _check_against_oracle("acoustic", "BPSK", 3, x, offs, lens, rec, pay)
 
 
+def _wide_guard_demodulator(cfg, x, offs, lens):
+    """A context whose guard bands for cfg are 50x the default (AMOD_GUARD_SCALE, read
+    when the context builds cfg's tables at its first decode): at these SNRs ambiguous
+    coarse / fine decisions, and so the listed paths, become common instead of a few per
+    10^4 frames."""
+    import os
+    dm = amodem.Demodulator(0)
+    os.environ["AMOD_GUARD_SCALE"] = "50"
+    try:
+        dm.decode_batch(x, offs[:1], lens[:1], cfg=cfg)
+    finally:
+        del os.environ["AMOD_GUARD_SCALE"]
+    return dm
+
+
 @pytest.mark.parametrize("preset,snr_db", [("acoustic", 6), ("standard", 7)])
 def test_listed_coarse_frames_match_oracle(preset, snr_db):
     """Frames the fast path lists for an ambiguous coarse decision run the replica's
     recurrence only up to the proven hull: the argmax still equals the oracle's."""
     cfg, x, offs, lens = _noisy_batch(preset, "BPSK", 3, 48, 64, snr_db, seed=3)
-    dm = amodem.Demodulator(0)
+    dm = _wide_guard_demodulator(cfg, x, offs, lens)
     rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
     full, fpay = dm.decode_batch(x, offs, lens, cfg=cfg, options=L.OPT_FORCE_EXACT)
     dm.close()
     coarse_listed = (rec["flags"] & (1 << 3)) != 0  # AMOD_FLAG_COARSE
-    listed = (rec["flags"] & L.FLAG_EXACT) != 0
+    listed = (rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY)) != 0
+    assert (coarse_listed & listed).sum() > 0, np.unique(rec["flags"])  # the listed path is exercised
     for i in np.nonzero(coarse_listed & listed)[0]:
         assert int(rec["coarse_idx"][i]) == int(full["coarse_idx"][i]), i
         assert float(rec["fine_metric"][i]) == float(full["fine_metric"][i]), i
@@ -114,3 +131,32 @@ def test_exact_mean_is_the_sequential_sum():
     _, mean, _ = O.preprocess(fr)
     assert mean == seq
     assert d.mean == seq
+
+
+@pytest.mark.parametrize("preset,snr_db", [("acoustic", 8), ("acoustic", 9), ("standard", 7)])
+def test_replayed_detection_equals_full_exact_path(preset, snr_db):
+    """Detection replay: a frame listed only for detection-stage guards gets its
+    detection from the fp64 replica and its symbols from k_demod (AMOD_FLAG_REPLAY);
+    every result field and payload byte equals the whole-frame replica's
+    (AMOD_NO_REPLAY) and the oracle's."""
+    import os
+    cfg, x, offs, lens = _noisy_batch(preset, "BPSK", 3, 48, 64, snr_db, seed=11)
+    dm = _wide_guard_demodulator(cfg, x, offs, lens)
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    os.environ["AMOD_NO_REPLAY"] = "1"
+    try:
+        ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    finally:
+        del os.environ["AMOD_NO_REPLAY"]
+    dm.close()
+    replayed = (rec["flags"] & L.FLAG_REPLAY) != 0
+    if preset == "acoustic":  # (standard at 7 dB: ambiguous coarse decisions end in detection errors)
+        assert replayed.sum() > 0, np.unique(rec["flags"])
+    assert not (ref["flags"] & L.FLAG_REPLAY).any()
+    for n in ("status", "preamble_idx", "coarse_idx", "fine_metric", "frame_type", "nbytes", "data_len",
+              "expected_crc", "actual_crc", "crc_valid"):
+        assert (rec[n] == ref[n]).all(), n
+    for i in range(len(offs)):
+        pv = int(rec["payload_valid"][i])
+        assert pay[i][:pv].tobytes() == rpay[i][:pv].tobytes(), i
+    _check_against_oracle(preset, "BPSK", 3, x, offs, lens, rec, pay)
