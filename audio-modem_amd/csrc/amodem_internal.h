@@ -125,6 +125,11 @@ struct DevWork {
   int32_t *rp_list;
   const int32_t *dm_count; // k_demod: frames dm_list[0 .. *dm_count) instead of [f0, f1)
   const int32_t *dm_list;
+  // k_demod beside a running exact kernel: when *yield_count > 0 (detection listed
+  // frames) only the first yield_blocks workgroups run, so every CU keeps room for the
+  // exact kernel's waves (0: the whole grid)
+  const int32_t *yield_count;
+  int32_t yield_blocks;
 };
 
 // AMOD_OPT_SOFT_COMBINE applies to repeated BPSK / QPSK frames

@@ -90,7 +90,7 @@ template <typename F> __device__ __forceinline__ void strided8(const float *__re
 }
 
 // fn(i, p[i]) for every i < N, as aligned float4 loads (a frame starts anywhere): one
-// workgroup streams a whole frame with 8 x 16 B in flight per thread. Each thread sees its
+// workgroup streams a whole frame with 4 x 16 B in flight per thread. Each thread sees its
 // samples in no particular order (its callers only take order-free sums and extremes, or
 // write sample i itself).
 template <typename F> __device__ __forceinline__ void stream4(const float *__restrict__ p, int N, F &&fn) {
@@ -108,12 +108,12 @@ template <typename F> __device__ __forceinline__ void stream4(const float *__res
     }
   };
   int v = threadIdx.x;
-  for (; v + 7 * XT < nvec; v += 8 * XT) {
-    float4 t[8];
+  for (; v + 3 * XT < nvec; v += 4 * XT) {
+    float4 t[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) t[u] = b[v + u * XT];
+    for (int u = 0; u < 4; ++u) t[u] = b[v + u * XT];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) use(v + u * XT, t[u]);
+    for (int u = 0; u < 4; ++u) use(v + u * XT, t[u]);
   }
   for (; v < nvec; v += XT) use(v, b[v]);
 }
@@ -179,7 +179,7 @@ __device__ int crosscorr_detect(const float *xs, int N, const DevCfg &cfg, XSmem
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-__global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const DevWork w) {
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_decode_exact(const DevCfg cfg, const DevWork w) {
   __shared__ XSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // listed frames are latency-bound chains (sequential recurrences) that run beside the
@@ -273,6 +273,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
       __syncthreads();
       exact_par = sm.status != 0;
       __syncthreads();
+      XSTAMP(13);
       if (!exact_par) {
         // Segments of G samples, certified one by one along the sequential order. A
         // segment whose sum|x| < 2^(em + 53) (em: its smallest sample ulp exponent) has
@@ -343,6 +344,7 @@ __global__ __launch_bounds__(XT) void k_decode_exact(const DevCfg cfg, const Dev
         }
       }
       __syncthreads();
+      XSTAMP(14);
       const double mean = sm.mean;
       double mx = 0.0;
       if (!sm.nonfin) {

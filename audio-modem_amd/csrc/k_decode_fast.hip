@@ -1396,7 +1396,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // A static stride: the dispatcher places the grid's workgroups round-robin over the CUs,
   // so every SIMD gets within one frame of the mean (a claim counter measured slower: its
   // atomics' returns hold up the in-order vmcnt waits of the sample loads)
-  const int wstride = (int)gridDim.x * NWAVE;
+  int nblk = (int)gridDim.x;
+  if (w.yield_blocks > 0 && w.yield_blocks < nblk && __builtin_amdgcn_readfirstlane(*w.yield_count) > 0)
+    nblk = w.yield_blocks;
+  if ((int)blockIdx.x >= nblk) return; // (before any frame: the grid's frames are strided over nblk)
+  const int wstride = nblk * NWAVE;
   auto next_frame = [&](int k, FrameS &F) -> int {
     FRESH_ARGS;
     for (; k < nfr; k += wstride) {

@@ -592,7 +592,17 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       if (rc) return rc;
       HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
       wb.f0 = 0; wb.f1 = nframes;
-      HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
+      {
+        // the exact kernel needs a wave slot and its registers on every SIMD it runs on:
+        // with frames listed, k_demod leaves one workgroup per CU free
+        amod::DevWork wm = wb;
+        const int nb = demod_blocks(nframes);
+        if (per_cu >= 2 && nb >= (int)(ctx->cu_count * per_cu)) {
+          wm.yield_count = fb;
+          wm.yield_blocks = (int)(ctx->cu_count * (per_cu - 1));
+        }
+        HIP_TRY(amod_launch_demod(d, wm, nb, s));
+      }
       HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0)); // workspace slots are shared
       }
     } else {

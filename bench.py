@@ -181,7 +181,7 @@ def main():
         for i in np.nonzero(rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY))[0][:32]:
             print("listed", i, hex(int(rec["flags"][i])), int(rec["coarse_idx"][i]),
                   [int(st[i, b] - st[i, a]) if st[i, a] and st[i, b] else None
-                   for a, b in ((8, 9), (9, 10), (10, 11), (11, 12))], file=sys.stderr)
+                   for a, b in ((8, 13), (13, 14), (14, 9), (9, 10), (10, 11), (11, 12))], file=sys.stderr)
     pay = d_pay.view(F, stride).cpu().numpy()
     for i in range(0, F, max(1, F // 16)):
         r = amodem.to_reference(rec[i], pay[i].tobytes(), not C4)
