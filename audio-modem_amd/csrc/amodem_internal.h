@@ -132,6 +132,16 @@ struct DevWork {
   int32_t yield_blocks;
 };
 
+// k_gap_scan -> streaming receiver: the scan that follows the frame of fine range r, run
+// from its speculated start (s0, block b1) to its detection (status 1)
+struct GapScan {
+  int64_t s0, b1;              // start: ac_pos = s0 (sums not initialised), IDLE in block b1
+  int64_t det_block, pre_pos;  // the block whose scan call detected, the coarse position
+  int64_t ac_pos, scanned;     // the scan position after it; positions stepped
+  double p, ra, rb;            // the running sums after it
+  int32_t status, pad;
+};
+
 // AMOD_OPT_SOFT_COMBINE applies to repeated BPSK / QPSK frames
 __host__ __device__ inline bool soft_combine_applies(uint32_t options, int rep, int mod) {
   return (options & AMOD_OPT_SOFT_COMBINE) && rep > 1 && (mod == AMOD_BPSK || mod == AMOD_QPSK);
@@ -466,7 +476,10 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
 hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
-                            int64_t maxcount, double *out, hipStream_t s);
+                            int64_t maxcount, double *out, double2 *barg, hipStream_t s);
+hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int64_t *first, const double2 *barg,
+                                int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks, int max_blocks,
+                                amod::GapScan *out, hipStream_t s);
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,
                               int nwin, float *out, hipStream_t s);
 hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s);

@@ -260,24 +260,174 @@ __global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ z
 
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
 // base[r] + j; one lane per position
+// barg (optional): per workgroup, the first maximum of its positions' metrics (NaN
+// skipped, as the refinement's `metric > best`) as (metric, j), at [r * gridDim.x + bx]
 __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const float *__restrict__ pre1,
                                               int sym, double pre1_energy, const int64_t *__restrict__ first,
                                               const int64_t *__restrict__ base, const int64_t *__restrict__ count,
-                                              int nranges, double *__restrict__ out) {
+                                              int nranges, double *__restrict__ out, double2 *__restrict__ barg) {
+  __shared__ double2 red[4];
   const int r = blockIdx.y;
   if (r >= nranges) return;
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= count[r]) return;
-  const int64_t d = first[r] + j;
-  double corr = 0.0, se = 0.0;
-  for (int i = 0; i < sym; ++i) {
-    const double s = sample_at(y, n, d + i);
-    corr += s * (double)pre1[i];
-    se += s * s;
+  double m = -__builtin_inf();
+  if (j < count[r]) {
+    const int64_t d = first[r] + j;
+    double corr = 0.0, se = 0.0;
+    for (int i = 0; i < sym; ++i) {
+      const double s = sample_at(y, n, d + i);
+      corr += s * (double)pre1[i];
+      se += s * s;
+    }
+    // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
+    const double denom = sqrt(se * pre1_energy);
+    const double v = denom > 0.001 ? corr / denom : __builtin_nan("");
+    out[base[r] + j] = v;
+    if (v == v) m = v;
   }
-  // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
-  const double denom = sqrt(se * pre1_energy);
-  out[base[r] + j] = denom > 0.001 ? corr / denom : __builtin_nan("");
+  if (!barg) return;
+  double bj = (double)j;
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(m, o, 64), oj = __shfl_xor(bj, o, 64);
+    if (om > m || (om == m && oj < bj)) { m = om; bj = oj; }
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_double2(m, bj);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double2 b = red[0];
+    for (int k = 1; k < 4; ++k)
+      if (red[k].x > b.x || (red[k].x == b.x && red[k].y < b.y)) b = red[k];
+    barg[(int64_t)r * gridDim.x + blockIdx.x] = b;
+  }
+}
+
+// Speculative gap scans (the streaming receiver's _scanForPreamble, app.js:775-847, as
+// Receiver::scan in stream.cpp replays it). For fine range r: its first fine-metric
+// maximum d is where the refinement would put the frame, so the receiver would reset to
+// IDLE with its scan at s0 = d + F (ac sums not initialised) in block ceil(s0 / 4096).
+// From that state the scan is a function of the stream alone: one wave per range runs it
+// block by block with the host's arithmetic in the host's order (IEEE double, no
+// contraction: this file is built with -ffp-contract=off) until a detection, and
+// records the state the host would be in. The host adopts a record only when its true
+// state matches the start exactly; anything else (no detection within the block limit,
+// the ring's oldest sample overtaken) is left to the host (status 0).
+// Positions go in tiles of 64: lane j forms position j's increments (coalesced loads),
+// the three running sums then advance through them in order (uniform, read lane by
+// lane), lane j keeps the sums at its position, and a tile in which no lane passes the
+// metric pre-check (no detection pending) is done; otherwise its positions from the first
+// such lane are stepped one by one from the kept sums.
+__device__ __forceinline__ double rl_d(double v, int j) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), j), hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+  return __hiloint2double(hi, lo);
+}
+__global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, int64_t n, int64_t lo,
+                                                 const int64_t *__restrict__ first, const double2 *__restrict__ barg,
+                                                 int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks,
+                                                 int max_blocks, GapScan *__restrict__ out) {
+  const int r = blockIdx.x, lane = threadIdx.x;
+  if (r >= nranges) return;
+  GapScan g{};
+  double2 b = barg[(int64_t)r * nbx];
+  for (int k = 1; k < nbx; ++k) {
+    const double2 v = barg[(int64_t)r * nbx + k];
+    if (v.x > b.x) b = v; // (blocks in position order: ties keep the first)
+  }
+  auto emit = [&]() { if (lane == 0) out[r] = g; };
+  if (!(b.x >= 0.1)) { emit(); return; } // the refinement fails there: no frame
+  const int64_t s0 = lo + first[r] + (int64_t)b.y + F; // global stream position
+  constexpr int64_t kBlk = 4096, half = 256;
+  const int64_t b1 = (s0 + kBlk - 1) / kBlk;
+  g.s0 = s0; g.b1 = b1;
+  auto S = [&](int64_t i) -> double { return (double)sample_at(y, n, i - lo); };
+  int64_t pos = s0, scanned = 0;
+  double p = 0.0, ra = 0.0, rb = 0.0; // uniform
+  bool init = false;
+  const double min_e = 0.001;
+  for (int64_t blk = b1; blk < min(nblocks, b1 + max_blocks); ++blk) {
+    const int64_t total = (blk + 1) * kBlk, oldest = total - cap;
+    if (pos < oldest + 2 * half) break; // the host re-positions the scan: its own business
+    const int64_t scan_end = total - 2 * half;
+    if (pos > scan_end) continue;
+    if (!init) { // the window sums, in order (products on the lanes, sums read lane by lane)
+      for (int m0 = 0; m0 < (int)half; m0 += 64) {
+        const double a = S(pos + m0 + lane), c = S(pos + m0 + lane + half);
+        const double ab = a * c, aa = a * a, cc = c * c;
+        for (int j = 0; j < 64; ++j) { p += rl_d(ab, j); ra += rl_d(aa, j); rb += rl_d(cc, j); }
+      }
+      init = true;
+    }
+    double best = 0.0;
+    int64_t best_pos = -1;
+    while (pos <= scan_end) {
+      const int T = (int)min<int64_t>(64, scan_end - pos + 1);
+      // increments of positions pos + j < scan_end (the one at scan_end takes none)
+      const int64_t x = pos + lane;
+      const bool upd = lane < T && x < scan_end;
+      double ip = 0.0, ia = 0.0, ib = 0.0;
+      if (upd) {
+        const double a_out = S(x), mid = S(x + half), b_in = S(x + 2 * half);
+        ip = mid * b_in - a_out * mid;
+        ia = mid * mid - a_out * a_out;
+        ib = b_in * b_in - mid * mid;
+      }
+      const unsigned long long um = __ballot(upd);
+      double sp = p, sa = ra, sb = rb; // lane j: the sums at position pos + j
+      for (int j = 0; j < T; ++j) {
+        if (lane == j) { sp = p; sa = ra; sb = rb; }
+        if ((um >> j) & 1) { p += rl_d(ip, j); ra += rl_d(ia, j); rb += rl_d(ib, j); }
+      }
+      // (p, ra, rb): the sums after the tile
+      const bool pending = best > 0.5 && best_pos >= 0;
+      const bool c = lane < T && sa > min_e && sb > min_e && sp * sp >= 0.49 * (sa * sb);
+      const unsigned long long hits = __ballot(c);
+      if (!pending && !hits) { pos += T; scanned += T; continue; }
+      // the tile's positions in parallel: lane j's metric from its kept sums (gated as the
+      // loop gates it), the running best as an inclusive prefix maximum (a later equal
+      // metric never replaces the earlier: strict '>'), and the 0.7 drop tested on the
+      // sums after position j (lane j + 1's, or the tile's end)
+      const double pn = __shfl_down(sp, 1, 64), ran = __shfl_down(sa, 1, 64), rbn = __shfl_down(sb, 1, 64);
+      const double pa = lane + 1 < T ? pn : p, raa = lane + 1 < T ? ran : ra, rba = lane + 1 < T ? rbn : rb;
+      double key = -__builtin_inf();
+      int kidx = 64;
+      if (c) {
+        const double metric = (sp * sp) / (sa * sb);
+        if (metric > 0.5) { key = metric; kidx = lane; }
+      }
+      for (int o = 1; o < 64; o <<= 1) {
+        const double ok = __shfl_up(key, o, 64);
+        const int oi = __shfl_up(kidx, o, 64);
+        if (lane >= o && (ok > key || (ok == key && oi < kidx))) { key = ok; kidx = oi; }
+      }
+      double bj = best;
+      int64_t bpj = best_pos;
+      if (key > bj) { bj = key; bpj = pos + kidx; }
+      bool det = false;
+      if (lane < T && bj > 0.5 && bpj >= 0 && raa > min_e && rba > min_e) det = (pa * pa) / (raa * rba) < bj * 0.7;
+      const unsigned long long dm = __ballot(det);
+      if (dm) {
+        const int j = __builtin_ctzll(dm);
+        g.status = 1; g.det_block = blk;
+        g.pre_pos = ((int64_t)__builtin_amdgcn_readlane((int)(bpj >> 32), j) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpj, j);
+        g.ac_pos = pos + j + 1;
+        g.p = rl_d(pa, j); g.ra = rl_d(raa, j); g.rb = rl_d(rba, j);
+        g.scanned = scanned + j + 1;
+        emit();
+        return;
+      }
+      best = rl_d(bj, T - 1);
+      best_pos = ((int64_t)__builtin_amdgcn_readlane((int)(bpj >> 32), T - 1) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpj, T - 1);
+      pos += T; scanned += T;
+    }
+    if (best > 0.5 && best_pos >= 0) { // end-of-block commit
+      g.status = 1; g.det_block = blk; g.pre_pos = best_pos; g.ac_pos = pos; g.p = p; g.ra = ra; g.rb = rb;
+      g.scanned = scanned;
+      emit();
+      return;
+    }
+  }
+  emit(); // status 0
 }
 
 // the host's sparse copy of the cleaned stream: compact granule j (1024 samples) is stream
@@ -341,10 +491,18 @@ hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double
 }
 hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
-                            int64_t maxcount, double *out, hipStream_t s) {
+                            int64_t maxcount, double *out, double2 *barg, hipStream_t s) {
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
   hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
-                     pre1_energy, first, base, count, nranges, out);
+                     pre1_energy, first, base, count, nranges, out, barg);
+  return hipGetLastError();
+}
+hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int64_t *first, const double2 *barg,
+                                int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks, int max_blocks,
+                                amod::GapScan *out, hipStream_t s) {
+  if (nranges <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amod::k_gap_scan, dim3((unsigned)nranges), dim3(64), 0, s, y, n, lo, first, barg,
+                     nbx, nranges, F, cap, nblocks, max_blocks, out);
   return hipGetLastError();
 }
 hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s) {

@@ -111,6 +111,25 @@ struct Receiver {
   // diagnostics (AMOD_STREAM_DIAG): scan positions stepped, time spent waiting for pieces
   int64_t scanned = 0;
   mutable double wait_ms = 0;
+  double scan_ms = 0, refine_ms = 0; // (only timed with AMOD_STREAM_DIAG)
+  bool timed = false;
+  // speculative gap scans from the GPU (k_gap_scan), sorted by start; adopted when the
+  // receiver stands exactly at a record's start and its detection falls before `stop_block`
+  const std::vector<amod::GapScan> *gaps = nullptr;
+  int64_t stop_block = INT64_MAX;
+  int64_t gap_hits = 0;
+  bool adopt_gap() {
+    if (!gaps || st.ac_init || st.state != IDLE) return false;
+    auto it = std::lower_bound(gaps->begin(), gaps->end(), st.ac_pos,
+                               [](const amod::GapScan &g, int64_t p) { return g.s0 < p; });
+    if (it == gaps->end() || it->s0 != st.ac_pos || it->b1 != st.block || it->det_block >= stop_block) return false;
+    st.block = it->det_block; // (the caller steps past it)
+    st.ac_pos = it->ac_pos; st.ac_p = it->p; st.ac_ra = it->ra; st.ac_rb = it->rb; st.ac_init = true;
+    st.pre_pos = it->pre_pos; st.state = DETECTED;
+    scanned += it->scanned;
+    ++gap_hits;
+    return true;
+  }
 
   // the host copy of the cleaned stream arrives in pieces: local samples [0, avail) are
   // there; a read past it waits for the piece that holds it
@@ -150,6 +169,7 @@ struct Receiver {
 
   // _scanForPreamble (app.js:775-847)
   void scan() {
+    if (adopt_gap()) return;
     const int64_t half = 256, total = tw(), oldest = total - cap;
     if (st.ac_pos < oldest + 2 * half) { st.ac_pos = std::max<int64_t>(oldest + 2 * half, 0); st.ac_init = false; }
     const int64_t scan_end = total - 2 * half;
@@ -225,7 +245,40 @@ struct Receiver {
     const int64_t half = 256;
     double p = st.ac_p, ra = st.ac_ra, rb = st.ac_rb;
     int64_t pos = st.ac_pos;
+    // Quiet stretches in batches: the increments of a batch are independent of the sums
+    // (one vectorisable pass, each the same rounded expression as the loop's), the three
+    // sums then advance through them in order, and positions failing the metric
+    // pre-check while no detection is pending change nothing else. The first batch
+    // position that passes it is stepped by the position-by-position body.
+    constexpr int kB = 64;
+    alignas(64) double ip[kB], ia[kB], ib[kB], sp[kB], sa[kB], sb[kB];
     while (pos <= lim) {
+      if (!(best > 0.5 && best_pos >= 0) && pos + kB - 1 <= std::min(lim, scan_end - 1)) {
+        const float *const a0 = yy + pos, *const m0 = yy + pos + half, *const b0 = yy + pos + 2 * half;
+        for (int j = 0; j < kB; ++j) {
+          const double a_out = a0[j], mid = m0[j], b_in = b0[j];
+          ip[j] = mid * b_in - a_out * mid;
+          ia[j] = mid * mid - a_out * a_out;
+          ib[j] = b_in * b_in - mid * mid;
+        }
+        double q = p, r = ra, t = rb;
+        for (int j = 0; j < kB; ++j) { // the state at position pos + j, then its update
+          sp[j] = q; sa[j] = r; sb[j] = t;
+          q += ip[j]; r += ia[j]; t += ib[j];
+        }
+        int hit = kB;
+        for (int j = 0; j < kB; ++j)
+          if (sa[j] > min_e && sb[j] > min_e && sp[j] * sp[j] >= 0.49 * (sa[j] * sb[j])) { hit = j; break; }
+        if (hit == kB) {
+          p = q; ra = r; rb = t;
+          pos += kB;
+          scanned += kB;
+          continue;
+        }
+        p = sp[hit]; ra = sa[hit]; rb = sb[hit]; // positions before it were no-ops
+        pos += hit;
+        scanned += hit;
+      }
       if (ra > min_e && rb > min_e) {
         const double pp = p * p, rr = ra * rb;
         if (pp >= 0.49 * rr) {
@@ -350,8 +403,17 @@ void run_blocks(Receiver &rx, const RxState &start, int64_t stop, bool first_onl
                 int64_t *sync_idx) {
   rx.st = start;
   rx.fails = &out.fails;
+  rx.stop_block = stop;
   if (sync_idx) *sync_idx = -1;
   while (rx.st.block < stop) {
+    if (rx.timed && rx.st.state != COLLECTING) { // diagnostics
+      const auto t0 = std::chrono::steady_clock::now();
+      const bool idle = rx.st.state == IDLE;
+      if (idle) rx.scan(); else rx.refine();
+      (idle ? rx.scan_ms : rx.refine_ms) += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      ++rx.st.block;
+      continue;
+    }
     switch (rx.st.state) {
     case IDLE: rx.scan(); break;
     case DETECTED: rx.refine(); break;
@@ -399,6 +461,9 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
   for (int k = 0; k <= T; ++k) bnd[k] = start.block + span * k / T;
   std::vector<Traj> seg(T);
   std::vector<Receiver> rxs(T, proto);
+  const bool diag = getenv("AMOD_STREAM_DIAG") != nullptr;
+  for (auto &r : rxs) r.timed = diag;
+  std::vector<double> th_ms(T, 0.0);
   std::vector<std::thread> th;
   for (int k = 0; k < T; ++k) {
     th.emplace_back([&, k] {
@@ -411,7 +476,9 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
         st.meta_received = start.meta_received;
         st.chunk_size = start.chunk_size;
       }
+      const auto t0 = std::chrono::steady_clock::now();
       run_blocks(rxs[k], st, bnd[k + 1], false, nullptr, seg[k], nullptr);
+      th_ms[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
   }
   for (auto &t : th) t.join();
@@ -445,6 +512,10 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
             std::chrono::duration<double, std::milli>(t_threads - t_par0).count(), wmax,
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_threads).count(), rx.wait_ms,
             (long long)sc, total.frames.size());
+    for (int k = 0; k < T; ++k)
+      fprintf(stderr, "[stream]   thread %d: %.3f ms (scan %.3f, refine %.3f), scanned %lld, frames %zu, gpu gaps %lld\n",
+              k, th_ms[k], rxs[k].scan_ms, rxs[k].refine_ms, (long long)rxs[k].scanned, seg[k].frames.size(),
+              (long long)rxs[k].gap_hits);
   }
   return total;
 }
@@ -472,6 +543,8 @@ struct StreamCache {
   DBuf d_pre1, d_first, d_base, d_count, d_out;
   DBuf w_pos, w_len, w_woff, w_win, w_res, w_pay;
   DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
+  DBuf d_barg, d_gaps;                      // k_fine's per-workgroup argmax, k_gap_scan's records
+  Pinned gaps_h;
   Pinned yh, yc, hot_h, metric_h;
   Pinned w_res_h, w_pay_h;                  // window decoder: results and payload rows (pinned D2H)
   bool apow_ready = false;
@@ -592,6 +665,37 @@ struct Prepass {
   // speculative segment), packs them on the GPU and copies them to the host in pieces.
   // Reads outside them still work (present() fetches). Returns false when the full copy
   // is (or was) used instead.
+  // ---- speculative gap scans on the GPU (k_gap_scan): one per fine range, from where the
+  // receiver would stand after the frame detected there (window length F)
+  int nbx = 0, nfr = 0;
+  std::vector<amod::GapScan> gaps;
+  bool gap_launched = false;
+  int gap_scan_launch(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int64_t cap) {
+    gaps.clear();
+    gap_launched = false;
+    if (nfr <= 0 || getenv("AMOD_NO_GAP_SCAN")) return AMOD_SUCCESS;
+    const int32_t maxp = start.meta_received ? (start.chunk_size ? start.chunk_size : 4096) + 11 : 280;
+    const int64_t F = amod_estimate_frame_samples(cfg, maxp);
+    if (c->d_gaps.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
+        c->gaps_h.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
+        amod_launch_gap_scan(c->d_y.as<float>(), n, lo, c->d_first.as<int64_t>(), c->d_barg.as<double2>(), nbx, nfr,
+                             F, cap, nblocks, 64, c->d_gaps.as<amod::GapScan>(), s_main) != hipSuccess ||
+        hipMemcpyAsync(c->gaps_h.p, c->d_gaps.p, sizeof(amod::GapScan) * (size_t)nfr, hipMemcpyDeviceToHost,
+                       s_main) != hipSuccess)
+      return AMOD_ERR_HIP;
+    gap_launched = true;
+    return AMOD_SUCCESS;
+  }
+  int gap_scan_finish() {
+    if (!gap_launched) return AMOD_SUCCESS;
+    if (hipStreamSynchronize(s_main) != hipSuccess) return AMOD_ERR_HIP;
+    const amod::GapScan *g = c->gaps_h.as<amod::GapScan>();
+    for (int r = 0; r < nfr; ++r)
+      if (g[r].status == 1) gaps.push_back(g[r]);
+    std::sort(gaps.begin(), gaps.end(), [](const amod::GapScan &a, const amod::GapScan &b) { return a.s0 < b.s0; });
+    return AMOD_SUCCESS;
+  }
+
   bool sparse_setup(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int nthreads) {
     if (!sparse || full_started) return false;
     ng = n >> kGranLog;
@@ -604,11 +708,15 @@ struct Prepass {
     };
     // hot regions (local), blocks less than 2 K samples apart merged
     std::vector<std::pair<int64_t, int64_t>> reg;
-    const uint8_t *hot = c->hot_h.as<uint8_t>();
-    for (int64_t b = 0; b < n / 32; ++b) {
-      if (!hot[b]) continue;
-      if (!reg.empty() && 32 * b <= reg.back().second + 2048) reg.back().second = 32 * b + 32;
-      else reg.push_back({32 * b, 32 * b + 32});
+    if (gap_launched) { // (the fine ranges: hot blocks +- 448 samples, merged)
+      for (size_t r = 0; r < ft.first.size(); ++r) reg.push_back({ft.first[r] - lo + 448, ft.first[r] - lo + ft.count[r] - 448});
+    } else {
+      const uint8_t *hot = c->hot_h.as<uint8_t>();
+      for (int64_t b = 0; b < n / 32; ++b) {
+        if (!hot[b]) continue;
+        if (!reg.empty() && 32 * b <= reg.back().second + 2048) reg.back().second = 32 * b + 32;
+        else reg.push_back({32 * b, 32 * b + 32});
+      }
     }
     const int32_t maxp = start.meta_received ? (start.chunk_size ? start.chunk_size : 4096) + 11 : 280;
     const int64_t F = amod_estimate_frame_samples(cfg, maxp);
@@ -620,6 +728,10 @@ struct Prepass {
       mark(p - 1024, it == reg.end() ? p + F + W : it->first);
     };
     for (size_t k = 0; k < reg.size(); ++k) {
+      if (gap_launched) { // the scans come from the GPU: the refinement window only
+        mark(reg[k].first - R, reg[k].second + R);
+        continue;
+      }
       mark(reg[k].first - R - 1024, reg[k].second + R + W);
       scan_from(reg[k].first - R + F); // the scan after the frame detected in region k
     }
@@ -763,11 +875,15 @@ struct Prepass {
       S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
+      nbx = (int)((maxc + 255) / 256);
+      nfr = nr;
+      S_TRY(c->d_barg.alloc(sizeof(double2) * (size_t)nr * nbx));
       for (int r0 = 0; r0 < nr; r0 += 65535) {
         const int k = std::min(65535, nr - r0);
         S_TRY(amod_launch_fine(c->d_y.as<float>(), n, c->d_pre1.as<float>(), cfg->symbol_len, p1e,
                                c->d_first.as<int64_t>() + r0, c->d_base.as<int64_t>() + r0,
-                               c->d_count.as<int64_t>() + r0, k, maxc, (double *)c->metric_h.dp, s));
+                               c->d_count.as<int64_t>() + r0, k, maxc, (double *)c->metric_h.dp,
+                               c->d_barg.as<double2>() + (int64_t)r0 * nbx, s));
       }
     }
     S_TRY(hipEventRecord(ev[2], s));
@@ -1032,7 +1148,20 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     } else {
       if (!sparse_done) { // from here on the state machine reads only where frames start
         sparse_done = true;
-        if (pp.sparse_setup(cfg, st, nblocks, nthreads)) {
+        // the GPU's gap scans run while the host sets up the sparse copy
+        const auto tg0 = clk::now();
+        int grc = pp.gap_scan_launch(cfg, st, nblocks, proto.cap);
+        if (grc) return amod_ctx_fail(ctx, "gap scan", grc);
+        const bool sp_ok = pp.sparse_setup(cfg, st, nblocks, nthreads);
+        const auto tg1 = clk::now();
+        grc = pp.gap_scan_finish();
+        if (grc) return amod_ctx_fail(ctx, "gap scan", grc);
+        if (!pp.gaps.empty()) proto.gaps = &pp.gaps;
+        if (getenv("AMOD_STREAM_DIAG"))
+          fprintf(stderr, "[stream] sparse setup %.3f ms, then gap scan: %zu records, +%.3f ms\n",
+                  std::chrono::duration<double, std::milli>(tg1 - tg0).count(), pp.gaps.size(),
+                  std::chrono::duration<double, std::milli>(clk::now() - tg1).count());
+        if (sp_ok) {
           proto.gptr = pp.gptr.get(); proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
         }
       }
