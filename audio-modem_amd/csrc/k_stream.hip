@@ -260,6 +260,7 @@ __global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ z
 
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
 // base[r] + j; one lane per position
+constexpr int kFineMaxSym = 1024; // symbol_len bound of k_fine's LDS window (presets: 576 .. 768)
 // barg (optional): per workgroup, the first maximum of its positions' metrics (NaN
 // skipped, as the refinement's `metric > best`) as (metric, j), at [r * gridDim.x + bx]
 __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const float *__restrict__ pre1,
@@ -267,15 +268,25 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
                                               const int64_t *__restrict__ base, const int64_t *__restrict__ count,
                                               int nranges, double *__restrict__ out, double2 *__restrict__ barg) {
   __shared__ double2 red[4];
+  __shared__ float win[256 + kFineMaxSym]; // the workgroup's samples [d0, d0 + 256 + sym)
   const int r = blockIdx.y;
   if (r >= nranges) return;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * 256, j = j0 + threadIdx.x;
+  if (j0 >= count[r]) { // (whole workgroup) no position: an empty record
+    if (barg && threadIdx.x == 0) barg[(int64_t)r * gridDim.x + blockIdx.x] = make_double2(-__builtin_inf(), (double)j0);
+    return;
+  }
+  {
+    const int64_t d0 = first[r] + j0;
+    for (int i = threadIdx.x; i < 256 + sym; i += 256) win[i] = sample_at(y, n, d0 + i);
+    __syncthreads();
+  }
   double m = -__builtin_inf();
   if (j < count[r]) {
-    const int64_t d = first[r] + j;
     double corr = 0.0, se = 0.0;
+    const float *const w = win + threadIdx.x;
     for (int i = 0; i < sym; ++i) {
-      const double s = sample_at(y, n, d + i);
+      const double s = w[i];
       corr += s * (double)pre1[i];
       se += s * s;
     }
@@ -493,6 +504,7 @@ hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sy
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
                             int64_t maxcount, double *out, double2 *barg, hipStream_t s) {
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
+  if (sym <= 0 || sym > amod::kFineMaxSym) return hipErrorInvalidValue;
   hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
                      pre1_energy, first, base, count, nranges, out, barg);
   return hipGetLastError();
