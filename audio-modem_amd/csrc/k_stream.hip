@@ -316,88 +316,154 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
 // Receiver::scan in stream.cpp replays it). For fine range r: its first fine-metric
 // maximum d is where the refinement would put the frame, so the receiver would reset to
 // IDLE with its scan at s0 = d + F (ac sums not initialised) in block ceil(s0 / 4096).
-// From that state the scan is a function of the stream alone: one wave per range runs it
-// block by block with the host's arithmetic in the host's order (IEEE double, no
-// contraction: this file is built with -ffp-contract=off) until a detection, and
-// records the state the host would be in. The host adopts a record only when its true
-// state matches the start exactly; anything else (no detection within the block limit,
-// the ring's oldest sample overtaken) is left to the host (status 0).
-// Positions go in tiles of 64: lane j forms position j's increments (coalesced loads),
-// the three running sums then advance through them in order (uniform, read lane by
-// lane), lane j keeps the sums at its position, and a tile in which no lane passes the
-// metric pre-check (no detection pending) is done; otherwise its positions from the first
-// such lane are stepped one by one from the kept sums.
+// From that state the scan is a function of the stream alone, run here block by block
+// with the host's arithmetic in the host's order (IEEE double, no contraction: this file
+// is built with -ffp-contract=off) until a detection; the record holds the state the
+// host would then be in. The host adopts a record only when its true state matches the
+// start exactly; anything else (no detection within the block limit, the ring's oldest
+// sample overtaken) is left to the host (status 0).
+// One wave runs kGapG gaps in tiles of 64 positions: (A) lane t forms position t's three
+// increments for each gap (coalesced loads), (B) lane g advances gap g's three running
+// sums through its tile in order and keeps the sums at every position, (C) lane t tests
+// position t of each gap: the metric pre-check, and where it passes (or a detection is
+// pending) the running best as an inclusive prefix maximum (a later equal metric never
+// replaces the earlier: strict '>') and the 0.7 drop on the sums after the position.
 __device__ __forceinline__ double rl_d(double v, int j) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), j), hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
   return __hiloint2double(hi, lo);
 }
+__device__ __forceinline__ int64_t rl_l(int64_t v, int j) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), j) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j));
+}
+constexpr int kGapG = 2;  // gaps per wave (measured: 8 -> 0.59 ms, 2 -> 0.40, 1 -> 0.57 on the C4-shaped stream)
+constexpr int kGapS = 65; // LDS row stride (doubles): lanes g of phase B on distinct banks
 __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, int64_t n, int64_t lo,
                                                  const int64_t *__restrict__ first, const double2 *__restrict__ barg,
                                                  int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks,
                                                  int max_blocks, GapScan *__restrict__ out) {
-  const int r = blockIdx.x, lane = threadIdx.x;
-  if (r >= nranges) return;
-  GapScan g{};
-  double2 b = barg[(int64_t)r * nbx];
-  for (int k = 1; k < nbx; ++k) {
-    const double2 v = barg[(int64_t)r * nbx + k];
-    if (v.x > b.x) b = v; // (blocks in position order: ties keep the first)
-  }
-  auto emit = [&]() { if (lane == 0) out[r] = g; };
-  if (!(b.x >= 0.1)) { emit(); return; } // the refinement fails there: no frame
-  const int64_t s0 = lo + first[r] + (int64_t)b.y + F; // global stream position
+  __shared__ double inc[3][kGapG][kGapS]; // phase A -> B: increments of each gap's tile positions
+  __shared__ double stt[3][kGapG][kGapS]; // phase B -> C: sums at each tile position, then the tile's end
   constexpr int64_t kBlk = 4096, half = 256;
-  const int64_t b1 = (s0 + kBlk - 1) / kBlk;
-  g.s0 = s0; g.b1 = b1;
-  auto S = [&](int64_t i) -> double { return (double)sample_at(y, n, i - lo); };
-  int64_t pos = s0, scanned = 0;
-  double p = 0.0, ra = 0.0, rb = 0.0; // uniform
-  bool init = false;
   const double min_e = 0.001;
-  for (int64_t blk = b1; blk < min(nblocks, b1 + max_blocks); ++blk) {
-    const int64_t total = (blk + 1) * kBlk, oldest = total - cap;
-    if (pos < oldest + 2 * half) break; // the host re-positions the scan: its own business
-    const int64_t scan_end = total - 2 * half;
-    if (pos > scan_end) continue;
-    if (!init) { // the window sums, in order (products on the lanes, sums read lane by lane)
-      for (int m0 = 0; m0 < (int)half; m0 += 64) {
-        const double a = S(pos + m0 + lane), c = S(pos + m0 + lane + half);
-        const double ab = a * c, aa = a * a, cc = c * c;
-        for (int j = 0; j < 64; ++j) { p += rl_d(ab, j); ra += rl_d(aa, j); rb += rl_d(cc, j); }
-      }
-      init = true;
+  const int lane = threadIdx.x;
+  const int r = blockIdx.x * kGapG + lane;
+  auto S = [&](int64_t i) -> double { return (double)sample_at(y, n, i - lo); };
+  // ---- per-gap state, lane g = gap g
+  bool act = lane < kGapG && r < nranges;
+  GapScan rec{};
+  int64_t pos = 0, blk = 0, blim = 0, scan_end = 0, best_pos = -1, scanned = 0;
+  double p = 0.0, ra = 0.0, rb = 0.0, best = 0.0;
+  // the block whose scan call steps position pos (oldest-sample check and block limit as
+  // the host's scan calls meet them); false: the record stays status 0
+  auto to_block = [&]() -> bool {
+    for (;;) {
+      if (blk >= blim) return false;
+      const int64_t total = (blk + 1) * kBlk;
+      if (pos < total - cap + 2 * half) return false; // the host re-positions the scan: its own business
+      scan_end = total - 2 * half;
+      if (pos <= scan_end) return true;
+      ++blk;
     }
-    double best = 0.0;
-    int64_t best_pos = -1;
-    while (pos <= scan_end) {
-      const int T = (int)min<int64_t>(64, scan_end - pos + 1);
-      // increments of positions pos + j < scan_end (the one at scan_end takes none)
-      const int64_t x = pos + lane;
-      const bool upd = lane < T && x < scan_end;
-      double ip = 0.0, ia = 0.0, ib = 0.0;
-      if (upd) {
-        const double a_out = S(x), mid = S(x + half), b_in = S(x + 2 * half);
-        ip = mid * b_in - a_out * mid;
-        ia = mid * mid - a_out * a_out;
-        ib = b_in * b_in - mid * mid;
+  };
+  if (act) {
+    double2 b = barg[(int64_t)r * nbx];
+    for (int k = 1; k < nbx; ++k) {
+      const double2 v = barg[(int64_t)r * nbx + k];
+      if (v.x > b.x) b = v; // (blocks in position order: ties keep the first)
+    }
+    if (b.x >= 0.1) { // else the refinement fails there: no frame, no record
+      pos = lo + first[r] + (int64_t)b.y + F;
+      blk = (pos + kBlk - 1) / kBlk;
+      rec.s0 = pos; rec.b1 = blk;
+      blim = min(nblocks, blk + max_blocks);
+      act = to_block();
+    } else {
+      act = false;
+    }
+  }
+  // ---- the window sums at the start, in order (products on the lanes, sums per gap)
+  {
+    const unsigned long long am = __ballot(act);
+    for (int c = 0; c < (int)half; c += 64) {
+      for (int gi = 0; gi < kGapG; ++gi) {
+        if (!((am >> gi) & 1)) continue;
+        const int64_t base = rl_l(pos, gi) + c;
+        const double a = S(base + lane), bb = S(base + lane + half);
+        inc[0][gi][lane] = a * bb; inc[1][gi][lane] = a * a; inc[2][gi][lane] = bb * bb;
       }
-      const unsigned long long um = __ballot(upd);
-      double sp = p, sa = ra, sb = rb; // lane j: the sums at position pos + j
-      for (int j = 0; j < T; ++j) {
-        if (lane == j) { sp = p; sa = ra; sb = rb; }
-        if ((um >> j) & 1) { p += rl_d(ip, j); ra += rl_d(ia, j); rb += rl_d(ib, j); }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (act)
+        for (int m = 0; m < 64; ++m) { p += inc[0][lane][m]; ra += inc[1][lane][m]; rb += inc[2][lane][m]; }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+  }
+  // ---- tiles; each tile's samples are loaded during the previous one (a continuing
+  // gap's next tile starts where this one ends, whatever happens at the block's end)
+  float va[kGapG], vm[kGapG], vb[kGapG];
+  auto load_tile = [&](unsigned long long live, int64_t at_lane) { // at_lane: lane g's tile start
+#pragma unroll
+    for (int gi = 0; gi < kGapG; ++gi) {
+      const int64_t x = ((live >> gi) & 1) ? rl_l(at_lane, gi) + lane - lo : -(int64_t)(1 << 20);
+      va[gi] = sample_at(y, n, x);
+      vm[gi] = sample_at(y, n, x + half);
+      vb[gi] = sample_at(y, n, x + 2 * half);
+    }
+  };
+  load_tile(__ballot(act), pos);
+  for (;;) {
+    const unsigned long long am = __ballot(act);
+    if (!am) break;
+    const int T = act ? (int)min<int64_t>(64, scan_end - pos + 1) : 0; // lane g: gap g's tile length
+    // (A) lane t: increments of position t of each live gap (none at scan_end)
+#pragma unroll
+    for (int gi = 0; gi < kGapG; ++gi) {
+      const bool up = ((am >> gi) & 1) && rl_l(pos, gi) + lane < rl_l(scan_end, gi);
+      const double a_out = va[gi], mid = vm[gi], b_in = vb[gi];
+      inc[0][gi][lane] = up ? mid * b_in - a_out * mid : 0.0;
+      inc[1][gi][lane] = up ? mid * mid - a_out * a_out : 0.0;
+      inc[2][gi][lane] = up ? b_in * b_in - mid * mid : 0.0;
+    }
+    load_tile(am, pos + T); // the next tile's samples, in flight under this one
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // (B) lane g: gap g's sums through its tile, in order
+    if (act) {
+      const int tu = (int)min<int64_t>(T, scan_end - pos); // positions with an update (all but scan_end)
+      int t = 0;
+      for (; t + 8 <= tu; t += 8) { // eight increments read ahead of the dependent sums
+        double i0[8], i1[8], i2[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { i0[u] = inc[0][lane][t + u]; i1[u] = inc[1][lane][t + u]; i2[u] = inc[2][lane][t + u]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          stt[0][lane][t + u] = p; stt[1][lane][t + u] = ra; stt[2][lane][t + u] = rb;
+          p += i0[u]; ra += i1[u]; rb += i2[u];
+        }
       }
-      // (p, ra, rb): the sums after the tile
-      const bool pending = best > 0.5 && best_pos >= 0;
-      const bool c = lane < T && sa > min_e && sb > min_e && sp * sp >= 0.49 * (sa * sb);
+      for (; t < T; ++t) {
+        stt[0][lane][t] = p; stt[1][lane][t] = ra; stt[2][lane][t] = rb;
+        if (t < tu) { p += inc[0][lane][t]; ra += inc[1][lane][t]; rb += inc[2][lane][t]; }
+      }
+      stt[0][lane][T] = p; stt[1][lane][T] = ra; stt[2][lane][T] = rb;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // (C) lane t: position t of each live gap
+    bool det_here = false; // lane g: gap g detected in this tile
+    for (int gi = 0; gi < kGapG; ++gi) {
+      if (!((am >> gi) & 1)) continue;
+      const int Tg = __builtin_amdgcn_readlane(T, gi);
+      const double sp = stt[0][gi][lane], sa = stt[1][gi][lane], sb = stt[2][gi][lane];
+      const bool c = lane < Tg && sa > min_e && sb > min_e && sp * sp >= 0.49 * (sa * sb);
       const unsigned long long hits = __ballot(c);
-      if (!pending && !hits) { pos += T; scanned += T; continue; }
-      // the tile's positions in parallel: lane j's metric from its kept sums (gated as the
-      // loop gates it), the running best as an inclusive prefix maximum (a later equal
-      // metric never replaces the earlier: strict '>'), and the 0.7 drop tested on the
-      // sums after position j (lane j + 1's, or the tile's end)
-      const double pn = __shfl_down(sp, 1, 64), ran = __shfl_down(sa, 1, 64), rbn = __shfl_down(sb, 1, 64);
-      const double pa = lane + 1 < T ? pn : p, raa = lane + 1 < T ? ran : ra, rba = lane + 1 < T ? rbn : rb;
+      const double bin = rl_d(best, gi);
+      const int64_t bpin = rl_l(best_pos, gi);
+      if (!(bin > 0.5 && bpin >= 0) && !hits) continue;
+      const int ln = min(lane + 1, 64);
+      const double pa = stt[0][gi][ln], raa = stt[1][gi][ln], rba = stt[2][gi][ln]; // sums after position t
       double key = -__builtin_inf();
       int kidx = 64;
       if (c) {
@@ -409,36 +475,49 @@ __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, in
         const int oi = __shfl_up(kidx, o, 64);
         if (lane >= o && (ok > key || (ok == key && oi < kidx))) { key = ok; kidx = oi; }
       }
-      double bj = best;
-      int64_t bpj = best_pos;
-      if (key > bj) { bj = key; bpj = pos + kidx; }
+      const int64_t base = rl_l(pos, gi);
+      double bj = bin;
+      int64_t bpj = bpin;
+      if (key > bj) { bj = key; bpj = base + kidx; }
       bool det = false;
-      if (lane < T && bj > 0.5 && bpj >= 0 && raa > min_e && rba > min_e) det = (pa * pa) / (raa * rba) < bj * 0.7;
+      if (lane < Tg && bj > 0.5 && bpj >= 0 && raa > min_e && rba > min_e) det = (pa * pa) / (raa * rba) < bj * 0.7;
       const unsigned long long dm = __ballot(det);
       if (dm) {
         const int j = __builtin_ctzll(dm);
-        g.status = 1; g.det_block = blk;
-        g.pre_pos = ((int64_t)__builtin_amdgcn_readlane((int)(bpj >> 32), j) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpj, j);
-        g.ac_pos = pos + j + 1;
-        g.p = rl_d(pa, j); g.ra = rl_d(raa, j); g.rb = rl_d(rba, j);
-        g.scanned = scanned + j + 1;
-        emit();
-        return;
+        const int64_t pre = rl_l(bpj, j);
+        const double dp = rl_d(pa, j), dra = rl_d(raa, j), drb = rl_d(rba, j);
+        if (lane == gi) {
+          rec.status = 1; rec.det_block = blk; rec.pre_pos = pre; rec.ac_pos = pos + j + 1;
+          rec.p = dp; rec.ra = dra; rec.rb = drb; rec.scanned = scanned + j + 1;
+          det_here = true;
+        }
+      } else {
+        const double nb = rl_d(bj, Tg - 1);
+        const int64_t nbp = rl_l(bpj, Tg - 1);
+        if (lane == gi) { best = nb; best_pos = nbp; }
       }
-      best = rl_d(bj, T - 1);
-      best_pos = ((int64_t)__builtin_amdgcn_readlane((int)(bpj >> 32), T - 1) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpj, T - 1);
-      pos += T; scanned += T;
     }
-    if (best > 0.5 && best_pos >= 0) { // end-of-block commit
-      g.status = 1; g.det_block = blk; g.pre_pos = best_pos; g.ac_pos = pos; g.p = p; g.ra = ra; g.rb = rb;
-      g.scanned = scanned;
-      emit();
-      return;
+    __builtin_amdgcn_wave_barrier();
+    // (D) lane g: the tile done; at the block's end the commit or the next block
+    if (act) {
+      if (det_here) {
+        act = false;
+      } else {
+        pos += T; scanned += T;
+        if (pos > scan_end) {
+          if (best > 0.5 && best_pos >= 0) { // end-of-block commit
+            rec.status = 1; rec.det_block = blk; rec.pre_pos = best_pos; rec.ac_pos = pos;
+            rec.p = p; rec.ra = ra; rec.rb = rb; rec.scanned = scanned;
+            act = false;
+          } else {
+            ++blk; best = 0.0; best_pos = -1;
+            act = to_block();
+          }
+        }
+      }
     }
   }
-  emit(); // status 0
+  if (lane < kGapG && r < nranges) out[r] = rec;
 }
 
 // the host's sparse copy of the cleaned stream: compact granule j (1024 samples) is stream
@@ -513,7 +592,8 @@ hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int
                                 int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks, int max_blocks,
                                 amod::GapScan *out, hipStream_t s) {
   if (nranges <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_gap_scan, dim3((unsigned)nranges), dim3(64), 0, s, y, n, lo, first, barg,
+  hipLaunchKernelGGL(amod::k_gap_scan, dim3((unsigned)((nranges + amod::kGapG - 1) / amod::kGapG)), dim3(64), 0, s, y, n,
+                     lo, first, barg,
                      nbx, nranges, F, cap, nblocks, max_blocks, out);
   return hipGetLastError();
 }

@@ -44,6 +44,9 @@ constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
 const int64_t kEmaChunk = amod_ema_chunk(); // k_ema chunk (EMA end states are reported per chunk)
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
 constexpr int kGranLog = 10, kGran = 1 << kGranLog; // sparse host copy granule (samples)
+// blocks a GPU gap scan runs before it leaves the gap to the host (the kernel's time is its
+// longest gap's: a stream's tail or a long silence is the host's)
+constexpr int kGapBlocks = 8;
 enum { IDLE = 0, DETECTED = 1, COLLECTING = 2 };
 
 struct DBuf {
@@ -679,7 +682,7 @@ struct Prepass {
     if (c->d_gaps.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
         c->gaps_h.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
         amod_launch_gap_scan(c->d_y.as<float>(), n, lo, c->d_first.as<int64_t>(), c->d_barg.as<double2>(), nbx, nfr,
-                             F, cap, nblocks, 64, c->d_gaps.as<amod::GapScan>(), s_main) != hipSuccess ||
+                             F, cap, nblocks, kGapBlocks, c->d_gaps.as<amod::GapScan>(), s_main) != hipSuccess ||
         hipMemcpyAsync(c->gaps_h.p, c->d_gaps.p, sizeof(amod::GapScan) * (size_t)nfr, hipMemcpyDeviceToHost,
                        s_main) != hipSuccess)
       return AMOD_ERR_HIP;
@@ -1157,10 +1160,13 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
         grc = pp.gap_scan_finish();
         if (grc) return amod_ctx_fail(ctx, "gap scan", grc);
         if (!pp.gaps.empty()) proto.gaps = &pp.gaps;
-        if (getenv("AMOD_STREAM_DIAG"))
-          fprintf(stderr, "[stream] sparse setup %.3f ms, then gap scan: %zu records, +%.3f ms\n",
-                  std::chrono::duration<double, std::milli>(tg1 - tg0).count(), pp.gaps.size(),
-                  std::chrono::duration<double, std::milli>(clk::now() - tg1).count());
+        if (getenv("AMOD_STREAM_DIAG")) {
+          int64_t smax = 0, ssum = 0;
+          for (auto &g : pp.gaps) { smax = std::max(smax, g.scanned); ssum += g.scanned; }
+          fprintf(stderr, "[stream] sparse setup %.3f ms, then gap scan: %zu records (%lld positions, longest %lld), +%.3f ms\n",
+                  std::chrono::duration<double, std::milli>(tg1 - tg0).count(), pp.gaps.size(), (long long)ssum,
+                  (long long)smax, std::chrono::duration<double, std::milli>(clk::now() - tg1).count());
+        }
         if (sp_ok) {
           proto.gptr = pp.gptr.get(); proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
         }
