@@ -21,3 +21,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_
 timeout -k 10 240 python3 "$B" --config c5 --snr 20 --no-e2e > "$out/bench_c5_20db.json" 2> "$out/c5_20.err" &&
 timeout -k 10 240 python3 "$B" --config c5 --snr 10 --soft --no-e2e > "$out/bench_c5_10db.json" 2> "$out/c5_10.err" &&
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/ktrace_c5" -o run --output-format csv -- python3 "$B" --config c5 --snr 10 $quick > /dev/null 2> "$out/ktrace_c5.err"
+# the streaming receiver's kernels (the bench's stream leg: C4-shaped 2000-chunk stream)
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$out/ktrace_stream" -o run --output-format csv -- python3 "$B" --steps 2 --warmup 1 --cpu-frames -1 --no-e2e > "$out/bench_stream_under_rocprof.json" 2> "$out/ktrace_stream.err"
