@@ -553,7 +553,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // exact-kernel grid: persistent workgroups over the listed frames (usually none: the
   // launch then costs its dispatch, so two per CU, not one per slot)
-  const int xslots = std::min({ctx->nslots, nframes, 2 * std::max(1, ctx->cu_count)});
+  int xslots = std::min({ctx->nslots, nframes, 2 * std::max(1, ctx->cu_count)});
+  if (const char *xs = getenv("AMOD_XSLOTS")) xslots = std::max(1, std::min(xslots, atoi(xs))); // experiments
   // list A's exact kernel, then (detection replay) k_demod over the frames it only
   // detected: a frame listed for COARSE / FINE / THRESH alone gets its preambleIdx from
   // the fp64 replica and its symbols from the fast path (AMOD_NO_REPLAY: diagnostics)

@@ -30,7 +30,18 @@ def main():
     dm.reserve(cfg, F, N)
     lib = L.load()
     ts = torch.cuda.current_stream(dev).cuda_stream
-    for label, stream in (("own stream", 0), ("torch stream", ts), ("own stream", 0), ("torch stream", ts)):
+    plan = [("own stream", 0, None), ("torch stream", ts, None), ("own stream", 0, None), ("torch stream", ts, None)]
+    for c in os.environ.get("PROBE_CHUNKS", "").split(","):
+        if c:
+            plan += [(f"chunks={c}", ts, ("AMOD_CHUNKS", c)), ("torch stream", ts, None)]
+    for c in os.environ.get("PROBE_XSLOTS", "").split(","):
+        if c:
+            plan += [(f"xslots={c}", ts, ("AMOD_XSLOTS", c)), ("torch stream", ts, None)]
+    for label, stream, knob in plan:
+        for k in ("AMOD_CHUNKS", "AMOD_XSLOTS"):
+            os.environ.pop(k, None)
+        if knob:
+            os.environ[knob[0]] = knob[1]
         for _ in range(3):
             dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
                              res.data_ptr(), pay.data_ptr(), stride, stream=stream)
@@ -46,8 +57,8 @@ def main():
         n = C.c_int64()
         lib.amod_kernel_breakdown(dm.ctx, ms, C.byref(n))
         lib.amod_set_profiling(dm.ctx, 0)
-        print(f"{label:14s} detect {ms[0] / n.value:.4f}  demod+aux {ms[1] / n.value:.4f}  exactB {ms[2] / n.value:.4f} ms",
-              flush=True)
+        print(f"{label:14s} detect {ms[0] / n.value:.4f}  demod+aux {ms[1] / n.value:.4f}  exactB {ms[2] / n.value:.4f} "
+              f"total {(ms[0] + ms[1] + ms[2]) / n.value:.4f} ms", flush=True)
     dm.close()
 
 
