@@ -189,3 +189,34 @@ def test_speculative_long_noisy_stream():
     par = _run(cfg, x, {"AMOD_STREAM_THREADS": "16", "AMOD_STREAM_MINSEG": "3"})
     assert len(seq[0]) >= 100
     assert np.array_equal(seq[0], par[0]) and seq[1] == par[1] and seq[3] == par[3] and seq[4] == par[4]
+
+
+def test_gpu_gap_scans_equal_host_scans():
+    """The scans between frames come from the GPU (k_gap_scan: speculated from each fine
+    range's first maximum, adopted only on an exact state match, gaps past 8 blocks left
+    to the host). A stream with irregular gaps (one of 60,000 samples), a DC step, AWGN
+    and corrupted chunks gives the same windows, results, failed refinements, counters
+    and file with them as with every scan run on the host (AMOD_NO_GAP_SCAN)."""
+    cfg = amodem.preset("standard", "QPSK", 1)
+    data = amodem.synth_payload(0x99, 80 * 1024)
+    parts = [np.zeros(7000, np.float32), amodem.build_metadata_frame(80, len(data), 1024, "gaps.bin", cfg=cfg)]
+    for i in range(80):
+        f = amodem.build_data_chunk_frame(data[i * 1024:(i + 1) * 1024], i, cfg=cfg)
+        if i in (9, 41):
+            f = f.copy()
+            f[4000:4400] = np.float32(-0.6)
+        parts.append(f)
+        parts.append(np.zeros(60000 if i == 30 else (i * 1453) % 9000, np.float32))
+    x = np.concatenate(parts + [np.zeros(30000, np.float32)])
+    x = np.concatenate([x, np.zeros(-len(x) % 4096, np.float32)])
+    x[len(x) // 3:] = (x[len(x) // 3:].astype(np.float64) - 0.03).astype(np.float32)
+    x = O.apply_post(x, [{"op": "noise", "snr": 28, "seed": 0x4321}])
+    host = _run(cfg, x, {"AMOD_NO_GAP_SCAN": "1", "AMOD_STREAM_THREADS": "16"})
+    gpu = _run(cfg, x, {"AMOD_STREAM_THREADS": "16"})
+    seq = _run(cfg, x, {"AMOD_STREAM_THREADS": "1", "AMOD_NO_GAP_SCAN": "1"})
+    assert len(host[0]) >= 70
+    keys = ("nframes", "nrefine_fail", "frames_decoded", "frame_errors", "final_state", "final_scan_pos")
+    for other in (gpu, seq):
+        assert np.array_equal(host[0], other[0]) and host[1] == other[1]
+        assert [host[2][k] for k in keys] == [other[2][k] for k in keys]
+        assert host[3] == other[3] and host[4] == other[4]
