@@ -30,35 +30,52 @@ struct amod_assembler {
   std::vector<uint8_t> bitmap;
   int32_t received = 0, crc_errors = 0;
   bool has_store = false;                          // IndexedDB opened by a metadata frame
-  std::map<int32_t, std::vector<uint8_t>> chunks;  // seqNum -> data (memory store)
+  // memory store: chunk bytes appended to one arena; seqNum -> (offset, length), dense for
+  // 0 <= seq < totalChunks (up to 1 M), a map for any other seqNum (a rewrite appends a
+  // new copy)
+  std::vector<uint8_t> arena;
+  std::vector<std::pair<int64_t, int32_t>> dense;  // offset -1: none
+  std::map<int32_t, std::pair<int64_t, int32_t>> other;
+  std::map<int32_t, bool> files;                   // file store: the seqNums written
   std::string dir;                                 // file store when not empty
   int32_t frames_decoded = 0, frame_errors = 0;    // StreamingReceiver counters
 
   std::string path(int32_t seq) const { return dir + "/chunk_" + std::to_string(seq) + ".bin"; }
   void clear_store() {
     if (!dir.empty())
-      for (const auto &kv : chunks) remove(path(kv.first).c_str());
-    chunks.clear();
+      for (const auto &kv : files) remove(path(kv.first).c_str());
+    files.clear();
+    arena.clear();
+    // (dense up to 1 M chunks; a larger claimed totalChunks keeps the map alone)
+    dense.assign(total_chunks > 0 && total_chunks <= (1 << 20) ? (size_t)total_chunks : 0, {-1, 0});
+    other.clear();
   }
   bool put(int32_t seq, const uint8_t *d, int32_t n) {
     if (dir.empty()) {
-      chunks[seq].assign(d, d + n);
+      const std::pair<int64_t, int32_t> e{(int64_t)arena.size(), n};
+      arena.insert(arena.end(), d, d + n);
+      if (seq >= 0 && (size_t)seq < dense.size()) dense[(size_t)seq] = e;
+      else other[seq] = e;
       return true;
     }
     FILE *f = fopen(path(seq).c_str(), "wb");
     if (!f) return false;
     const bool ok = n == 0 || fwrite(d, 1, (size_t)n, f) == (size_t)n;
     fclose(f);
-    chunks[seq].clear(); // key only; bytes live in the file
+    files[seq] = true; // the bytes live in the file
     return ok;
   }
   bool get(int32_t seq, std::vector<uint8_t> &out) const {
-    auto it = chunks.find(seq);
-    if (it == chunks.end()) return false;
     if (dir.empty()) {
-      out = it->second;
+      std::pair<int64_t, int32_t> e{-1, 0};
+      if (seq >= 0 && (size_t)seq < dense.size()) e = dense[(size_t)seq];
+      else if (auto it = other.find(seq); it != other.end()) e = it->second;
+      if (e.first < 0) return false;
+      out.assign(arena.begin() + e.first, arena.begin() + e.first + e.second);
       return true;
     }
+    if (!files.count(seq)) return false;
+    {
     FILE *f = fopen(path(seq).c_str(), "rb");
     if (!f) return false;
     out.clear();
@@ -67,6 +84,7 @@ struct amod_assembler {
     while ((k = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + k);
     fclose(f);
     return true;
+    }
   }
   bool is_received(int64_t seq) const {
     if (!has_bitmap || seq < 0 || (seq >> 3) >= (int64_t)bitmap.size()) return false;
