@@ -840,7 +840,9 @@ struct Prepass {
       S_TRY(enqueue_pieces(0));
       full_started = true;
     }
+    const auto tq0 = std::chrono::steady_clock::now();
     S_TRY(hipStreamSynchronize(s));
+    const auto tq1 = std::chrono::steady_clock::now();
     fixed = (int64_t)fx;
     // fine ranges (local positions): every position within 448 samples of a hot block
     const int64_t pad = 448;
@@ -853,6 +855,11 @@ struct Prepass {
     };
     bool open = false;
     for (int64_t b = 0; b < nhot; ++b) {
+      if ((b & 7) == 0 && b + 8 <= nhot) { // eight quiet blocks at a time
+        uint64_t w8;
+        memcpy(&w8, hot + b, 8);
+        if (!w8) { b += 7; continue; }
+      }
       if (!hot[b]) continue;
       const int64_t za = 32 * b - pad, zb = 32 * b + 31 + pad;
       if (open && za <= rhi + 1) rhi = std::max(rhi, zb);
@@ -889,8 +896,14 @@ struct Prepass {
                                c->d_barg.as<double2>() + (int64_t)r0 * nbx, s));
       }
     }
+    const auto tq2 = std::chrono::steady_clock::now();
     S_TRY(hipEventRecord(ev[2], s));
     S_TRY(hipStreamSynchronize(s));
+    if (getenv("AMOD_STREAM_DIAG"))
+      fprintf(stderr, "[stream] prepass: wait for EMA+screen %.3f ms, fine ranges + launch %.3f ms, k_fine wait %.3f ms\n",
+              std::chrono::duration<double, std::milli>(tq1 - tq0).count(),
+              std::chrono::duration<double, std::milli>(tq2 - tq1).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq2).count());
     float ta = 0, tb = 0;
     S_TRY(hipEventElapsedTime(&ta, ev[0], ev[1]));
     S_TRY(hipEventElapsedTime(&tb, ev[1], ev[2]));
