@@ -24,6 +24,10 @@ constexpr int XT = 256;     // threads per workgroup
 constexpr int CH = 4096;    // sample chunk staged in LDS for the sequential lanes
 
 constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH doubles overlay the FFT arrays)
+#ifndef AMOD_SEG_G
+#define AMOD_SEG_G 1024
+#endif
+constexpr int kSegG = AMOD_SEG_G; // samples per certified segment of the mean (at least)
 
 struct alignas(16) XSmem {
   float chunk[CH + 520];
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_
       __syncthreads();
       XSTAMP(13);
       if (!exact_par) {
-        // Segments of G samples, certified one by one along the sequential order. A
+        // Segments of G >= kSegG samples, certified one by one along the sequential order. A
         // segment whose sum|x| < 2^(em + 53) (em: its smallest sample ulp exponent) has
         // exact internal sums in any order, so its total comes out exact from one thread's
         // running sum. With S the running (sequential) sum at its start and q the smaller
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_
         // L2-resident after the pass above): no cross-lane scans.
         constexpr int SEGCAP = SCH;
         double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_e = sm.sc + 2 * SEGCAP;
-        const int G = 256 * max(1, (N + 256 * SEGCAP - 1) / (256 * SEGCAP));
+        const int G = kSegG * max(1, (N + kSegG * SEGCAP - 1) / (kSegG * SEGCAP));
         const int nseg = (N + G - 1) / G;
         for (int sg = tid; sg < nseg; sg += XT) {
           const int b0 = sg * G, e1 = min(N, b0 + G);
