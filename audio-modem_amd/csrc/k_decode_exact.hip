@@ -363,8 +363,15 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_
         }
         __syncthreads();
         mx = sm.mx;
-        if (mx > 1e-6) stream4(xr, N, [&](int i, float x) { xs[i] = (float)((double)(float)((double)x - mean) / mx); });
-        else stream4(xr, N, [&](int i, float x) { xs[i] = (float)((double)x - mean); });
+        // a replayed detection reads the normalised samples only up to its fine window
+        // (the recurrence stops at the proven hull's end; k_demod reads the raw samples)
+        int nn = N;
+        if (replay) {
+          const DetRec dr = w.det[f];
+          if (dr.sc_lo >= 0 && dr.sc_hi >= dr.sc_lo) nn = (int)min<int64_t>(N, (int64_t)dr.sc_hi + kFft + 3 * CP + SYM + 1);
+        }
+        if (mx > 1e-6) stream4(xr, nn, [&](int i, float x) { xs[i] = (float)((double)(float)((double)x - mean) / mx); });
+        else stream4(xr, nn, [&](int i, float x) { xs[i] = (float)((double)x - mean); });
       } else { // NaN / Inf: Math.max's NaN propagation over every sample, then the division
         stream4(xr, N, [&](int i, float x) {
           const float o = (float)((double)x - mean);
