@@ -249,12 +249,15 @@ def main():
             dom_bytes = 4.0 * 512 * (nsym_dec + 1) * F
         achieved = dom_bytes / (stage_ms[dom] / 1e3) / 1e9
         traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        # HBM bytes per launch of the dominant kernel from the committed PMC pass
+        # (FETCH_SIZE x 2 + WRITE_SIZE, tools/traffic.py) when it was taken on this workload
+        tf = os.path.join(ROOT, "profiles", "r02", "traffic.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
-            if tj.get("frames") == F and tj.get("samples_per_frame") == spf:
-                traffic = tj.get("hbm_bytes_per_launch")
+            kt = tj.get("kernels", {}).get(names[dom])
+            if tj.get("frames") == F and tj.get("samples_per_frame") == spf and kt:
+                traffic = (kt["read_bytes"] + kt["write_bytes"]) / kt.get("dispatches_per_step", 1.0)
         mod = "QAM16" if C3 else ("BPSK" if C5 else "QPSK")
         name = "C3" if C3 else ("C4" if C4 else ("C5" if C5 else "C2"))
         cpu, tx_cpu, d2h = None, None, None
