@@ -38,7 +38,8 @@ def main():
         for name, (rt, args) in L.SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = rt, args
-        for stop in (("99", "1") if os.environ.get("AB_SCAN") else ("99",)):
+        stops = os.environ.get("AB_STOPS") or ("99,1" if os.environ.get("AB_SCAN") else "99")
+        for stop in stops.split(","):  # 99 whole chain, 2 detection only, 1 scan only
             os.environ["AMOD_STOP_AFTER"] = stop
             h = C.c_void_p()
             L.check(lib.amod_open(0, C.byref(h)))
@@ -51,7 +52,7 @@ def main():
             if stop == "99":
                 rec = np.frombuffer(res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
                 assert ((rec["status"] == 0) & (rec["crc_valid"] == 1)).all(), path
-            runs.append((os.path.basename(os.path.dirname(path)) + ("/full" if stop == "99" else "/scan"), lib, h, run))
+            runs.append((os.path.basename(os.path.dirname(path)) + {"99": "/full", "2": "/detect", "1": "/scan"}.get(stop, "/" + stop), lib, h, run))
     os.environ.pop("AMOD_STOP_AFTER", None)
     times = {name: [] for name, *_ in runs}
     for _ in range(3):  # warm-up
