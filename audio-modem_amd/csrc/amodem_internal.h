@@ -466,9 +466,10 @@ hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::DevWork &w, h
 hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s);
 int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds);
 void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_words, int *vote_off);
-hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s);
+hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s,
+                             bool beside_demod = false); // list A runs beside k_demod
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
-int amod_fast_lds_bytes(int nb_cap, int fine_cap); // dynamic LDS of one k_detect workgroup
+int amod_fast_lds_bytes(int nb_cap, int fine_cap, int sym); // dynamic LDS of one k_detect workgroup
 // streaming receiver pieces (k_stream.hip)
 int64_t amod_ema_chunk();
 hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,

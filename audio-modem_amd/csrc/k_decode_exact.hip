@@ -183,7 +183,11 @@ __device__ int crosscorr_detect(const float *xs, int N, const DevCfg &cfg, XSmem
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_decode_exact(const DevCfg cfg, const DevWork w) {
+// WPE 3: list A's instance, capped at 168 VGPRs so its waves fit beside k_demod (45 VGPRs
+// spill to scratch); WPE 2: list B's, which runs alone after k_demod (222 VGPRs, no
+// scratch: its launch skips the scratch setup even when the list is empty)
+template <int WPE>
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_decode_exact(const DevCfg cfg, const DevWork w) {
   __shared__ XSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // listed frames are latency-bound chains (sequential recurrences) that run beside the
@@ -730,8 +734,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(3))) void k_
 } // namespace
 } // namespace amod
 
-extern "C" hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s) {
+extern "C" hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s,
+                                        bool beside_demod) {
   if (nslots <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_decode_exact, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
+  if (beside_demod)
+    hipLaunchKernelGGL(amod::k_decode_exact<3>, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
+  else
+    hipLaunchKernelGGL(amod::k_decode_exact<2>, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
   return hipGetLastError();
 }

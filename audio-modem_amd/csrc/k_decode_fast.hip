@@ -48,7 +48,8 @@ constexpr int FIRST_SYMS = AMOD_FIRST_SYMS;  // data symbols always decoded (the
 #endif
 constexpr int SB = AMOD_SB;                  // stream pass: chunks per load batch
 #ifndef AMOD_WPE
-#define AMOD_WPE 6                           // waves per SIMD the register budget is sized for
+#define AMOD_WPE 7                           // waves per SIMD the register budget is sized for (72 VGPRs;
+                                             // C2's LDS fits 7 workgroups per CU: 0.277 -> 0.273 ms)
 #endif
 #ifndef AMOD_SCAN_WPE
 #define AMOD_SCAN_WPE 5                      // k_corr_scan (the scan phase alone)
@@ -62,18 +63,22 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 // by the stages, addressed by float / float2 / word index.
 //   stages 0-1: s1[nbc] s2[nbc] sx[nbc] (block moments -> caps / E_b / Z_b), cand[256] (int16),
 //               cmax[256], pass-1 cache[SC_CACHE][32] (float2: top metric, uncertainty bits)
-//   stage 2   : tmpl[768] m[FC + 8] yw[FC + 800] q[FC + 280] (folded window) E[FC + 800]
-//               (prefix of squares of yw); FC = the launch's fine-search capacity
+//   stage 2   : tmpl[T] m[FC + 8] yw[FC + Y] q[FC + 280] (folded window) E[FC + Y] (prefix of
+//               squares of yw); FC = the launch's fine-search capacity, T = SYM rounded to 8,
+//               Y = max(SYM + 24, 528): the staged span P + SYM + 16 and the fold's reads to
+//               qn + 256 (sized from the preset's symbol length: C2's workgroup fits 7 per CU)
 extern __shared__ __attribute__((aligned(16))) unsigned char amod_dyn[];
 #define LDS_F (reinterpret_cast<float *>(amod_dyn))
 #define LDS_F2 (reinterpret_cast<float2 *>(amod_dyn))
 #define LDS_U (reinterpret_cast<uint32_t *>(amod_dyn))
 #define LDS_I16 (reinterpret_cast<int16_t *>(amod_dyn))
-__host__ __device__ constexpr int fine_m(int) { return 768; }
-__host__ __device__ constexpr int fine_yw(int fc) { return 768 + fc + 8; }
-__host__ __device__ constexpr int fine_q(int fc) { return fine_yw(fc) + fc + 800; }
-__host__ __device__ constexpr int fine_e(int fc) { return fine_q(fc) + fc + 280; }
-__host__ __device__ constexpr int fine_floats(int fc) { return fine_e(fc) + fc + 800; }
+__host__ __device__ constexpr int fine_t(int sym) { return (sym + 7) & ~7; }
+__host__ __device__ constexpr int fine_y(int sym) { return ((sym + 24 > 528 ? sym + 24 : 528) + 7) & ~7; }
+__host__ __device__ constexpr int fine_m(int, int sym) { return fine_t(sym); }
+__host__ __device__ constexpr int fine_yw(int fc, int sym) { return fine_t(sym) + fc + 8; }
+__host__ __device__ constexpr int fine_q(int fc, int sym) { return fine_yw(fc, sym) + fc + fine_y(sym); }
+__host__ __device__ constexpr int fine_e(int fc, int sym) { return fine_q(fc, sym) + fc + 280; }
+__host__ __device__ constexpr int fine_floats(int fc, int sym) { return fine_e(fc, sym) + fc + fine_y(sym); }
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct Smem {  // fixed part (static LDS)
@@ -930,7 +935,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
       FRESH_ARGS;
       const int FC = w.fine_cap; // positions the launch's LDS holds (>= 12 CP + 1: every window the
                                  // coarse stage lets through)
-      const int FM = fine_m(FC), FYW = fine_yw(FC), FQ = fine_q(FC), FE = fine_e(FC);
+      const int FM = fine_m(FC, SYM), FYW = fine_yw(FC, SYM), FQ = fine_q(FC, SYM), FE = fine_e(FC, SYM);
       const float A = sm.A, B = sm.B;
       const int R = 3 * CP;
       const int c_lo = sm.clo, c_hi = sm.chi;
@@ -1869,10 +1874,10 @@ __host__ demod_fn demod_kernel(const DevCfg &cfg, bool dbg) {
 // ------------------------------------------------------------ launchers
 // dynamic LDS bytes of a k_detect workgroup with nb_cap moment blocks and fine_cap
 // fine-search positions
-extern "C" int amod_fast_lds_bytes(int nb_cap, int fine_cap) {
+extern "C" int amod_fast_lds_bytes(int nb_cap, int fine_cap, int sym) {
   using namespace amod;
   const int mom = 12 * nb_cap + 2 * SC_MAXCAND + 4 * SC_MAXCAND + 8 * 32 * SC_CACHE;
-  const int fine = 4 * fine_floats(fine_cap);
+  const int fine = 4 * fine_floats(fine_cap, sym);
   return (std::max(mom, fine) + 15) & ~15;
 }
 // per-wave bit-stream words of k_demod (stream, then the voted stream when rep > 1)
@@ -1892,7 +1897,7 @@ extern "C" hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::De
     return hipGetLastError();
   }
   auto *k = w.dbg ? amod::k_detect_dbg : (cfg.stop_after == 1 ? amod::k_corr_scan : amod::k_detect);
-  hipLaunchKernelGGL(k, dim3(n), dim3(amod::WG), (unsigned)amod_fast_lds_bytes(w.nb_cap, w.fine_cap), s, cfg, w);
+  hipLaunchKernelGGL(k, dim3(n), dim3(amod::WG), (unsigned)amod_fast_lds_bytes(w.nb_cap, w.fine_cap, cfg.sym), s, cfg, w);
   return hipGetLastError();
 }
 extern "C" hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s) {

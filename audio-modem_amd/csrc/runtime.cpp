@@ -563,7 +563,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     amod::DevWork wa = w;
     wa.f0 = 0; wa.f1 = nframes;
     if (replay) { wa.rp_count = fb + 2; wa.rp_list = fb + 64 + 4 * nframes; }
-    HIP_TRY(amod_launch_exact(d, wa, xslots, st));
+    HIP_TRY(amod_launch_exact(d, wa, xslots, st, true));
     if (replay) {
       amod::DevWork wc = wb; // its guards list into B
       wc.f0 = 0; wc.f1 = nframes;
