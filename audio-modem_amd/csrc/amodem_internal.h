@@ -130,6 +130,10 @@ struct DevWork {
   // exact kernel's waves (0: the whole grid)
   const int32_t *yield_count;
   int32_t yield_blocks;
+  // exact kernel, list B (the step's last launch): workgroup 0 zeroes fb_reset[0..31], the
+  // counter set the previous decode used (decodes alternate between two sets of 32), so
+  // the next decode needs no memset dispatch (null: no reset)
+  int32_t *fb_reset;
 };
 
 // k_gap_scan -> streaming receiver: the scan that follows the frame of fine range r, run

@@ -194,6 +194,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // throughput-bound k_demod: their waves issue first on a shared SIMD
   __builtin_amdgcn_s_setprio(3);
   const int count = *w.fb_count;
+  if (w.fb_reset && blockIdx.x == 0 && tid < 32) w.fb_reset[tid] = 0; // the other counter set
   const int SYM = cfg.sym, CP = cfg.cp;
   for (int item = blockIdx.x; item < count; item += gridDim.x) {
     const int f = w.fb_list[item];

@@ -240,6 +240,11 @@ struct amod_ctx {
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
   int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0;
+  // fb[0..63] holds two counter sets of 32; a decode uses set fb_parity and its list-B
+  // launch zeroes the other (fb_reset). fb_zeroed: both sets are zero when this decode's
+  // launches run; a reallocation or an aborted launch sequence clears it (memset)
+  bool fb_zeroed = false;
+  int fb_parity = 0;
   void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
   void (*ext_free[4])(void *) = {nullptr, nullptr, nullptr, nullptr};
   int64_t soft_stride = 0;
@@ -432,15 +437,23 @@ int ensure_chain(amod_ctx *ctx, int32_t nframes) {
   return AMOD_SUCCESS;
 }
 
+// exact-list counters + lists for nframes frames (grow-only; a new buffer is not zeroed)
+static hipError_t fb_grow(amod_ctx *ctx, int32_t nframes) {
+  const size_t bytes = sizeof(int32_t) * (size_t)(64 + 5 * (size_t)std::max(nframes, 1));
+  if (bytes <= ctx->fb.n) return hipSuccess;
+  ctx->fb_zeroed = false;
+  return ctx->fb.ensure(bytes);
+}
+
 int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
   if (max_len < 0) { // device path: keep what amod_reserve set up, or size from a default
-    HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 5 * (size_t)std::max(nframes, 1))));
+    HIP_TRY(fb_grow(ctx, nframes));
     if (ctx->nslots > 0) return AMOD_SUCCESS;
     max_len = 65536;
   }
   const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
       std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
-  HIP_TRY(ctx->fb.ensure(sizeof(int32_t) * (size_t)(64 + 5 * (size_t)std::max(nframes, 1))));
+  HIP_TRY(fb_grow(ctx, nframes));
   // grow-only: a later, smaller reservation never shrinks a stride or the slot count that
   // earlier (longer) frames were sized for
   const int64_t words = (max_bits_for(c, max_len) + 31) / 32;
@@ -480,10 +493,11 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   amod::DevWork w{};
   w.samples = samples; w.off = offsets; w.len = lengths; w.nframes = nframes;
   w.res = results; w.payload = payload; w.stride = payload_stride; w.dbg = debug;
-  int32_t *fb = (int32_t *)ctx->fb.p;
+  int32_t *const fb_base = (int32_t *)ctx->fb.p;
+  int32_t *fb = fb_base + 32 * ctx->fb_parity; // this decode's counter set; lists from fb_base + 64
   // exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod;
   // list C (fb[2]): frames whose detection the exact kernel replayed, for k_demod
-  w.fb_count = fb; w.fb_list = fb + 64; w.fb_flags = fb + 64 + nframes;
+  w.fb_count = fb; w.fb_list = fb_base + 64; w.fb_flags = fb_base + 64 + nframes;
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
@@ -517,7 +531,8 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.stamps = (unsigned long long *)ctx->stamps.p;
     ctx->nstamps = nframes;
   }
-  HIP_TRY(hipMemsetAsync(fb, 0, 256, s)); // exact-list and job counters
+  if (!ctx->fb_zeroed) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // both counter sets
+  ctx->fb_zeroed = false; // until this decode's list-B launch is enqueued with its reset
   std::array<hipEvent_t, 4> ev{};
   if (ctx->profiling) {
     if (ctx->ev_free.empty()) {
@@ -547,7 +562,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (!demod || debug) nchunk = 1;
   nchunk = std::min(nchunk, std::max(1, nframes));
   amod::DevWork wb = w; // every field as w, list B
-  wb.fb_count = fb + 1; wb.fb_list = fb + 64 + 2 * nframes; wb.fb_flags = fb + 64 + 3 * nframes;
+  wb.fb_count = fb + 1; wb.fb_list = fb_base + 64 + 2 * nframes; wb.fb_flags = fb_base + 64 + 3 * nframes;
   if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   for (auto &e : ctx->chunk_ev)
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -562,12 +577,12 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   auto exact_a = [&](hipStream_t st) -> int {
     amod::DevWork wa = w;
     wa.f0 = 0; wa.f1 = nframes;
-    if (replay) { wa.rp_count = fb + 2; wa.rp_list = fb + 64 + 4 * nframes; }
+    if (replay) { wa.rp_count = fb + 2; wa.rp_list = fb_base + 64 + 4 * nframes; }
     HIP_TRY(amod_launch_exact(d, wa, xslots, st, true));
     if (replay) {
       amod::DevWork wc = wb; // its guards list into B
       wc.f0 = 0; wc.f1 = nframes;
-      wc.dm_count = fb + 2; wc.dm_list = fb + 64 + 4 * nframes;
+      wc.dm_count = fb + 2; wc.dm_list = fb_base + 64 + 4 * nframes;
       HIP_TRY(amod_launch_demod(d, wc, std::min(demod_blocks(nframes), std::max(1, ctx->cu_count)), st));
     }
     return AMOD_SUCCESS;
@@ -626,7 +641,10 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(2));
+  wb.fb_reset = fb_base + 32 * (1 - ctx->fb_parity); // zeroed for the next decode
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
+  ctx->fb_zeroed = xslots > 0;
+  ctx->fb_parity ^= 1;
   HIP_TRY(mark(3));
   if (ctx->profiling) ctx->ev_used.push_back(ev);
   return AMOD_SUCCESS;
