@@ -160,3 +160,31 @@ def test_replayed_detection_equals_full_exact_path(preset, snr_db):
         pv = int(rec["payload_valid"][i])
         assert pay[i][:pv].tobytes() == rpay[i][:pv].tobytes(), i
     _check_against_oracle(preset, "BPSK", 3, x, offs, lens, rec, pay)
+
+
+def test_listed_frames_across_consecutive_decodes():
+    """The exact-list counters alternate between two sets from one decode to the next
+    (each decode's list-B launch zeroes the set the previous one used, instead of a
+    memset): repeated decodes on one context, with many frames listed and with batches
+    of other sizes, forced-exact decodes and a buffer reallocation in between, return
+    the same records every time, equal to the oracle's."""
+    cfg, x, offs, lens = _noisy_batch("acoustic", "BPSK", 3, 48, 64, 6, seed=11)
+    dm = _wide_guard_demodulator(cfg, x, offs, lens)
+    first, fpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    assert ((first["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY)) != 0).sum() > 0
+    _check_against_oracle("acoustic", "BPSK", 3, x, offs, lens, first, fpay)
+    big_offs = np.concatenate([offs, offs, offs, offs])
+    big_lens = np.concatenate([lens, lens, lens, lens])
+    for k in range(6):
+        if k == 1:
+            dm.decode_batch(x, offs[:5], lens[:5], cfg=cfg)
+        if k == 2:
+            dm.decode_batch(x, offs, lens, cfg=cfg, options=L.OPT_FORCE_EXACT)
+        if k == 3:  # more frames than before: the counter and list buffer grows
+            big, _ = dm.decode_batch(x, big_offs, big_lens, cfg=cfg)
+            for n in ("status", "preamble_idx", "nbytes", "crc_valid", "flags"):
+                assert (big[n] == np.concatenate([first[n]] * 4)).all(), n
+        rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
+        assert rec.tobytes() == first.tobytes(), k
+        assert (pay == fpay).all(), k
+    dm.close()
