@@ -245,6 +245,8 @@ struct amod_ctx {
   // launches run; a reallocation or an aborted launch sequence clears it (memset)
   bool fb_zeroed = false;
   int fb_parity = 0;
+  bool fb_captured = false; // a decode was captured into a hipGraph: its replays memset and
+                            // dirty the counters unseen by the host, so every decode memsets
   void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
   void (*ext_free[4])(void *) = {nullptr, nullptr, nullptr, nullptr};
   int64_t soft_stride = 0;
@@ -531,7 +533,10 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.stamps = (unsigned long long *)ctx->stamps.p;
     ctx->nstamps = nframes;
   }
-  if (!ctx->fb_zeroed) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // both counter sets
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) ctx->fb_captured = true;
+  if (!ctx->fb_zeroed || ctx->fb_captured) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // both counter sets
   ctx->fb_zeroed = false; // until this decode's list-B launch is enqueued with its reset
   std::array<hipEvent_t, 4> ev{};
   if (ctx->profiling) {
@@ -641,10 +646,10 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(2));
-  wb.fb_reset = fb_base + 32 * (1 - ctx->fb_parity); // zeroed for the next decode
+  wb.fb_reset = ctx->fb_captured ? nullptr : fb_base + 32 * (1 - ctx->fb_parity); // zeroed for the next decode
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
-  ctx->fb_zeroed = xslots > 0;
-  ctx->fb_parity ^= 1;
+  ctx->fb_zeroed = xslots > 0 && !ctx->fb_captured;
+  if (!ctx->fb_captured) ctx->fb_parity ^= 1;
   HIP_TRY(mark(3));
   if (ctx->profiling) ctx->ev_used.push_back(ev);
   return AMOD_SUCCESS;

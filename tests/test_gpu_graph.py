@@ -1,0 +1,72 @@
+"""amod_decode_device captured into a hipGraph (include/amodem.h: amod_reserve, then
+capture) and replayed: every replay, and an eager decode after the replays, returns the
+eager decode's records and payload. Frames are listed for the exact kernel (wide guard
+bands), so the exact-list counters — zeroed by a memset inside a captured decode, by
+the previous decode's list-B launch otherwise — are exercised across replays."""
+import os
+
+import numpy as np
+import pytest
+
+import amodem
+from amodem import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def test_captured_decode_replays_equal_eager():
+    import torch
+    cfg = amodem.preset("acoustic", "BPSK", 3)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, 32, payload_len=64, threads=8)
+    sp = float(np.mean(x[x != 0] ** 2))
+    rng = np.random.default_rng(5)
+    x = (x + rng.standard_normal(len(x)).astype(np.float32) * np.float32(np.sqrt(sp / 10 ** 0.6))).astype(np.float32)
+    F, N = len(offs), int(lens.max())
+    dev = torch.device("cuda", 0)
+    xs = torch.zeros(len(x) + 16, dtype=torch.float32, device=dev)
+    xs[:len(x)].copy_(torch.from_numpy(x))
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    stride = amodem.payload_stride(cfg, N)
+    res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
+    pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
+
+    dm = amodem.Demodulator(0)
+    os.environ["AMOD_GUARD_SCALE"] = "50"  # read when the context builds cfg's tables
+    try:
+        dm.reserve(cfg, F, N)
+        s = torch.cuda.Stream()
+
+        def decode():
+            dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
+                             res.data_ptr(), pay.data_ptr(), stride, stream=torch.cuda.current_stream().cuda_stream)
+
+        with torch.cuda.stream(s):
+            decode()
+            decode()
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["AMOD_GUARD_SCALE"]
+    ref_res, ref_pay = res.cpu().numpy().copy(), pay.cpu().numpy().copy()
+    rec = np.frombuffer(ref_res.tobytes(), amodem.RESULT_DTYPE)
+    assert ((rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY)) != 0).sum() > 0, np.unique(rec["flags"])
+
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        decode()
+    torch.cuda.synchronize()
+    for k in range(4):
+        res.zero_()
+        pay.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(res.cpu().numpy(), ref_res), k
+        assert np.array_equal(pay.cpu().numpy(), ref_pay), k
+    res.zero_()
+    with torch.cuda.stream(s):
+        decode()
+    torch.cuda.synchronize()
+    assert np.array_equal(res.cpu().numpy(), ref_res)
+    assert np.array_equal(pay.cpu().numpy(), ref_pay)
+    del g
+    dm.close()
