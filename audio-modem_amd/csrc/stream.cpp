@@ -1389,7 +1389,11 @@ extern "C" int amod_live_open(amod_ctx *ctx, const amod_cfg *cfg, amod_assembler
   rx.ring = lv->ring.data();
   rx.tw_live = 0;
   rx.pre1.resize(cfg->symbol_len);
-  amod_preamble1(cfg, rx.pre1.data());
+  if (amod_preamble1(cfg, rx.pre1.data()) != AMOD_SUCCESS) {
+    if (lv->own_assembler) amod_asm_close(lv->assembler);
+    delete lv;
+    return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
+  }
   for (float v : rx.pre1) rx.pre1_energy += (double)v * (double)v;
   rx.fails = &lv->fails;
   amod_asm_info inf;
