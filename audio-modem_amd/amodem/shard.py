@@ -278,8 +278,10 @@ def stream_receive_sharded(dm, cfg, samples_for, n: int, rank: int, world: int, 
                             f"the rest re-run from there on rank 0")
                 own = st.block * BLOCK
                 lo2 = max(0, (own - EMA_WARM) // EMA_CHUNK * EMA_CHUNK)
-                # (payload rows as wide as the longest window: dispatch feeds them one by one)
-                ev2, pay2, fl2, _, _ = dm.stream_shard(cfg, samples_for(lo2, npad), lo2, npad, own, npad, start=st)
+                # (payload rows as wide as the longest window the new chunk size cuts:
+                # dispatch feeds them one by one)
+                ev2, pay2, fl2, _, _ = dm.stream_shard(cfg, samples_for(lo2, npad), lo2, npad, own, npad, start=st,
+                                                       chunk_size=int(new_chunk) if new_meta else 0)
                 fails = [f for f in fails if f[0] < st.block] + [f for f in fl2 if f[0] >= st.block]
                 traj = traj[: i + 1] + list(zip(ev2, pay2))
                 meta, chunk_now = new_meta, new_chunk

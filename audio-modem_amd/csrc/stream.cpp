@@ -1281,6 +1281,10 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
   }
   if (!start) { st.meta_received = meta_received != 0; st.chunk_size = chunk_size; }
   const int64_t stop = hi / kBlock;
+  // a window whose decoded bytes do not fit the caller's rows is an error, never a cut row
+  auto row_too_narrow = [&] {
+    return amod_ctx_fail(ctx, "payload stride too small for a decoded window (pass the chunk size)", AMOD_ERR_ARG);
+  };
   Traj tr;
   int64_t fine_host = 0;
   WindowDecoder wd;
@@ -1299,6 +1303,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       apply_meta(wd.res[0], t1.frames[0].after);
       tr.frames.push_back(t1.frames[0]);
       res.push_back(wd.res[0]);
+      if (wd.res[0].payload_valid > stride) return row_too_narrow();
       pay.insert(pay.end(), wd.row(0), wd.row(0) + std::min<int64_t>(wd.stride, stride));
       if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
       st = t1.frames[0].after;
@@ -1323,6 +1328,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       res.insert(res.end(), wd.res.begin(), wd.res.end());
       for (size_t i = c0; i < c1; ++i) { // rows at the caller's stride
         const uint8_t *row = wd.row(i - c0);
+        if (wd.res[i - c0].payload_valid > stride) return row_too_narrow();
         pay.insert(pay.end(), row, row + std::min<int64_t>(wd.stride, stride));
         if (wd.stride < stride) pay.insert(pay.end(), (size_t)(stride - wd.stride), 0);
       }
