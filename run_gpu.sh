@@ -6,10 +6,10 @@ for s in "$@"; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider;;
-    bench) run bench 600 python bench.py --steps 20 --warmup 3;;
+    bench) run bench 900 python bench.py --steps 20 --warmup 3;;
     benchc3) run bench_c3 600 python bench.py --config c3 --steps 10 --warmup 2;;
-    bench2g) run bench2g 600 env AMOD_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0 &&
-            run bench2g_c4 600 env AMOD_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config c4 --frames 4000 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0;;
+    bench2g) run bench2g 600 env AMOD_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0 --no-e2e --legs c4,c5;;
+    bench2fail) echo "== bench2fail"; timeout -k 10 300 python bench.py --gpus 2 > gpurun_out/bench2fail.log 2>&1; echo "rc=$? (2 expected)"; tail -2 gpurun_out/bench2fail.log;;
     benchc4) run bench_c4 600 python bench.py --config c4 --steps 10 --warmup 2 --stream-chunks 0;;
     stamps) run stamps 300 python tools/stamps.py;;
     stages) run stages 600 env STAGES=${STAGES:-0,1,2,3,99} python tools/stage_profile.py;;

@@ -1,0 +1,50 @@
+#!/usr/bin/env node
+// The Node.js host path of the drop-in (bench.py host_api leg): decodeBatch from the JS
+// surface (audio-modem_amd/js/modem.js, N-API -> amod_decode_host), as app.js's callers
+// (app.js:513, 928) would drive the engine with a whole batch, timed end to end (host
+// Float32Array in, reference-shaped result objects out), and the native call alone.
+// Usage: node tools/node_decode_batch.js <spec.json>
+// spec: {samples: <float32 file>, offsets, lengths, preset, mod, rep, chunk, reps, device}
+'use strict';
+const fs = require('fs');
+const path = require('path');
+const modem = require(path.join(__dirname, '..', 'audio-modem_amd', 'js', 'modem.js'));
+
+async function main() {
+  const spec = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+  const buf = fs.readFileSync(spec.samples);
+  const x = new Float32Array(buf.buffer, buf.byteOffset, buf.length >> 2);
+  const offs = Float64Array.from(spec.offsets), lens = Int32Array.from(spec.lengths);
+  modem.setOFDMConfig(spec.preset);
+  const opts = { device: spec.device | 0, devices: 1, mode: spec.chunk ? 'chunk' : 'received' };
+  const reps = spec.reps || 3;
+  const med = (a) => a.slice().sort((p, q) => p - q)[a.length >> 1];
+  const whole = [], nat = [];
+  let res = null;
+  for (let r = 0; r <= reps; r++) {
+    const t0 = process.hrtime.bigint();
+    res = await modem.decodeBatch(x, offs, lens, spec.mod, spec.rep, opts);
+    const t1 = process.hrtime.bigint();
+    if (r) whole.push(Number(t1 - t0) / 1e6);
+  }
+  // the N-API call alone (records + payload ArrayBuffers, no per-frame result objects)
+  const cfg = {
+    fft_size: 512, cp_len: modem.OFDM.CP_LEN, symbol_len: modem.OFDM.SYMBOL_LEN, sample_rate: 44100,
+    sub_start: modem.OFDM.SUB_START, sub_end: modem.OFDM.SUB_END, pilots: modem.OFDM.PILOTS.slice(),
+    modulation: { BPSK: 0, QPSK: 1, QAM16: 2 }[spec.mod], repetition: spec.rep,
+  };
+  for (let r = 0; r <= reps; r++) {
+    const t0 = process.hrtime.bigint();
+    await modem.native.decodeAsync(x, offs, lens, cfg, spec.chunk ? 1 : 0, 0, spec.device | 0, 1);
+    const t1 = process.hrtime.bigint();
+    if (r) nat.push(Number(t1 - t0) / 1e6);
+  }
+  const ok = res.filter((r) => r.crcValid === true).length;
+  process.stdout.write(JSON.stringify({
+    what: `decodeBatch(${lens.length} frames) from node ${process.version}: host Float32Array -> N-API -> ` +
+      'amod_decode_host -> result objects, median of ' + reps,
+    ms: med(whole), native_call_ms: med(nat), frames: lens.length, frames_crc_valid: ok,
+  }));
+}
+
+main().catch((e) => { process.stderr.write(String(e && e.stack || e)); process.exit(1); });
