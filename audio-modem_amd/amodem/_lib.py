@@ -23,6 +23,8 @@ OPT_SOFT_COMBINE = 2  # not reference behaviour: soft repetition combining (opt-
 
 OK = 0
 E_CAPACITY = 100
+# amod_kernel_stages slots
+STAGE_DETECT, STAGE_DEMOD, STAGE_EXACT_B, STAGE_AUX, STAGE_JOIN_WAIT, STAGE_DEMOD_PATH, STAGE_COUNT = range(7)
 FLAG_SPAN = 1 << 9
 FLAG_SOFT = 1 << 10
 FLAG_REPLAY = 1 << 11
@@ -116,6 +118,7 @@ SIGNATURES = {
     "amod_synchronize": (C.c_int, [_P]),
     "amod_set_profiling": (C.c_int, [_P, C.c_int]),
     "amod_kernel_breakdown": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "amod_kernel_stages": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int64)]),
     "amod_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int64)]),
     "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,

@@ -42,6 +42,8 @@ struct DevTables {
   const uint32_t *crc_m2;  // [32][4][256] shift-by-(512*q) operators, q<32
   const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
   const uint32_t *crc_mat; // [kCrcMats][32] shift-by-(16*q) zero-byte operators as GF(2) matrices (column i = image of bit i)
+  const uint32_t *crc_pre; // [16] register k zero bytes before the message start that becomes ~0 there
+                           // (the inverse k-byte shift of ~0): chunk 0 left-padded to 16 bytes
   const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
   const double2 *tw_inv;   // [511] inverse-transform recurrence twiddles (fftIterative, ifft)
   const float *tmpl;       // [3][symbol_len] pre1, pre2, CE symbols (f32, before normalisation)

@@ -77,6 +77,9 @@ extern "C" int amod_group_decode_host(amod_group *g, const amod_cfg *cfg, int32_
     th.emplace_back([&, k, a, b] {
       int64_t lo = INT64_MAX, hi = 0;
       for (int32_t i = a; i < b; ++i) { lo = std::min(lo, offsets[i]); hi = std::max(hi, offsets[i] + lengths[i]); }
+      // keep every frame's offset mod 4: the fast path's block moments sit on 16-byte
+      // boundaries of the buffer, so its approximate coarse_idx follows the alignment
+      lo &= ~int64_t(3);
       std::vector<int64_t> loc((size_t)(b - a));
       for (int32_t i = a; i < b; ++i) loc[(size_t)(i - a)] = offsets[i] - lo;
       rc[(size_t)k] = amod_decode_host(g->ctx[(size_t)k], cfg, mode, samples + lo, hi - lo, loc.data(), lengths + a,

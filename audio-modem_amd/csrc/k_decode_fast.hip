@@ -1260,27 +1260,23 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
 // the exact kernel instead.
 
 // Wave-level CRC-32 (modem.js:443-457) of bytes [0, L) of stream v. The message is cut
-// into 16-byte chunks, right-aligned (chunk 0 may be short); every chunk's register is
-// computed independently with slice-by-4 tables (chunk 0 from the initial ~0, the others
-// from 0), moved to the message end by the GF(2) matrix of its zero-byte shift, and the
-// images are XOR-combined (CRC linearity). Lane l takes chunks l, l + 64, ... (ILP across
-// them), so one pass covers up to kCrcMats chunks; longer messages carry the register
-// into the next block.
-// bytes i .. i + 3 of an MSB-first stream as one little-endian word (CRC byte order)
-__device__ __forceinline__ uint32_t le_word_at(const uint32_t *v, int i) {
+// into 16-byte chunks, right-aligned; chunk 0 is left-padded with zero bytes to a whole
+// chunk and starts from t.crc_pre[pad] (the register that the pad's zero bytes advance to
+// the reference's initial ~0), every other chunk from 0. Each chunk's register comes from
+// slice-by-4 lookups in a copy of the table in LDS (t4l: 4 KB, the wave's exchange buffer,
+// free at the frame end), is moved to the message end by the GF(2) matrix of its
+// zero-byte shift and the images are XOR-combined (CRC linearity). Lane l takes chunks
+// whose distance to the end is l, l + 64, ..., CRC_ILP of them interleaved, so the
+// dependent lookups of different chunks overlap; the whole message is one pass (the
+// frame-end CRC was a chain of global-memory lookups: 13.5k cycles per C2 frame, 24.7k per
+// C4 window, tools/demod_profile.py).
+// bytes i .. i + 3 of an MSB-first stream as one little-endian word (CRC byte order);
+// bytes before the stream start (i >= -15) read as zero
+__device__ __forceinline__ uint32_t le_word_pad(const uint32_t *v, int i) {
   const int wi = i >> 2, sh = 8 * (i & 3);
-  const uint32_t lo = v[wi];
-  return __builtin_bswap32(sh ? (lo << sh) | (v[wi + 1] >> (32 - sh)) : lo);
-}
-// CRC register over bytes [beg, end) from c; t4 = the slice-by-4 tables
-__device__ __forceinline__ uint32_t crc_chunk(const uint32_t *v, int beg, int end, uint32_t c, const uint32_t *t4) {
-  int i = beg;
-  for (; i + 4 <= end; i += 4) {
-    c ^= le_word_at(v, i);
-    c = t4[768 + (c & 0xFF)] ^ t4[512 + ((c >> 8) & 0xFF)] ^ t4[256 + ((c >> 16) & 0xFF)] ^ t4[c >> 24];
-  }
-  for (; i < end; ++i) c = t4[(c ^ stream_byte(v, i)) & 0xFF] ^ (c >> 8);
-  return c;
+  const uint32_t lo = wi >= 0 ? v[max(wi, 0)] : 0u;
+  const uint32_t hi = wi >= -1 ? v[max(wi + 1, 0)] : 0u;
+  return __builtin_bswap32(sh ? (lo << sh) | (hi >> (32 - sh)) : lo);
 }
 __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32_t c) {
   const uint4 *const mq = reinterpret_cast<const uint4 *>(mat + 32 * q);
@@ -1295,8 +1291,56 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   }
   return r;
 }
-__device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4) {
+constexpr int CRC_ILP = 4;
+__device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *t4l) {
   const int lane = wave_lane();
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(t.crc_s4);
+    uint4 *dst = reinterpret_cast<uint4 *>(t4l);
+    uint4 a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = src[lane + 64 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[lane + 64 * k] = a[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const uint32_t *const t4 = t4l;
+  const int nch = (L + kCrcChunk - 1) / kCrcChunk;
+  const uint32_t r0 = t.crc_pre[(kCrcChunk - (L & (kCrcChunk - 1))) & (kCrcChunk - 1)];
+  uint32_t acc = 0;
+  for (int q0 = 0; q0 < nch; q0 += 64 * CRC_ILP) {
+    uint32_t c[CRC_ILP];
+    int beg[CRC_ILP];
+#pragma unroll
+    for (int k = 0; k < CRC_ILP; ++k) {
+      const int q = q0 + 64 * k + lane; // chunk distance to the end, in chunks
+      beg[k] = L - kCrcChunk * (q + 1);
+      c[k] = q == nch - 1 ? r0 : 0u;
+    }
+#pragma unroll
+    for (int st = 0; st < kCrcChunk / 4; ++st) {
+#pragma unroll
+      for (int k = 0; k < CRC_ILP; ++k) {
+        if (q0 + 64 * k >= nch) continue; // wave-uniform
+        uint32_t x = c[k] ^ le_word_pad(v, max(beg[k], -kCrcChunk) + 4 * st);
+        c[k] = t4[768 + (x & 0xFF)] ^ t4[512 + ((x >> 8) & 0xFF)] ^ t4[256 + ((x >> 16) & 0xFF)] ^ t4[x >> 24];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CRC_ILP; ++k) {
+      const int q = q0 + 64 * k + lane;
+      if (q0 + 64 * k < nch && q < nch) acc ^= crc_shift(t.crc_mat, q, c[k]);
+    }
+  }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc)) ^ 0xFFFFFFFFu;
+}
+
+// the same over messages longer than kCrcMats chunks (8 KB): kCrcMats-chunk blocks in
+// sequence, each block's first chunk carrying the register of the blocks before it
+__device__ inline uint32_t wave_crc32_long(const uint32_t *v, int L, const DevTables &t) {
+  const int lane = wave_lane();
+  const uint32_t *t4 = t.crc_s4;
   constexpr int BLOCKB = kCrcMats * kCrcChunk; // bytes per block
   uint32_t reg = 0xFFFFFFFFu; // carried between blocks (uniform)
   for (int p0 = 0; p0 < L; p0 += BLOCKB) {
@@ -1306,7 +1350,13 @@ __device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables 
     for (int j = lane; j < nch; j += 64) {
       const int end = plen - (nch - 1 - j) * kCrcChunk; // exclusive, relative to p0
       const int beg = max(0, end - kCrcChunk);
-      const uint32_t c = crc_chunk(v, p0 + beg, p0 + end, j == 0 ? reg : 0u, t4);
+      uint32_t c = j == 0 ? reg : 0u;
+      int i = p0 + beg;
+      for (; i + 4 <= p0 + end; i += 4) {
+        c ^= le_word_pad(v, i);
+        c = t4[768 + (c & 0xFF)] ^ t4[512 + ((c >> 8) & 0xFF)] ^ t4[256 + ((c >> 16) & 0xFF)] ^ t4[c >> 24];
+      }
+      for (; i < p0 + end; ++i) c = t4[(c ^ stream_byte(v, i)) & 0xFF] ^ (c >> 8);
       acc ^= crc_shift(t.crc_mat, nch - 1 - j, c);
     }
     reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
@@ -1314,11 +1364,45 @@ __device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables 
   return reg ^ 0xFFFFFFFFu;
 }
 
-// Majority vote (modem.js:487-495) of the first nbits of `bits` into `voted`, one wave.
+// Majority vote (modem.js:487-495) of the first nbits of `bits` into `voted`, one wave:
+// voted word wd is the vote over raw words [REP wd, REP wd + REP), which each lane reads
+// once; the bit extraction is unrolled (REP known at compile time), no per-bit LDS reads.
+// Bits of the last word past the voted count are zero.
+template <int REP> __device__ __forceinline__ void wave_vote_t(const uint32_t *bits, int nbits, uint32_t *voted) {
+  const int nv = nbits / REP;
+  const int nw = (nv + 31) >> 5;
+  constexpr int thr = (REP + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
+  for (int wd = wave_lane(); wd < nw; wd += 64) {
+    uint32_t raw[REP];
+#pragma unroll
+    for (int u = 0; u < REP; ++u) raw[u] = bits[REP * wd + u];
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      int sum = 0;
+#pragma unroll
+      for (int u = 0; u < REP; ++u) {
+        const int pos = b * REP + u;
+        sum += (raw[pos >> 5] >> (31 - (pos & 31))) & 1;
+      }
+      word |= (uint32_t)(sum >= thr) << (31 - b);
+    }
+    const int valid = nv - 32 * wd;
+    if (valid < 32) word &= ~(0xFFFFFFFFu >> valid);
+    voted[wd] = word;
+  }
+}
 __device__ inline void wave_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
+  switch (rep) {
+  case 2: wave_vote_t<2>(bits, nbits, voted); return;
+  case 3: wave_vote_t<3>(bits, nbits, voted); return;
+  case 4: wave_vote_t<4>(bits, nbits, voted); return;
+  case 5: wave_vote_t<5>(bits, nbits, voted); return;
+  default: break;
+  }
   const int nv = nbits / rep;
   const int nw = (nv + 31) >> 5;
-  const int thr = (rep + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
+  const int thr = (rep + 1) >> 1;
   for (int wd = wave_lane(); wd < nw; wd += 64) {
     uint32_t word = 0;
     for (int b = 0; b < 32; ++b) {
@@ -1783,7 +1867,10 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           }
           DSTAMP(24, true);
           if (crc_len >= 0) {
-            r.actual_crc = wave_crc32(v, crc_len, cfg.t, cfg.t.crc_s4); // 4 KB table, L1-resident
+            // the slice-by-4 table goes to this wave's exchange buffer (the frame's FFTs are done)
+            r.actual_crc = crc_len <= kCrcMats * kCrcChunk
+                               ? wave_crc32(v, crc_len, cfg.t, reinterpret_cast<uint32_t *>(X2))
+                               : wave_crc32_long(v, crc_len, cfg.t);
             r.crc_valid = r.expected_crc == r.actual_crc;
           }
           DSTAMP(25, true);

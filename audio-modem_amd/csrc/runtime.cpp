@@ -195,13 +195,22 @@ void shift_operator(int64_t nbytes, uint32_t *op /*4*256*/) {
     }                                                                                   \
   } while (0)
 
+// Grow-only device buffer. A buffer a captured hipGraph may still reference (`keep`
+// set once a decode was captured) is never freed when it grows: the old allocation moves
+// to `retired` and lives until the context closes, so replays keep valid memory.
 struct DevBuf {
   void *p = nullptr;
   size_t n = 0;
+  const bool *keep = nullptr;
+  std::vector<void *> *retired = nullptr;
   ~DevBuf() { if (p) (void)hipFree(p); }
   hipError_t ensure(size_t bytes) {
     if (bytes <= n) return hipSuccess;
-    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+    if (p) {
+      if (keep && *keep && retired) retired->push_back(p);
+      else (void)hipFree(p);
+      p = nullptr; n = 0;
+    }
     hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
     if (e == hipSuccess) n = std::max<size_t>(bytes, 256);
     return e;
@@ -253,7 +262,13 @@ struct amod_ctx {
   int soft_slots = 0;
   int64_t xs_stride = 0, bits_stride = 0;
   int nslots = 0;
-  int64_t max_len = 0; // longest frame any reservation was sized for
+  int64_t max_len = 0; // longest frame any reservation was sized for (exact-kernel workspace)
+  // device path (amod_decode_device): the fast-path capacity, in samples, of the latest
+  // amod_reserve (default 65536 before any). A frame's route depends on the frame, the
+  // options and this capacity only, never on other calls' shapes (host paths size it from
+  // the launch's own longest frame)
+  int64_t dev_cap = 65536;
+  std::vector<void *> retired; // buffers a captured graph may reference (freed at close)
   // host-path staging
   DevBuf h_samples, h_off, h_len, h_res, h_payload, h_dbg;
   std::mutex mu;
@@ -262,8 +277,10 @@ struct amod_ctx {
   int64_t nstamps = 0;
   // kernel timing (amod_set_profiling)
   bool profiling = false;
-  // per decode: before k_detect, after k_detect, after k_demod, after k_decode_exact
-  std::vector<std::array<hipEvent_t, 4>> ev_used, ev_free;
+  // per decode: before k_detect, after k_detect, after k_demod (on the launch stream),
+  // the end of the second stream's chain (list A's exact kernel + replay k_demod), after
+  // the launch stream has joined it, after list B's exact kernel
+  std::vector<std::array<hipEvent_t, 6>> ev_used, ev_free;
 };
 
 namespace {
@@ -289,8 +306,9 @@ int validate(const amod_cfg *c) {
 
 int build_crc(amod_ctx *ctx) {
   if (ctx->crc.p) return AMOD_SUCCESS;
-  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024 + amod::kCrcMats * 32);
+  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024 + amod::kCrcMats * 32 + 16);
   uint32_t *s4 = h.data(), *m1 = s4 + 1024, *m2 = m1 + 32 * 1024, *mb = m2 + 32 * 1024, *mat = mb + 1024;
+  uint32_t *pre = mat + amod::kCrcMats * 32;
   const uint32_t *t0 = crc_table();
   for (int i = 0; i < 256; ++i) s4[i] = t0[i];
   for (int k = 1; k < 4; ++k)
@@ -305,6 +323,19 @@ int build_crc(amod_ctx *ctx) {
     for (int q = 0; q < amod::kCrcMats; ++q) {
       mat[32 * q + b] = r;
       for (int i = 0; i < 16; ++i) r = crc_table()[r & 0xFF] ^ (r >> 8);
+    }
+  }
+  // pre[k]: the register k zero bytes earlier that the k bytes advance to ~0. One zero
+  // byte maps r to T[r & 0xFF] ^ (r >> 8); the top byte of T[x] is a bijection of x, so
+  // the step inverts: x from the top byte, then r = ((r' ^ T[x]) << 8) | x
+  {
+    uint32_t inv_top[256];
+    for (uint32_t x = 0; x < 256; ++x) inv_top[crc_table()[x] >> 24] = x;
+    uint32_t r = 0xFFFFFFFFu;
+    for (int k = 0; k < 16; ++k) {
+      pre[k] = r;
+      const uint32_t x = inv_top[r >> 24];
+      r = ((r ^ crc_table()[x]) << 8) | x;
     }
   }
   HIP_TRY(ctx->crc.ensure(h.size() * 4));
@@ -407,6 +438,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.t.crc_m2 = crc + 1024 + 32 * 1024;
     d.t.crc_mb = crc + 1024 + 64 * 1024;
     d.t.crc_mat = crc + 1024 + 64 * 1024 + 1024;
+    d.t.crc_pre = d.t.crc_mat + amod::kCrcMats * 32;
     it = ctx->tables.emplace(key, std::move(ts)).first;
   }
   out = it->second->cfg;
@@ -448,10 +480,10 @@ static hipError_t fb_grow(amod_ctx *ctx, int32_t nframes) {
 }
 
 int reserve(amod_ctx *ctx, const amod_cfg *c, int32_t nframes, int64_t max_len) {
-  if (max_len < 0) { // device path: keep what amod_reserve set up, or size from a default
+  if (max_len < 0) { // device path: keep what amod_reserve set up, or size for dev_cap
     HIP_TRY(fb_grow(ctx, nframes));
-    if (ctx->nslots > 0) return AMOD_SUCCESS;
-    max_len = 65536;
+    if (ctx->nslots > 0 && ctx->max_len >= ctx->dev_cap) return AMOD_SUCCESS;
+    max_len = ctx->dev_cap;
   }
   const int64_t nslots = std::max<int64_t>(1, std::min<int64_t>({(int64_t)nframes, 512,
       std::max<int64_t>(1, (int64_t)(2ll << 30) / std::max<int64_t>(1, max_len * 4))}));
@@ -513,9 +545,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     w.soft = (float *)ctx->soft.p;
     w.soft_stride = ctx->soft_stride;
   }
-  // fast-path capacities from the longest frame of this launch (host path) or of the
+  // fast-path capacities from the longest frame of this launch (host path) or the latest
   // reservation (device path); a frame's route depends only on it and on the frame
-  const ChainDims dims = chain_dims(cfg, max_len >= 0 ? max_len : ctx->max_len);
+  const ChainDims dims = chain_dims(cfg, max_len >= 0 ? max_len : ctx->dev_cap);
   rc = ensure_chain(ctx, nframes);
   if (rc) return rc;
   w.nb_cap = dims.nb_cap; w.fine_cap = dims.fine_cap; w.mcap = dims.mcap; w.fast_len = dims.fast_len;
@@ -538,7 +570,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (cap != hipStreamCaptureStatusNone) ctx->fb_captured = true;
   if (!ctx->fb_zeroed || ctx->fb_captured) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // both counter sets
   ctx->fb_zeroed = false; // until this decode's list-B launch is enqueued with its reset
-  std::array<hipEvent_t, 4> ev{};
+  std::array<hipEvent_t, 6> ev{};
   if (ctx->profiling) {
     if (ctx->ev_free.empty()) {
       for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
@@ -547,7 +579,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       ctx->ev_free.pop_back();
     }
   }
-  auto mark = [&](int i) -> hipError_t { return ctx->profiling ? hipEventRecord(ev[i], s) : hipSuccess; };
+  auto mark = [&](int i, hipStream_t on = nullptr) -> hipError_t {
+    return ctx->profiling ? hipEventRecord(ev[i], on ? on : s) : hipSuccess;
+  };
   // d.stop_after (diagnostics, AMOD_STOP_AFTER): <= 2 stops after detection
   const bool demod = d.stop_after >= 3;
   const int lds = 4 * 4 * w.stream_words; // k_demod: 4 waves per block
@@ -604,13 +638,16 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       if (getenv("AMOD_EXACT_SERIAL")) {
         wb.f0 = 0; wb.f1 = nframes;
         HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
+        HIP_TRY(mark(2));
         rc = exact_a(s);
         if (rc) return rc;
+        HIP_TRY(mark(3));
       } else {
       HIP_TRY(hipEventRecord(ctx->chunk_ev[0], s));
       HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[0], 0));
       rc = exact_a(ctx->aux);
       if (rc) return rc;
+      HIP_TRY(mark(3, ctx->aux));
       HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
       wb.f0 = 0; wb.f1 = nframes;
       {
@@ -624,10 +661,13 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
         }
         HIP_TRY(amod_launch_demod(d, wm, nb, s));
       }
+      HIP_TRY(mark(2));
       HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0)); // workspace slots are shared
       }
     } else {
       HIP_TRY(amod_launch_exact(d, w, xslots, s));
+      HIP_TRY(mark(2));
+      HIP_TRY(mark(3));
     }
   } else {
     for (int c = 0; c < nchunk; ++c) {
@@ -641,16 +681,18 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     HIP_TRY(mark(1)); // every k_detect done (on s)
     HIP_TRY(hipEventRecord(ctx->chunk_ev[kMaxChunks], ctx->aux));
     HIP_TRY(hipStreamWaitEvent(s, ctx->chunk_ev[kMaxChunks], 0));
+    HIP_TRY(mark(2)); // (chunked diagnostics: k_demod ends with the join)
     rc = exact_a(s);
     if (rc) return rc;
+    HIP_TRY(mark(3));
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
-  HIP_TRY(mark(2));
+  HIP_TRY(mark(4));
   wb.fb_reset = ctx->fb_captured ? nullptr : fb_base + 32 * (1 - ctx->fb_parity); // zeroed for the next decode
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
   ctx->fb_zeroed = xslots > 0 && !ctx->fb_captured;
   if (!ctx->fb_captured) ctx->fb_parity ^= 1;
-  HIP_TRY(mark(3));
+  HIP_TRY(mark(5));
   if (ctx->profiling) ctx->ev_used.push_back(ev);
   return AMOD_SUCCESS;
 }
@@ -786,6 +828,10 @@ int amod_open(int device, amod_ctx **out) {
   HIP_TRY(hipSetDevice(device));
   auto *ctx = new amod_ctx();
   ctx->device = device;
+  for (DevBuf *b : {&ctx->fb, &ctx->xs, &ctx->bits, &ctx->soft, &ctx->det}) {
+    b->keep = &ctx->fb_captured;
+    b->retired = &ctx->retired;
+  }
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return fail(nullptr, "hipStreamCreate failed", AMOD_ERR_HIP);
@@ -806,6 +852,7 @@ int amod_close(amod_ctx *ctx) {
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &ev : ctx->ev_used) for (auto &e : ev) (void)hipEventDestroy(e);
+  for (void *p : ctx->retired) (void)hipFree(p);
   for (auto &ev : ctx->ev_free) for (auto &e : ev) (void)hipEventDestroy(e);
   delete ctx;
   return AMOD_SUCCESS;
@@ -866,6 +913,7 @@ int amod_reserve(amod_ctx *ctx, const amod_cfg *cfg, int32_t nframes, int64_t ma
   amod::DevCfg d;
   int rc = get_tables(ctx, cfg, d);
   if (rc) return rc;
+  if (max_len >= 0) ctx->dev_cap = max_len; // the device path's fast-path capacity from now on
   return reserve(ctx, cfg, nframes, max_len);
 }
 
@@ -936,23 +984,33 @@ int amod_set_profiling(amod_ctx *ctx, int enable) {
   return AMOD_SUCCESS;
 }
 
-int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n) {
-  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n) {
+  if (!ctx || nslots < 0 || (nslots && !ms)) return fail(ctx, "invalid argument", AMOD_ERR_ARG);
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->device));
-  double acc[3] = {0, 0, 0};
+  // the slots: {from event, to event} (amod.h AMOD_STAGE_*)
+  static const int span[AMOD_STAGE_COUNT][2] = {{0, 1}, {1, 2}, {4, 5}, {1, 3}, {2, 4}, {1, 4}};
+  double acc[AMOD_STAGE_COUNT] = {0};
   for (auto &ev : ctx->ev_used) {
-    HIP_TRY(hipEventSynchronize(ev[3]));
-    for (int i = 0; i < 3; ++i) {
+    HIP_TRY(hipEventSynchronize(ev[5]));
+    for (int i = 0; i < AMOD_STAGE_COUNT; ++i) {
       float t = 0;
-      HIP_TRY(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      HIP_TRY(hipEventElapsedTime(&t, ev[span[i][0]], ev[span[i][1]]));
       acc[i] += t;
     }
     ctx->ev_free.push_back(ev);
   }
-  if (ms) for (int i = 0; i < 3; ++i) ms[i] = acc[i];
+  for (int i = 0; i < nslots; ++i) ms[i] = i < AMOD_STAGE_COUNT ? acc[i] : 0.0;
   if (n) *n = (int64_t)ctx->ev_used.size();
   ctx->ev_used.clear();
+  return AMOD_SUCCESS;
+}
+
+int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n) {
+  double st[AMOD_STAGE_COUNT];
+  const int rc = amod_kernel_stages(ctx, st, AMOD_STAGE_COUNT, n);
+  if (rc) return rc;
+  if (ms) { ms[0] = st[AMOD_STAGE_DETECT]; ms[1] = st[AMOD_STAGE_DEMOD_PATH]; ms[2] = st[AMOD_STAGE_EXACT_B]; }
   return AMOD_SUCCESS;
 }
 

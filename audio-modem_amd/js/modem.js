@@ -250,43 +250,59 @@ const PRE_DEMOD = new Set([1, 2, 3, 4, 12]); // outcomes decided before demodula
 const E_INVALID_LEN = 7, E_UNKNOWN_TYPE = 13, E_CAPACITY = 100;
 const REC = 96; // sizeof(amod_result)
 
-function utf8(bytes) {
-  return new TD().decode(bytes);
+// TextDecoder().decode (the reference decodes names with a fresh TextDecoder): one
+// decoder for every call, and plain ASCII (no BOM, no multi-byte sequence: the decoder's
+// output is then the bytes' own code points) without it
+const UTF8 = new TD();
+function utf8(bytes, off, len) {
+  if (off === undefined) { off = 0; len = bytes.length; }
+  let s = '';
+  for (let i = 0; i < len; i++) {
+    const c = bytes[off + i];
+    if (c > 0x7F || len > 256) return UTF8.decode(bytes.subarray(off, off + len));
+    s += String.fromCharCode(c);
+  }
+  return s;
 }
 
-// one amod_result record (+ its payload slot) -> the reference's return object
-function formatResult(view, i, payload, stride, viaLegacy) {
+// one amod_result record (+ its payload slot) -> the reference's return object.
+// share = false: `data` is a fresh Uint8Array (bytes.slice, modem.js:636,837); share =
+// true (decodeBatch): `data` is a view of the call's own payload buffer (every frame's
+// range its own, nothing else holds the buffer), which spares one allocation per frame
+function formatResult(view, i, payload, stride, viaLegacy, share, u8) {
   const o = i * REC;
-  const g = (k) => view.getInt32(o + 4 * k, true);
-  const status = g(0), preambleIdx = g(1), frameType = g(3), aux = g(4);
-  const slot = new Uint8Array(payload, i * stride, stride);
+  const status = view.getInt32(o, true);
+  const preambleIdx = view.getInt32(o + 4, true), frameType = view.getInt32(o + 12, true);
   if (status === E_CAPACITY) throw new Error('frame exceeds the reserved decode workspace');
   if (status === 0) {
-    const nameOff = g(6), nameLen = g(7), dataOff = g(8), dataLen = g(9);
-    const crc = {
-      crcValid: g(16) !== 0,
-      expectedCRC: view.getUint32(o + 56, true),
-      actualCRC: view.getUint32(o + 60, true),
-    };
+    const base = i * stride;
+    const nameOff = base + view.getInt32(o + 24, true), nameLen = view.getInt32(o + 28, true);
+    const dataOff = base + view.getInt32(o + 32, true), dataLen = view.getInt32(o + 36, true);
+    const crcValid = view.getInt32(o + 64, true) !== 0;
+    const expectedCRC = view.getUint32(o + 56, true), actualCRC = view.getUint32(o + 60, true);
+    const all = u8 || new Uint8Array(payload);
     if (frameType === FRAME_META) {
-      const r = Object.assign({
-        frameType: FRAME_META, totalChunks: g(11), totalFileSize: g(12), chunkSize: g(13),
-        fileName: utf8(slot.slice(nameOff, nameOff + nameLen)),
-      }, crc);
+      const r = {
+        frameType: FRAME_META, totalChunks: view.getInt32(o + 44, true), totalFileSize: view.getInt32(o + 48, true),
+        chunkSize: view.getInt32(o + 52, true), fileName: utf8(all, nameOff, nameLen), crcValid, expectedCRC,
+        actualCRC,
+      };
       if (viaLegacy) r.preambleIdx = preambleIdx;
       return r;
     }
+    const data = share ? all.subarray(dataOff, dataOff + dataLen) : all.slice(dataOff, dataOff + dataLen);
     if (frameType === FRAME_DATA) {
-      const r = Object.assign({
-        frameType: FRAME_DATA, seqNum: g(10), data: slot.slice(dataOff, dataOff + dataLen), dataLen,
-      }, crc);
+      const r = { frameType: FRAME_DATA, seqNum: view.getInt32(o + 40, true), data, dataLen, crcValid, expectedCRC,
+        actualCRC };
       if (viaLegacy) r.preambleIdx = preambleIdx;
       return r;
     }
-    return Object.assign({
-      data: slot.slice(dataOff, dataOff + dataLen), dataLen, fileName: utf8(slot.slice(nameOff, nameOff + nameLen)),
-    }, crc, { preambleIdx, frameType: 'legacy' });
+    return {
+      data, dataLen, fileName: utf8(all, nameOff, nameLen), crcValid, expectedCRC, actualCRC, preambleIdx,
+      frameType: 'legacy',
+    };
   }
+  const aux = view.getInt32(o + 16, true);
   if (status === E_INVALID_LEN) return { error: `Invalid data length: ${aux}` };
   if (status === E_UNKNOWN_TYPE) return { error: `Unknown frame type: 0x${aux.toString(16)}`, frameType: aux };
   const r = { error: ERR[status] };
@@ -307,7 +323,7 @@ function decodeOne(signal, modName, repetition, mode) {
   const out = native.decode(asFloat32(signal), null, null, cfg, mode, 0);
   const view = new DataView(out.results);
   if (!known && !PRE_DEMOD.has(view.getInt32(0, true))) modulationId(modName);
-  return formatResult(view, 0, out.payload, out.stride, mode === MODE_RECEIVED);
+  return formatResult(view, 0, out.payload, out.stride, mode === MODE_RECEIVED, false);
 }
 
 // decodeReceivedSignal(signal, modName, repetition) (modem.js:557-654)
@@ -332,12 +348,15 @@ function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
   const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
   return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0,
     Math.max(1, o.devices | 0))
-    .then((out) => {
-      const view = new DataView(out.results);
-      const res = new Array(lens.length);
-      for (let i = 0; i < lens.length; i++) res[i] = formatResult(view, i, out.payload, out.stride, mode === MODE_RECEIVED);
-      return res;
-    });
+    .then((out) => formatBatch(out.results, out.payload, out.stride, lens.length, mode === MODE_RECEIVED));
+}
+
+// every record of a batch -> the reference's result objects, in frame order
+function formatBatch(results, payload, stride, n, viaLegacy) {
+  const view = new DataView(results), u8 = new Uint8Array(payload);
+  const res = new Array(n);
+  for (let i = 0; i < n; i++) res[i] = formatResult(view, i, payload, stride, viaLegacy, true, u8);
+  return res;
 }
 
 // analyzeLoopback(recorded, modName, repetition, testData) (modem.js:975-1082).
@@ -518,7 +537,7 @@ const api = {
   decodeReceivedSignal, FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame, decodeChunkFrame,
   estimateFrameSamples, generateSweepTone, generateTestSignal, analyzeLoopback,
   decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native, ChunkAssembler, receiveStream,
-  StreamingReceiver, RECV_STATE,
+  StreamingReceiver, RECV_STATE, _formatBatch: formatBatch,
 };
 
 module.exports = api;

@@ -148,7 +148,14 @@ int32_t amod_estimate_frame_samples(const amod_cfg *cfg, int32_t payload_bytes);
 /* bytes each frame's payload slot needs for frames up to max_frame_len samples */
 int64_t amod_payload_stride(const amod_cfg *cfg, int64_t max_frame_len);
 /* pre-size the workspace so a later decode of this shape allocates nothing
-   (required before capturing amod_decode_device into a hipGraph) */
+   (required before capturing amod_decode_device into a hipGraph). max_frame_len also
+   sets the device path's fast-path capacity from this call on (default 65536 samples):
+   on amod_decode_device a frame's route (fast kernels or the exact replica, visible in
+   amod_result.flags / coarse_idx / fine_metric / payload_valid; never in the reference's
+   fields) depends on the frame, the options and the latest reservation only. Host
+   decodes size their own capacity from their longest frame. After a decode was captured
+   into a graph, a buffer that must grow is kept (not freed) until amod_close, so the
+   graph's replays stay valid. */
 int amod_reserve(amod_ctx *ctx, const amod_cfg *cfg, int32_t nframes, int64_t max_frame_len);
 
 /* ---- decode ----
@@ -175,8 +182,23 @@ int amod_set_profiling(amod_ctx *ctx, int enable);
 int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_launches, double *exact_ms,
                       int64_t *exact_launches);
 /* the same events split by launch: ms[0..2] = k_detect (k_chunk_prep in chunk mode),
-   k_demod, k_decode_exact, accumulated over *n decodes; resets like amod_kernel_times */
+   k_demod up to the launch stream's join with the second stream (so it includes any
+   part of list A's exact chain that outlasts k_demod), list B's k_decode_exact;
+   accumulated over *n decodes; resets like amod_kernel_times */
 int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n);
+/* the stage slots of amod_kernel_stages (ms[AMOD_STAGE_*], milliseconds summed over *n
+   decodes; resets like amod_kernel_times) */
+enum {
+  AMOD_STAGE_DETECT = 0,     /* k_detect / k_chunk_prep */
+  AMOD_STAGE_DEMOD = 1,      /* k_demod alone (launch stream) */
+  AMOD_STAGE_EXACT_B = 2,    /* list B's k_decode_exact (frames k_demod listed) */
+  AMOD_STAGE_AUX = 3,        /* second stream: list A's k_decode_exact + the replay k_demod,
+                                from the end of k_detect (runs beside k_demod) */
+  AMOD_STAGE_JOIN_WAIT = 4,  /* end of k_demod -> the launch stream joined the second one */
+  AMOD_STAGE_DEMOD_PATH = 5, /* k_demod + the join wait (amod_kernel_breakdown's ms[1]) */
+  AMOD_STAGE_COUNT = 6
+};
+int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n);
 
 /* parity-test view of one frame's intermediates (filled when debug != NULL) */
 #define AMOD_DBG_BAND 256

@@ -20,6 +20,9 @@ for s in "$@"; do
     variants) for v in ${VARIANTS:-w5s8}; do run bench_$v 300 env AMODEM_LIB=audio-modem_amd/lib/variants/$v/libamodem.so python bench.py --steps 20 --warmup 3 --cpu-frames -1; done;;
     pmcic) run pmc_ic 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/pmc_ic -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-frames -1;;
     pmcstages2) run pmc_stages2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LEVEL_WAVES SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_VMEM --kernel-trace -d gpurun_out/pmc_stages2 -o run --output-format csv -- python tools/stage_profile.py;;
+    demodprof) run demod_c2 300 python tools/demod_profile.py c2 && run demod_c4 300 python tools/demod_profile.py c4 && run demod_c5 300 python tools/demod_profile.py c5;;
+    pmcc4) run pmc_c4_sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --kernel-trace --stats -d gpurun_out/pmc_c4_sq -o run --output-format csv -- python bench.py --config ${PMCCFG:-c4} --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 5 --warmup 2 &&
+           run pmc_c4_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d gpurun_out/pmc_c4_fetch -o run --output-format csv -- python bench.py --config ${PMCCFG:-c4} --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 5 --warmup 2;;
     listpc) run listpc 120 rocprofv3 -L;;
     ab) run ab 600 python tools/ab.py $(for v in ${VARIANTS}; do echo audio-modem_amd/lib/variants/$v/libamodem.so; done);;
   esac

@@ -40,16 +40,14 @@ def test_group_equals_single_context(devices):
     assert sum(split) == len(offs) and len(split) == len(devices)
     if len(devices) > 1:
         assert min(split) > 0
-    # reference-visible fields (flags / coarse_idx / fine_metric / payload_valid say how the
-    # engine produced a result: they may follow the launch's workspace capacities)
-    vis = [n for n in amodem.RESULT_DTYPE.names
-           if n not in ("flags", "payload_valid", "fine_metric", "coarse_idx", "reserved")]
-    for n in vis:
+    # whole records (the engine-side fields too: a frame's route depends on the frame and on
+    # the launch's own capacity, which every frame of a host launch fits) and whole rows
+    inv = np.argsort(perm)
+    for n in amodem.RESULT_DTYPE.names:
+        if n == "reserved":
+            continue
         assert (rec[n] == ref[n]).all(), n
-        assert (rec2[n] == ref[n][perm]).all(), n
-    for i in range(len(offs)):
-        k = min(int(ref["payload_valid"][i]), int(rec["payload_valid"][i]),
-                int(rec2["payload_valid"][np.nonzero(perm == i)[0][0]]))
-        assert pay[i, :k].tobytes() == rpay[i, :k].tobytes()
-        assert pay2[np.nonzero(perm == i)[0][0], :k].tobytes() == rpay[i, :k].tobytes()
+        assert (rec2[n][inv] == ref[n]).all(), n
+    assert np.array_equal(pay, rpay)
+    assert np.array_equal(pay2[inv], rpay)
     assert (ref["status"] == 0).all()

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Diagnostics: k_demod phase marks (AMOD_STAMPS=1, s_memtime per wave) on a bench workload.
+
+  python tools/demod_profile.py [c2|c4|c5] [frames]
+
+Job 1 of each frame: 16 samples folded -> 17 FFT -> 18 band + equalise -> 19 guards + pilot
+reductions -> 20 demap + bit stream -> 21 end of job; frame end: 22 start -> 23 parse_need ->
+24 parse -> 25 CRC -> 26 stores. Prints median / p10 / p90 cycles between marks, the wave
+lifetime and the frames per wave."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    conf = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    frames = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    env = bench.Env()
+    wl = bench.Workload(env, conf, frames, snr=10.0)
+    for _ in range(20):
+        wl.step()
+    os.environ["AMOD_STAMPS"] = "1"
+    for _ in range(3):
+        wl.step()
+    wl.dm.synchronize()
+    del os.environ["AMOD_STAMPS"]
+    st = np.zeros(wl.F * 32, dtype=np.uint64)
+    n = env.lib.amod_debug_stamps(wl.dm.ctx, st.ctypes.data, st.size)
+    st = st[:n].reshape(-1, 32).astype(np.int64)
+    print(f"{conf}: {wl.F} frames x {int(wl.dlens[0])} samples")
+    for seq in ([16, 17, 18, 19, 20, 21], [22, 23, 24, 25, 26]):
+        for a, b in zip(seq, seq[1:]):
+            ok = (st[:, a] != 0) & (st[:, b] != 0)
+            d = st[ok, b] - st[ok, a]
+            if ok.any():
+                print(f"  {a} -> {b}  n={ok.sum():6d}  median {np.median(d):8.0f}  p10 {np.percentile(d, 10):8.0f}"
+                      f"  p90 {np.percentile(d, 90):8.0f}")
+    ok = (st[:, 21] != 0) & (st[:, 16] != 0)
+    print("job 1 total median", np.median(st[ok, 21] - st[ok, 16]))
+    ok = (st[:, 21] != 0) & (st[:, 27] != 0)
+    if ok.any():
+        d = st[ok, 27] - st[ok, 21]
+        print(f"job 1 end -> job 2 samples ready: median {np.median(d):.0f} p10 {np.percentile(d, 10):.0f} "
+              f"p90 {np.percentile(d, 90):.0f}")
+    ok = (st[:, 28] != 0) & (st[:, 29] != 0)
+    if ok.any():
+        a, b = st[ok, 28], st[ok, 29]
+        print(f"waves {ok.sum()}: lifetime median {np.median(b - a):.0f} p10 {np.percentile(b - a, 10):.0f} "
+              f"p90 {np.percentile(b - a, 90):.0f}; start spread {a.max() - a.min()}, kernel span {b.max() - a.min()}; "
+              f"frames per wave {wl.F / ok.sum():.2f}")
+    wl.close()
+
+
+if __name__ == "__main__":
+    main()
