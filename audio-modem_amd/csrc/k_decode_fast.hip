@@ -1292,7 +1292,7 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   return r;
 }
 constexpr int CRC_ILP = 4;
-__device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *t4l) {
+__device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *t4l) {
   const int lane = wave_lane();
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(t.crc_s4);
@@ -1338,7 +1338,7 @@ __device__ inline uint32_t wave_crc32(const uint32_t *v, int L, const DevTables 
 
 // the same over messages longer than kCrcMats chunks (8 KB): kCrcMats-chunk blocks in
 // sequence, each block's first chunk carrying the register of the blocks before it
-__device__ inline uint32_t wave_crc32_long(const uint32_t *v, int L, const DevTables &t) {
+__device__ __forceinline__ uint32_t wave_crc32_long(const uint32_t *v, int L, const DevTables &t) {
   const int lane = wave_lane();
   const uint32_t *t4 = t.crc_s4;
   constexpr int BLOCKB = kCrcMats * kCrcChunk; // bytes per block
@@ -1392,7 +1392,7 @@ template <int REP> __device__ __forceinline__ void wave_vote_t(const uint32_t *b
     voted[wd] = word;
   }
 }
-__device__ inline void wave_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
+__device__ __forceinline__ void wave_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
   switch (rep) {
   case 2: wave_vote_t<2>(bits, nbits, voted); return;
   case 3: wave_vote_t<3>(bits, nbits, voted); return;

@@ -28,6 +28,9 @@
 // Built with -ffp-contract=off.
 #include "amodem_internal.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace amod {
 namespace {
 
@@ -36,8 +39,9 @@ __device__ __forceinline__ float sample_at(const float *x, int64_t n, int64_t i)
 constexpr double kAlpha = 0.999;
 constexpr double kOneMinusAlpha = 1.0 - 0.999; // (1 - this.dcAlpha), evaluated in double
 constexpr int kL = 1024;                       // EMA chunk (one lane each in k_ema_out)
-constexpr int kWarm = 16;                      // warm-up chunks before each chunk (longer than
-                                               // a transmitter's inter-frame silence)
+constexpr int kWarmDefault = 4;                // warm-up chunks before each chunk (the parallel fix
+                                               // rounds settle the chunks whose chains had not met)
+constexpr int kEmaRounds = 3;                  // parallel fix rounds before the serial safety net
 constexpr int kTile = 64;                      // samples per lane per LDS tile
 
 // one step of processAudioBlock's DC removal (app.js:753): fl(fl(a m) + fl((1 - a) x))
@@ -75,7 +79,7 @@ constexpr int kRow = kTile + 4; // row stride (floats): 16-byte rows for ds_read
 __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, int64_t nx, int64_t n,
                                                  const double *__restrict__ c,
                                                  double A, float *__restrict__ y, double *__restrict__ warm,
-                                                 double *__restrict__ end, int64_t nch) {
+                                                 double *__restrict__ end, int64_t nch, int kWarm) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kRow];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t k0 = ((int64_t)blockIdx.x * 4 + wv) * 64; // the wave's first chunk
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
   float *const T = tile[wv];
   // lane l's row at step j covers samples [(k0 + l - kWarm) L + 64 j, + 64) (warm-up
   // chunks first, then chunk k0 + l); rows before the stream start are skipped
-  constexpr int steps = (kWarm + 1) * kL / kTile, wsteps = kWarm * kL / kTile;
+  const int steps = (kWarm + 1) * kL / kTile, wsteps = kWarm * kL / kTile;
   const int rr = lane >> 4, c4 = lane & 15; // load/store slot: rows rr + 4 q, column 4 c4
   // the wave's window as raw buffers: out-of-range dwords read 0 / are not written, so no
   // load or store sits under a branch (offsets before the stream start wrap out of range)
@@ -166,47 +170,94 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
   if (k < nch) end[k] = m;
 }
 
-// (3) chunks whose warm-up state is not bit-equal to the previous chunk's end state
-// (warm-up not converged): listed for k_ema_fix. Chunk 0 starts from the true zero.
-__global__ __launch_bounds__(256) void k_ema_check(const double *__restrict__ warm, const double *__restrict__ end,
-                                                   int64_t nch, unsigned long long *__restrict__ cnt,
-                                                   int64_t *__restrict__ list) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x + 1;
+// (3) chunks whose start state is not bit-equal to the previous chunk's end state
+// (warm-up not converged): flagged (lflag) and listed for the fix passes. Chunk 0 starts
+// from the true zero; cnt is one round's counter
+__global__ __launch_bounds__(256) void k_ema_check_flag(const double *__restrict__ warm, const double *__restrict__ end,
+                                                        int64_t nch, unsigned long long *__restrict__ cnt,
+                                                        int64_t *__restrict__ list, uint8_t *__restrict__ lflag) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= nch) return;
-  if (__double_as_longlong(warm[k]) != __double_as_longlong(end[k - 1])) {
-    const unsigned long long i = atomicAdd(cnt, 1ull);
-    list[i] = k;
-  }
+  const bool bad = k > 0 && __double_as_longlong(warm[k]) != __double_as_longlong(end[k - 1]);
+  lflag[k] = bad;
+  if (bad) list[atomicAdd(cnt, 1ull)] = k;
 }
 
-// (4) one wave: the listed chunks in order, each recomputed from its predecessor's true
-// end state, and the next chunk too while its warm-up state disagrees with the new end.
-// Afterwards every cleaned sample equals the reference's. fixed = chunks recomputed.
-// The state is wave-uniform; 64 samples are loaded coalesced, stepped lane by lane in
-// order (readlane), and stored coalesced.
-__global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int64_t nx, int64_t n, float *__restrict__ y,
-                                                const double *__restrict__ warm, double *__restrict__ end, int64_t nch,
-                                                const unsigned long long *__restrict__ cnt, int64_t *__restrict__ list,
-                                                unsigned long long *__restrict__ fixed) {
-  if (blockIdx.x != 0) return;
-  const int lane = threadIdx.x;
+// (4') one round of the parallel fix: one wave per RUN of listed chunks (a listed chunk whose
+// predecessor is not listed heads one; chunk 0 and every verified chunk before a head end
+// in the true state). The wave recomputes the head from its predecessor's end state, then
+// walks on while the next chunk is listed behind it (the same run) or its recorded start
+// state differs from the new end (the change propagates), recording each chunk's start
+// state in warm[] and its end in end[]. It stops before a chunk another run's wave owns.
+// Runs are independent, so they proceed in parallel; a start state read while another
+// run rewrote it is caught by the next round's check (amod_launch_ema runs rounds until a
+// check lists nothing). The state is wave-uniform; 64 samples per step are loaded
+// coalesced, stepped in order through readlane and stored coalesced (as k_ema_fix).
+__global__ __launch_bounds__(256) void k_ema_runs(const float *__restrict__ x, int64_t nx, int64_t n,
+                                                  float *__restrict__ y, double *__restrict__ warm,
+                                                  double *__restrict__ end, int64_t nch,
+                                                  const unsigned long long *__restrict__ cnt,
+                                                  const int64_t *__restrict__ list, const uint8_t *__restrict__ lflag,
+                                                  unsigned long long *__restrict__ fixed) {
+  const int lane = threadIdx.x & 63;
   const int64_t nl = (int64_t)*cnt;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
   unsigned long long nf = 0;
-  if (nl > 0) {
-    if (lane == 0) // the listed indices in increasing order (atomic append order is arbitrary)
-      for (int64_t i = 1; i < nl; ++i) {
-        const int64_t v = list[i];
-        int64_t j = i - 1;
-        while (j >= 0 && list[j] > v) { list[j + 1] = list[j]; --j; }
-        list[j + 1] = v;
+  for (int64_t li = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); li < nl; li += nwaves) {
+    int64_t t = list[li];
+    if (lflag[t - 1]) continue; // inside a run: its head's wave takes it
+    double m = end[t - 1];
+    for (;;) {
+      if (lane == 0) warm[t] = m; // the start state this chunk's outputs now come from
+      const int64_t a = t * kL, b = a + kL < n ? a + kL : n;
+      for (int64_t b0 = a; b0 < b; b0 += 64) {
+        const float xv = b0 + lane < b && b0 + lane < nx ? x[b0 + lane] : 0.f;
+        const int nj = b - b0 < 64 ? (int)(b - b0) : 64;
+        float yv = 0.f;
+        for (int j = 0; j < nj; ++j) {
+          const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+          m = ema_step(m, xj);
+          const float o = (float)((double)xj - m);
+          yv = lane == j ? o : yv;
+        }
+        if (b0 + lane < b) y[b0 + lane] = yv;
       }
-    __syncthreads();
-    int64_t done = 0; // chunks below this are final
-    for (int64_t li = 0; li < nl; ++li) {
-      int64_t t = list[li];
+      if (lane == 0) end[t] = m;
+      ++nf;
+      if (t + 1 >= nch) break;
+      const bool next_listed = lflag[t + 1] != 0, cur_listed = lflag[t] != 0;
+      if (next_listed ? !cur_listed : __double_as_longlong(warm[t + 1]) == __double_as_longlong(m)) break;
+      ++t;
+    }
+  }
+  if (lane == 0 && nf) atomicAdd(fixed, nf);
+}
+
+// (4) the safety net after the parallel rounds, one wave: the chunks still flagged (lflag,
+// from the last k_ema_check_flag), in increasing order (found 64 at a time by a ballot
+// over the flags; nothing to do when the count is zero), each recomputed from its
+// predecessor's true end state, and the next chunk too while its start state disagrees
+// with the new end. Afterwards every cleaned sample equals the reference's. fixed +=
+// chunks recomputed. The state is wave-uniform; 64 samples are loaded coalesced, stepped
+// lane by lane in order (readlane), and stored coalesced.
+__global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int64_t nx, int64_t n, float *__restrict__ y,
+                                                double *__restrict__ warm, double *__restrict__ end, int64_t nch,
+                                                const unsigned long long *__restrict__ cnt,
+                                                const uint8_t *__restrict__ lflag,
+                                                unsigned long long *__restrict__ fixed) {
+  if (blockIdx.x != 0 || *cnt == 0) return;
+  const int lane = threadIdx.x;
+  unsigned long long nf = 0;
+  int64_t done = 0; // chunks below this are final
+  for (int64_t base = 0; base < nch; base += 64) {
+    uint64_t fl = __ballot(base + lane < nch && lflag[base + lane] != 0);
+    while (fl) {
+      int64_t t = base + __builtin_ctzll(fl);
+      fl &= fl - 1;
       if (t < done) continue;
-      for (;;) {
-        double m = end[t - 1]; // true: every earlier chunk is verified or recomputed
+      double m = end[t - 1]; // true: every earlier chunk is verified or recomputed
+      for (;;) {             // (m carries the state through the chain, no re-read)
+        if (lane == 0) warm[t] = m;
         const int64_t a = t * kL, b = a + kL < n ? a + kL : n;
         for (int64_t b0 = a; b0 < b; b0 += 64) {
           const float xv = b0 + lane < b && b0 + lane < nx ? x[b0 + lane] : 0.f;
@@ -228,7 +279,7 @@ __global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int
       }
     }
   }
-  if (lane == 0) *fixed = nf;
+  if (lane == 0 && nf) *fixed += nf;
 }
 
 // 32-sample block sums of the cleaned stream in fp64: z_b = sum y[k] y[k+256], e_b =
@@ -565,11 +616,33 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
   hipError_t e = hipMemsetAsync(fixed, 0, 2 * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)nch), dim3(256), 0, s, x, nx, apow, scr);
+  static const int warm_chunks = [] {
+    const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
+    return e ? std::max(0, atoi(e)) : amod::kWarmDefault;
+  }();
   hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, x, nx, n, scr, A, y, warm,
-                     end, nch);
-  hipLaunchKernelGGL(amod::k_ema_check, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, warm, end, nch, fixed + 1,
-                     list);
-  hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, list, fixed);
+                     end, nch, warm_chunks);
+  // parallel fix rounds: each round checks every chunk's start state against its
+  // predecessor's end and recomputes the listed runs in parallel; after kEmaRounds rounds
+  // the serial fix settles anything left (normally nothing: runs are a chunk or two long)
+  uint8_t *const lflag = reinterpret_cast<uint8_t *>(list + nch);
+  static const int rounds = [] {
+    const char *e = getenv("AMOD_EMA_ROUNDS"); // experiments
+    return e ? std::max(0, atoi(e)) : amod::kEmaRounds;
+  }();
+  for (int r = 0; r < rounds; ++r) {
+    e = hipMemsetAsync(fixed + 1, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(amod::k_ema_check_flag, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, warm, end, nch,
+                       fixed + 1, list, lflag);
+    hipLaunchKernelGGL(amod::k_ema_runs, dim3(2048), dim3(256), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, list,
+                       lflag, fixed);
+  }
+  e = hipMemsetAsync(fixed + 1, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(amod::k_ema_check_flag, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, warm, end, nch,
+                     fixed + 1, list, lflag);
+  hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, lflag, fixed);
   return hipGetLastError();
 }
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {

@@ -785,7 +785,7 @@ struct Prepass {
     S_TRY(c->d_warm.alloc(sizeof(double) * nchunks));
     S_TRY(c->d_end.alloc(sizeof(double) * nchunks));
     S_TRY(c->d_scr.alloc(sizeof(double) * nchunks));
-    S_TRY(c->d_list.alloc(sizeof(int64_t) * nchunks));
+    S_TRY(c->d_list.alloc((sizeof(int64_t) + 1) * nchunks + 64)); // list, then one flag byte per chunk
     S_TRY(c->d_apow.alloc(sizeof(double) * kEmaChunk));
     S_TRY(c->d_fixed.alloc(16));
     if (!c->apow_ready) {
@@ -1049,7 +1049,7 @@ extern "C" int amod_dc_remove_device(amod_ctx *ctx, const float *x, int64_t n, f
   S_TRY(warm.alloc(sizeof(double) * nch));
   S_TRY(end.alloc(sizeof(double) * nch));
   S_TRY(scr.alloc(sizeof(double) * nch));
-  S_TRY(list.alloc(sizeof(int64_t) * nch));
+  S_TRY(list.alloc((sizeof(int64_t) + 1) * nch + 64)); // list, then one flag byte per chunk
   S_TRY(apow.alloc(sizeof(double) * kEmaChunk));
   S_TRY(fixed.alloc(16));
   std::vector<double> ap((size_t)kEmaChunk);

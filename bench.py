@@ -318,6 +318,14 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     # reported on its own), list B's exact kernel
     stage_ms = [st_ms[L.STAGE_DETECT], st_ms[L.STAGE_DEMOD], st_ms[L.STAGE_EXACT_B]]
     rec = wl.records()
+    if os.environ.get("AMOD_STAMPS"):  # diagnostics: exact-kernel phase marks of the listed frames
+        st = np.zeros(wl.F * 32, dtype=np.uint64)
+        n = lib.amod_debug_stamps(wl.dm.ctx, st.ctypes.data, st.size)
+        st = st[:n].reshape(-1, 32).astype(np.int64)
+        for i in np.nonzero(rec["flags"] & (env.L.FLAG_EXACT | env.L.FLAG_REPLAY))[0][:32]:
+            print("listed", i, hex(int(rec["flags"][i])), int(rec["coarse_idx"][i]),
+                  [int(st[i, b] - st[i, a]) if st[i, a] and st[i, b] else None
+                   for a, b in ((8, 13), (13, 14), (14, 9), (9, 10), (10, 11), (11, 12))], file=sys.stderr)
     ok = int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum())
     fallback = int((rec["flags"] != 0).sum())
     # correctness of what was timed (the last timed step's results): clean configs decode

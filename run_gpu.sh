@@ -23,6 +23,9 @@ for s in "$@"; do
     demodprof) run demod_c2 300 python tools/demod_profile.py c2 && run demod_c4 300 python tools/demod_profile.py c4 && run demod_c5 300 python tools/demod_profile.py c5;;
     pmcc4) run pmc_c4_sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --kernel-trace --stats -d gpurun_out/pmc_c4_sq -o run --output-format csv -- python bench.py --config ${PMCCFG:-c4} --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 5 --warmup 2 &&
            run pmc_c4_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d gpurun_out/pmc_c4_fetch -o run --output-format csv -- python bench.py --config ${PMCCFG:-c4} --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 5 --warmup 2;;
+    streamdiag) run stream_diag 300 python tools/stream_diag.py ${NCHUNKS:-32000};;
+    emasweep) for W in ${WARMS:-16 4 2 1}; do run ema_w$W 300 env AMOD_EMA_WARM=$W python tools/ema_probe.py ${NCHUNKS:-32000} || exit 1; done;;
+    c5stamps) run c5stamps 300 env AMOD_STAMPS=1 python bench.py --config c5 --snr 10 --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 3 --warmup 1;;
     listpc) run listpc 120 rocprofv3 -L;;
     ab) run ab 600 python tools/ab.py $(for v in ${VARIANTS}; do echo audio-modem_amd/lib/variants/$v/libamodem.so; done);;
   esac
