@@ -145,7 +145,9 @@ struct GapScan {
   int64_t det_block, pre_pos;  // the block whose scan call detected, the coarse position
   int64_t ac_pos, scanned;     // the scan position after it; positions stepped
   double p, ra, rb;            // the running sums after it
-  int32_t status, pad;
+  int32_t status, ref_ok;      // ref_ok: the refinement of pre_pos below is valid (k_gap_refine)
+  double ref_best;             // _refineAndCollect over [pre_pos - 3 cp, pre_pos + 3 cp]: the first
+  int64_t ref_pos;             // maximum (NaN skipped; -inf and pre_pos when none)
 };
 
 // AMOD_OPT_SOFT_COMBINE applies to repeated BPSK / QPSK frames
@@ -481,12 +483,14 @@ int64_t amod_ema_chunk();
 hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
                            int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s);
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
-hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
+hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
-                            int64_t maxcount, double *out, double2 *barg, hipStream_t s);
+                            int64_t maxcount, double *out, double *out_dev, double2 *barg, hipStream_t s);
 hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int64_t *first, const double2 *barg,
                                 int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks, int max_blocks,
                                 amod::GapScan *out, hipStream_t s);
+hipError_t amod_launch_gap_refine(amod::GapScan *g, int nrec, int64_t lo, const int64_t *first, const int64_t *base,
+                                  const int64_t *count, int nranges, const double *metric, int64_t radius, hipStream_t s);
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,
                               int nwin, float *out, hipStream_t s);
 hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s);

@@ -54,7 +54,9 @@ struct FileArena {
 #endif
     filler = std::thread([q = p, len = n] {
       constexpr int kPopulateWrite = 23; // MADV_POPULATE_WRITE (Linux 5.14)
-      constexpr size_t kStep = size_t(8) << 20;
+      // one huge page per call: each call holds the address-space lock (read) while it
+      // zeroes, and the receiver's own mappings (thread stacks, vectors) wait for it
+      constexpr size_t kStep = size_t(2) << 20;
       for (size_t o = 0; o < len; o += kStep) {
         const size_t m = std::min(kStep, len - o);
         if (madvise(q + o, m, kPopulateWrite) != 0) { // older kernels: touch every page, value kept

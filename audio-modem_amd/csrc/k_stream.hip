@@ -41,8 +41,11 @@ constexpr double kOneMinusAlpha = 1.0 - 0.999; // (1 - this.dcAlpha), evaluated 
 constexpr int kL = 1024;                       // EMA chunk (one lane each in k_ema_out)
 constexpr int kWarmDefault = 4;                // warm-up chunks before each chunk (the parallel fix
                                                // rounds settle the chunks whose chains had not met)
-constexpr int kEmaRounds = 3;                  // parallel fix rounds before the serial safety net
-constexpr int kTile = 64;                      // samples per lane per LDS tile
+constexpr int kEmaRounds = 6;                  // parallel fix rounds before the serial safety net
+constexpr int kTile = 32;                      // samples per lane per LDS tile (36.9 KB per workgroup:
+                                               // four per CU; 16 with 8 waves per SIMD measured slower)
+constexpr int kLPR = kTile / 4;                // lanes per tile row in the coalesced loads / stores
+constexpr int kRPI = 64 / kLPR;                // tile rows per load instruction
 
 // one step of processAudioBlock's DC removal (app.js:753): fl(fl(a m) + fl((1 - a) x))
 __device__ __forceinline__ double ema_step(double m, float x) { return kAlpha * m + kOneMinusAlpha * (double)x; }
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
   // lane l's row at step j covers samples [(k0 + l - kWarm) L + 64 j, + 64) (warm-up
   // chunks first, then chunk k0 + l); rows before the stream start are skipped
   const int steps = (kWarm + 1) * kL / kTile, wsteps = kWarm * kL / kTile;
-  const int rr = lane >> 4, c4 = lane & 15; // load/store slot: rows rr + 4 q, column 4 c4
+  const int rr = lane / kLPR, c4 = lane % kLPR; // load/store slot: rows rr + kRPI q, column 4 c4
   // the wave's window as raw buffers: out-of-range dwords read 0 / are not written, so no
   // load or store sits under a branch (offsets before the stream start wrap out of range)
   const int64_t wb = (k0 - kWarm) * kL > 0 ? (k0 - kWarm) * kL : 0, yb = k0 * kL;
@@ -104,11 +107,11 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
       (void *)(x + wb), (short)0, (int)(4 * (xlen < (1 << 28) ? xlen : (1 << 28))), 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)(y + yb), (short)0, (int)(4 * (ylen < (1 << 28) ? ylen : (1 << 28))), 0x00020000);
-  float4 pf[16]; // the next tile's samples
+  float4 pf[kLPR]; // the next tile's samples
   auto load = [&](int j) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t g = (k0 + rr + 4 * q - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
+    for (int q = 0; q < kLPR; ++q) {
+      const int64_t g = (k0 + rr + kRPI * q - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * g), 0, 0);
       pf[q] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
   for (int j = 0; j < steps; ++j) {
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int q = 0; q < 16; ++q) *reinterpret_cast<float4 *>(T + (rr + 4 * q) * kRow + 4 * c4) = pf[q];
+    for (int q = 0; q < kLPR; ++q) *reinterpret_cast<float4 *>(T + (rr + kRPI * q) * kRow + 4 * c4) = pf[q];
     __builtin_amdgcn_wave_barrier();
     if (j + 1 < steps) load(j + 1); // in flight under this tile's recurrence
     const int64_t row0 = (k - kWarm) * kL + (int64_t)kTile * j; // first sample of this lane's row
@@ -126,23 +129,21 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
     float *const R = T + lane * kRow;
     if (row0 >= kw * kL) { // warm-up from the chunk kw (its approximate seed), then chunk k
       if (row0 + kTile <= n) {
-        // eight samples a group: the (1 - a) x products first, then the dependent chain
+        // four samples a group: the (1 - a) x products first, then the dependent chain
         // fl(fl(a m) + b) alone, then the outputs from the saved states
-#pragma unroll 2
-        for (int i = 0; i < kTile; i += 8) {
-          const float4 v0 = *reinterpret_cast<const float4 *>(R + i), v1 = *reinterpret_cast<const float4 *>(R + i + 4);
-          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          double b[8], ms[8];
+        for (int i = 0; i < kTile; i += 4) {
+          const float4 v0 = *reinterpret_cast<const float4 *>(R + i);
+          const float xv[4] = {v0.x, v0.y, v0.z, v0.w};
+          double b[4], ms[4];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) b[u] = kOneMinusAlpha * (double)xv[u];
+          for (int u = 0; u < 4; ++u) b[u] = kOneMinusAlpha * (double)xv[u];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) { m = kAlpha * m + b[u]; ms[u] = m; }
+          for (int u = 0; u < 4; ++u) { m = kAlpha * m + b[u]; ms[u] = m; }
           if (out) {
-            float o[8];
+            float o[4];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) o[u] = (float)((double)xv[u] - ms[u]);
+            for (int u = 0; u < 4; ++u) o[u] = (float)((double)xv[u] - ms[u]);
             *reinterpret_cast<float4 *>(R + i) = make_float4(o[0], o[1], o[2], o[3]);
-            *reinterpret_cast<float4 *>(R + i + 4) = make_float4(o[4], o[5], o[6], o[7]);
           }
         }
       } else { // the stream's last samples
@@ -156,8 +157,8 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
     if (out) {
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int r = rr + 4 * q;
+      for (int q = 0; q < kLPR; ++q) {
+        const int r = rr + kRPI * q;
         const int64_t g = r * kL + (int64_t)kTile * (j - wsteps) + 4 * c4;
         const float4 v = *reinterpret_cast<const float4 *>(T + r * kRow + 4 * c4);
         __amdgpu_buffer_rsrc_t yrr = yr;
@@ -183,54 +184,70 @@ __global__ __launch_bounds__(256) void k_ema_check_flag(const double *__restrict
   if (bad) list[atomicAdd(cnt, 1ull)] = k;
 }
 
-// (4') one round of the parallel fix: one wave per RUN of listed chunks (a listed chunk whose
-// predecessor is not listed heads one; chunk 0 and every verified chunk before a head end
-// in the true state). The wave recomputes the head from its predecessor's end state, then
-// walks on while the next chunk is listed behind it (the same run) or its recorded start
+// (4') one round of the parallel fix: one LANE per run of flagged chunks (a flagged chunk
+// whose predecessor is not flagged heads one; every verified chunk before a head ends in
+// the true state). The lane recomputes the head from its predecessor's end state, then
+// walks on while the next chunk is flagged behind it (the same run) or its recorded start
 // state differs from the new end (the change propagates), recording each chunk's start
-// state in warm[] and its end in end[]. It stops before a chunk another run's wave owns.
-// Runs are independent, so they proceed in parallel; a start state read while another
-// run rewrote it is caught by the next round's check (amod_launch_ema runs rounds until a
-// check lists nothing). The state is wave-uniform; 64 samples per step are loaded
-// coalesced, stepped in order through readlane and stored coalesced (as k_ema_fix).
+// state in warm[] and its end in end[]; it stops before a chunk another run's lane owns.
+// Runs are independent, so 64 of them step in parallel per wave (each lane its own
+// exact chain over its own samples, 16 per load); a start state read while another run
+// rewrote it is caught by the next round's check. Lanes whose runs end early idle until
+// the wave's longest run is done (runs are a chunk or a few).
 __global__ __launch_bounds__(256) void k_ema_runs(const float *__restrict__ x, int64_t nx, int64_t n,
                                                   float *__restrict__ y, double *__restrict__ warm,
                                                   double *__restrict__ end, int64_t nch,
                                                   const unsigned long long *__restrict__ cnt,
                                                   const int64_t *__restrict__ list, const uint8_t *__restrict__ lflag,
                                                   unsigned long long *__restrict__ fixed) {
-  const int lane = threadIdx.x & 63;
   const int64_t nl = (int64_t)*cnt;
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if ((int64_t)blockIdx.x * 256 >= nl) return; // (whole workgroup past the list)
+  bool active = li < nl;
+  int64_t t = active ? list[li] : 1;
+  if (active && lflag[t - 1]) active = false; // inside a run: its head's lane takes it
+  double m = active ? end[t - 1] : 0.0;
   unsigned long long nf = 0;
-  for (int64_t li = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); li < nl; li += nwaves) {
-    int64_t t = list[li];
-    if (lflag[t - 1]) continue; // inside a run: its head's wave takes it
-    double m = end[t - 1];
-    for (;;) {
-      if (lane == 0) warm[t] = m; // the start state this chunk's outputs now come from
+  while (__ballot(active)) {
+    if (active) {
+      warm[t] = m; // the start state this chunk's outputs now come from
       const int64_t a = t * kL, b = a + kL < n ? a + kL : n;
-      for (int64_t b0 = a; b0 < b; b0 += 64) {
-        const float xv = b0 + lane < b && b0 + lane < nx ? x[b0 + lane] : 0.f;
-        const int nj = b - b0 < 64 ? (int)(b - b0) : 64;
-        float yv = 0.f;
-        for (int j = 0; j < nj; ++j) {
-          const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
-          m = ema_step(m, xj);
-          const float o = (float)((double)xj - m);
-          yv = lane == j ? o : yv;
+      if (b - a == kL && a + kL <= nx) {
+        const float4 *src = reinterpret_cast<const float4 *>(x + a);
+        float4 *dst = reinterpret_cast<float4 *>(y + a);
+        for (int i = 0; i < kL / 4; i += 4) {
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = src[i + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { m = ema_step(m, xs[q]); o[q] = (float)((double)xs[q] - m); }
+            dst[i + u] = make_float4(o[0], o[1], o[2], o[3]);
+          }
         }
-        if (b0 + lane < b) y[b0 + lane] = yv;
+      } else { // the stream's last chunk
+        for (int64_t g = a; g < b; ++g) {
+          const float xv = g < nx ? x[g] : 0.f;
+          m = ema_step(m, xv);
+          y[g] = (float)((double)xv - m);
+        }
       }
-      if (lane == 0) end[t] = m;
+      end[t] = m;
       ++nf;
-      if (t + 1 >= nch) break;
-      const bool next_listed = lflag[t + 1] != 0, cur_listed = lflag[t] != 0;
-      if (next_listed ? !cur_listed : __double_as_longlong(warm[t + 1]) == __double_as_longlong(m)) break;
-      ++t;
+      if (t + 1 >= nch) {
+        active = false;
+      } else {
+        const bool next_flagged = lflag[t + 1] != 0, cur_flagged = lflag[t] != 0;
+        if (next_flagged ? !cur_flagged : __double_as_longlong(warm[t + 1]) == __double_as_longlong(m)) active = false;
+        else ++t;
+      }
     }
   }
-  if (lane == 0 && nf) atomicAdd(fixed, nf);
+  nf = wave_sum(nf);
+  if ((threadIdx.x & 63) == 0 && nf) atomicAdd(fixed, nf);
 }
 
 // (4) the safety net after the parallel rounds, one wave: the chunks still flagged (lflag,
@@ -249,7 +266,13 @@ __global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int
   const int lane = threadIdx.x;
   unsigned long long nf = 0;
   int64_t done = 0; // chunks below this are final
-  for (int64_t base = 0; base < nch; base += 64) {
+  for (int64_t b16 = 0; b16 < nch; b16 += 1024) { // 16 flags per lane per load
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (b16 + 16 * lane + 16 <= nch) q = *reinterpret_cast<const uint4 *>(lflag + b16 + 16 * lane);
+    else for (int i = 0; i < 16 && b16 + 16 * lane + i < nch; ++i) reinterpret_cast<uint8_t *>(&q)[i] = lflag[b16 + 16 * lane + i];
+    if (!__ballot((q.x | q.y | q.z | q.w) != 0)) continue;
+    for (int sub = 0; sub < 16; ++sub) {
+    const int64_t base = b16 + 64 * sub;
     uint64_t fl = __ballot(base + lane < nch && lflag[base + lane] != 0);
     while (fl) {
       int64_t t = base + __builtin_ctzll(fl);
@@ -278,21 +301,28 @@ __global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int
         break;
       }
     }
+    }
   }
   if (lane == 0 && nf) *fixed += nf;
 }
 
 // 32-sample block sums of the cleaned stream in fp64: z_b = sum y[k] y[k+256], e_b =
-// sum y[k]^2 over k in [32 b, 32 b + 32); one lane per sample, 32-lane reductions
+// sum y[k]^2 over k in [32 b, 32 b + 32) (a screening hint: any order); four samples per
+// lane (float4, coalesced), 8-lane reductions. n is a multiple of 4.
 __global__ __launch_bounds__(256) void k_sc_blocks(const float *__restrict__ y, int64_t n, int64_t nblk,
                                                    double2 *__restrict__ ze) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const double a = sample_at(y, n, k), c = sample_at(y, n, k + 256);
-  double z = a * c, e = a * a;
+  const int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 a = k < n ? *reinterpret_cast<const float4 *>(y + k) : zero4;
+  const float4 c = k + 256 < n ? *reinterpret_cast<const float4 *>(y + k + 256) : zero4;
+  double z = (double)a.x * c.x, e = (double)a.x * a.x;
+  z = __builtin_fma((double)a.y, (double)c.y, z); e = __builtin_fma((double)a.y, (double)a.y, e);
+  z = __builtin_fma((double)a.z, (double)c.z, z); e = __builtin_fma((double)a.z, (double)a.z, e);
+  z = __builtin_fma((double)a.w, (double)c.w, z); e = __builtin_fma((double)a.w, (double)a.w, e);
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) { z += __shfl_xor(z, o, 32); e += __shfl_xor(e, o, 32); }
+  for (int o = 1; o < 8; o <<= 1) { z += __shfl_xor(z, o, 8); e += __shfl_xor(e, o, 8); }
   const int64_t b = k >> 5;
-  if ((threadIdx.x & 31) == 0 && b < nblk) ze[b] = make_double2(z, e);
+  if ((threadIdx.x & 7) == 0 && b < nblk) ze[b] = make_double2(z, e);
 }
 
 // hot flag per block: the metric at position 32 b (window = 8 blocks) >= thresh
@@ -314,10 +344,11 @@ __global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ z
 constexpr int kFineMaxSym = 1024; // symbol_len bound of k_fine's LDS window (presets: 576 .. 768)
 // barg (optional): per workgroup, the first maximum of its positions' metrics (NaN
 // skipped, as the refinement's `metric > best`) as (metric, j), at [r * gridDim.x + bx]
-__global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const float *__restrict__ pre1,
+__global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const double *__restrict__ pre1,
                                               int sym, double pre1_energy, const int64_t *__restrict__ first,
                                               const int64_t *__restrict__ base, const int64_t *__restrict__ count,
-                                              int nranges, double *__restrict__ out, double2 *__restrict__ barg) {
+                                              int nranges, double *__restrict__ out, double *__restrict__ out_dev,
+                                              double2 *__restrict__ barg) {
   __shared__ double2 red[4];
   __shared__ float win[256 + kFineMaxSym]; // the workgroup's samples [d0, d0 + 256 + sym)
   const int r = blockIdx.y;
@@ -336,15 +367,19 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
   if (j < count[r]) {
     double corr = 0.0, se = 0.0;
     const float *const w = win + threadIdx.x;
+    // f32 x f32 products are exact in double, so fma(s, q, corr) is the reference's
+    // corr + s * q with its one rounding: half the fp64 operations of mul + add
+#pragma unroll 8
     for (int i = 0; i < sym; ++i) {
       const double s = w[i];
-      corr += s * (double)pre1[i];
-      se += s * s;
+      corr = __builtin_fma(s, pre1[i], corr);
+      se = __builtin_fma(s, s, se);
     }
     // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
     const double denom = sqrt(se * pre1_energy);
     const double v = denom > 0.001 ? corr / denom : __builtin_nan("");
     out[base[r] + j] = v;
+    if (out_dev) out_dev[base[r] + j] = v; // (the device copy k_gap_refine reads)
     if (v == v) m = v;
   }
   if (!barg) return;
@@ -571,6 +606,51 @@ __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, in
   if (lane < kGapG && r < nranges) out[r] = rec;
 }
 
+// The refinement (_refineAndCollect, app.js:849-898) of each gap record's detection, from
+// k_fine's metrics: over d in [pre_pos - radius, pre_pos + radius] the first d whose metric
+// is the largest (the reference's `metric > best` from best = -inf: NaN never wins, a later
+// equal metric never replaces an earlier one). Valid (ref_ok) only when one fine range holds
+// the whole window; the host uses it when its own window is exactly this one (the ring has
+// not overtaken the start). One wave per record.
+__global__ __launch_bounds__(256) void k_gap_refine(GapScan *__restrict__ g, int nrec, int64_t lo,
+                                                    const int64_t *__restrict__ first, const int64_t *__restrict__ base,
+                                                    const int64_t *__restrict__ count, int nranges,
+                                                    const double *__restrict__ metric, int64_t radius) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= nrec) return;
+  const int64_t pre = g[r].pre_pos;
+  int ok = g[r].status == 1;
+  const int64_t fs = pre - radius - lo, fe = pre + radius - lo; // local positions
+  int k = -1;
+  if (ok) { // the last range starting at or before fs
+    int a = 0, b = nranges; // first[a..b) ascending
+    while (a < b) { const int mid = (a + b) >> 1; if (first[mid] <= fs) a = mid + 1; else b = mid; }
+    k = a - 1;
+    ok = k >= 0 && fe < first[max(k, 0)] + count[max(k, 0)];
+  }
+  if (!ok) {
+    if (lane == 0) g[r].ref_ok = 0;
+    return;
+  }
+  const double *const mv = metric + base[k] + (fs - first[k]);
+  double m = -__builtin_inf();
+  int64_t mj = INT64_MAX;
+  for (int64_t j = lane; j <= fe - fs; j += 64) {
+    const double v = mv[j];
+    if (v > m) { m = v; mj = j; } // per lane: the first strict maximum of its positions
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(m, o, 64);
+    const int64_t oj = __shfl_xor(mj, o, 64);
+    if (om > m || (om == m && oj < mj)) { m = om; mj = oj; }
+  }
+  if (lane == 0) {
+    g[r].ref_best = m;
+    g[r].ref_pos = m > -__builtin_inf() ? lo + fs + mj : pre;
+    g[r].ref_ok = 1;
+  }
+}
+
 // the host's sparse copy of the cleaned stream: compact granule j (1024 samples) is stream
 // granule src[j]; one workgroup per granule, float4 per thread, coalesced both ways
 __global__ __launch_bounds__(256) void k_gather(const float *__restrict__ y, const int32_t *__restrict__ src,
@@ -625,7 +705,7 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
   // parallel fix rounds: each round checks every chunk's start state against its
   // predecessor's end and recomputes the listed runs in parallel; after kEmaRounds rounds
   // the serial fix settles anything left (normally nothing: runs are a chunk or two long)
-  uint8_t *const lflag = reinterpret_cast<uint8_t *>(list + nch);
+  uint8_t *const lflag = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(list + nch) + 15) & ~uintptr_t(15));
   static const int rounds = [] {
     const char *e = getenv("AMOD_EMA_ROUNDS"); // experiments
     return e ? std::max(0, atoi(e)) : amod::kEmaRounds;
@@ -635,8 +715,8 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(amod::k_ema_check_flag, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, warm, end, nch,
                        fixed + 1, list, lflag);
-    hipLaunchKernelGGL(amod::k_ema_runs, dim3(2048), dim3(256), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, list,
-                       lflag, fixed);
+    hipLaunchKernelGGL(amod::k_ema_runs, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, x, nx, n, y, warm, end,
+                       nch, fixed + 1, list, lflag, fixed);
   }
   e = hipMemsetAsync(fixed + 1, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
@@ -648,17 +728,18 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {
   const int64_t nblk = (n + 31) / 32;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::k_sc_blocks, dim3((unsigned)((32 * nblk + 255) / 256)), dim3(256), 0, s, y, n, nblk, ze);
+  if (n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(amod::k_sc_blocks, dim3((unsigned)((32 * nblk + 1023) / 1024)), dim3(256), 0, s, y, n, nblk, ze);
   hipLaunchKernelGGL(amod::k_sc_screen, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, ze, nblk, thresh, hot);
   return hipGetLastError();
 }
-hipError_t amod_launch_fine(const float *y, int64_t n, const float *pre1, int sym, double pre1_energy,
+hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,
-                            int64_t maxcount, double *out, double2 *barg, hipStream_t s) {
+                            int64_t maxcount, double *out, double *out_dev, double2 *barg, hipStream_t s) {
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
   if (sym <= 0 || sym > amod::kFineMaxSym) return hipErrorInvalidValue;
   hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
-                     pre1_energy, first, base, count, nranges, out, barg);
+                     pre1_energy, first, base, count, nranges, out, out_dev, barg);
   return hipGetLastError();
 }
 hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int64_t *first, const double2 *barg,
@@ -668,6 +749,13 @@ hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int
   hipLaunchKernelGGL(amod::k_gap_scan, dim3((unsigned)((nranges + amod::kGapG - 1) / amod::kGapG)), dim3(64), 0, s, y, n,
                      lo, first, barg,
                      nbx, nranges, F, cap, nblocks, max_blocks, out);
+  return hipGetLastError();
+}
+hipError_t amod_launch_gap_refine(amod::GapScan *g, int nrec, int64_t lo, const int64_t *first, const int64_t *base,
+                                  const int64_t *count, int nranges, const double *metric, int64_t radius, hipStream_t s) {
+  if (nrec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amod::k_gap_refine, dim3((unsigned)((nrec + 3) / 4)), dim3(256), 0, s, g, nrec, lo, first, base,
+                     count, nranges, metric, radius);
   return hipGetLastError();
 }
 hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float *out, hipStream_t s) {

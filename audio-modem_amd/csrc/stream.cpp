@@ -44,6 +44,7 @@ constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
 const int64_t kEmaChunk = amod_ema_chunk(); // k_ema chunk (EMA end states are reported per chunk)
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
 constexpr int kGranLog = 10, kGran = 1 << kGranLog; // sparse host copy granule (samples)
+constexpr int64_t kFirstPiece = int64_t(1) << 20;   // sparse mode: the first piece copied at once
 // blocks a GPU gap scan runs before it leaves the gap to the host (the kernel's time is its
 // longest gap's: a stream's tail or a long silence is the host's)
 constexpr int kGapBlocks = 8;
@@ -98,6 +99,18 @@ struct FineTable {
     m = metric[base[r] + (d - first[r])];
     return true;
   }
+  // the metrics of positions [d0, d1] when one range holds them all, else nullptr
+  const double *span(int64_t d0, int64_t d1, size_t &last) const {
+    double m;
+    if (!lookup(d0, m, last) || d1 >= first[last] + count[last]) return nullptr;
+    return metric + base[last] + (d0 - first[last]);
+  }
+};
+
+// k_gap_refine's refinement of a detection at pre_pos (window pre_pos +- 3 cp)
+struct GpuRefine {
+  int64_t pre_pos, best_pos;
+  double best;
 };
 
 struct Receiver {
@@ -107,6 +120,9 @@ struct Receiver {
   std::vector<float> pre1;
   double pre1_energy = 0;
   const FineTable *fine = nullptr;
+  const std::vector<GpuRefine> *refs = nullptr; // sorted by pre_pos
+  int64_t ref_hits = 0;
+  int32_t est_payload = -1, est_samples = 0; // estimateFrameSamples(max_payload), cached
   RxState st;
   std::vector<std::pair<int64_t, int64_t>> *fails = nullptr; // (block, preambleGlobalPos) of failed refinements
   int64_t fine_host = 0; // positions the host had to correlate itself
@@ -341,7 +357,20 @@ struct Receiver {
     const int64_t fs = std::max(total - cap, st.pre_pos - radius), fe = std::min(total - plen, st.pre_pos + radius);
     double best = -INFINITY;
     int64_t best_pos = st.pre_pos;
-    for (int64_t d = fs; d <= fe; ++d) {
+    const GpuRefine *gr = nullptr;
+    if (refs && fs == st.pre_pos - radius && fe == st.pre_pos + radius) {
+      auto it = std::lower_bound(refs->begin(), refs->end(), st.pre_pos,
+                                 [](const GpuRefine &a, int64_t p) { return a.pre_pos < p; });
+      if (it != refs->end() && it->pre_pos == st.pre_pos) gr = &*it;
+    }
+    if (gr) {
+      best = gr->best; // the same window's first maximum, from the GPU's metrics
+      best_pos = gr->best_pos;
+      ++ref_hits;
+    } else if (const double *mv = (fine && fs <= fe) ? fine->span(fs, fe, cursor) : nullptr) {
+      for (int64_t d = fs; d <= fe; ++d) // the common case: one contiguous run of k_fine metrics
+        if (mv[d - fs] > best) { best = mv[d - fs]; best_pos = d; }
+    } else for (int64_t d = fs; d <= fe; ++d) {
       double metric;
       if (!fine || !fine->lookup(d, metric, cursor)) {
         double corr = 0, se = 0;
@@ -364,7 +393,8 @@ struct Receiver {
     }
     st.pre_pos = best_pos;
     const int32_t max_payload = st.meta_received ? (st.chunk_size ? st.chunk_size : 4096) + 11 : 280;
-    st.frame_end = st.pre_pos + amod_estimate_frame_samples(cfg, max_payload);
+    if (max_payload != est_payload) { est_payload = max_payload; est_samples = amod_estimate_frame_samples(cfg, max_payload); }
+    st.frame_end = st.pre_pos + est_samples;
     st.state = COLLECTING;
   }
 
@@ -516,9 +546,9 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_threads).count(), rx.wait_ms,
             (long long)sc, total.frames.size());
     for (int k = 0; k < T; ++k)
-      fprintf(stderr, "[stream]   thread %d: %.3f ms (scan %.3f, refine %.3f), scanned %lld, frames %zu, gpu gaps %lld\n",
-              k, th_ms[k], rxs[k].scan_ms, rxs[k].refine_ms, (long long)rxs[k].scanned, seg[k].frames.size(),
-              (long long)rxs[k].gap_hits);
+      fprintf(stderr, "[stream]   thread %d: %.3f ms (scan %.3f, refine %.3f), scanned %lld, frames %zu, gpu gaps %lld, "
+              "gpu refinements %lld\n", k, th_ms[k], rxs[k].scan_ms, rxs[k].refine_ms, (long long)rxs[k].scanned,
+              seg[k].frames.size(), (long long)rxs[k].gap_hits, (long long)rxs[k].ref_hits);
   }
   return total;
 }
@@ -543,13 +573,20 @@ struct Pinned {
 // device and pinned buffers of the streaming receiver, kept per context (grow-only)
 struct StreamCache {
   DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
-  DBuf d_pre1, d_first, d_base, d_count, d_out;
-  DBuf w_pos, w_len, w_woff, w_win, w_res, w_pay;
+  DBuf d_pre1, d_first, d_base, d_count, d_out, d_metric;
+  // window decoder: two batches in flight (one decoding while the host dispatches the other)
+  DBuf w_pos[2], w_len[2], w_woff[2], w_win[2], w_res[2], w_pay[2];
+  hipEvent_t w_done[2] = {};
   DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
   DBuf d_barg, d_gaps;                      // k_fine's per-workgroup argmax, k_gap_scan's records
   Pinned gaps_h;
   Pinned yh, yc, hot_h, metric_h;
-  Pinned w_res_h, w_pay_h;                  // window decoder: results and payload rows (pinned D2H)
+  Pinned w_res_h[2], w_pay_h[2];            // window decoder: results and payload rows (pinned D2H)
+  // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
+  std::vector<uint8_t> sp_need;
+  std::vector<int32_t> sp_cidx;
+  std::unique_ptr<std::atomic<const float *>[]> sp_gptr;
+  size_t sp_gcap = 0;
   bool apow_ready = false;
   hipStream_t s2 = nullptr;                 // the cleaned stream's device-to-host copy
   static constexpr int kPieces = 16;
@@ -561,6 +598,8 @@ struct StreamCache {
     for (auto e : piece)
       if (e) (void)hipEventDestroy(e);
     for (auto e : cpiece)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : w_done)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -578,6 +617,8 @@ struct Prepass {
   const float *x = nullptr; // device samples of [lo, lo + nvalid)
   FineTable ft;
   int64_t lo = 0, n = 0, fixed = 0;
+  bool dev_metrics = false; // k_fine also keeps its metrics on the device (k_gap_refine reads them)
+  int64_t nmetric = 0;
   std::vector<double> ema_end; // EMA state after each k_ema chunk (true states)
   double t_ema = 0, t_fine = 0;
   const float *y() const { return c->d_y.as<float>(); }
@@ -590,11 +631,17 @@ struct Prepass {
   mutable bool full_started = false;
   mutable std::mutex mu;
   hipStream_t s_main = nullptr;
+  // piece q of the host copy is local samples [pstart(q), pstart(q + 1)); the first ends at
+  // p0_end (sparse: just the metadata phase's reads, so the DMA engine is soon free again)
+  int64_t p0_end = 0;
+  int64_t pstart(int q) const {
+    return q == 0 ? 0 : q == 1 ? p0_end : q >= StreamCache::kPieces ? n : n * q / StreamCache::kPieces;
+  }
   // the host copy of the cleaned stream holds local samples [0, g)
   void wait_y(int64_t g) const {
-    if (g > n / StreamCache::kPieces) start_full();
+    if (g > p0_end) start_full();
     for (int q = 0; q < StreamCache::kPieces; ++q) {
-      const int64_t a = n * q / StreamCache::kPieces;
+      const int64_t a = pstart(q);
       if (a >= g) break;
       (void)hipEventSynchronize(c->piece[q]);
     }
@@ -602,7 +649,7 @@ struct Prepass {
   // pieces [q0, kPieces) of the full copy (q0 = 1: the rest after the first)
   hipError_t enqueue_pieces(int q0) const {
     for (int q = q0; q < StreamCache::kPieces; ++q) {
-      const int64_t a = n * q / StreamCache::kPieces, b = n * (q + 1) / StreamCache::kPieces;
+      const int64_t a = pstart(q), b = pstart(q + 1);
       if (b > a) {
         const hipError_t e = hipMemcpyAsync(c->yh.p + a, c->d_y.as<float>() + a, sizeof(float) * (size_t)(b - a),
                                             hipMemcpyDeviceToHost, c->s2);
@@ -622,11 +669,12 @@ struct Prepass {
 
   // ---- sparse copy of the cleaned stream (the parallel phase's reads)
   int64_t ng = 0, first_g = 0; // granules; those inside the first piece
-  std::vector<int32_t> cidx;   // granule -> packed index (-1: not packed)
-  std::unique_ptr<std::atomic<const float *>[]> gptr;
+  int32_t *cidx = nullptr;     // granule -> packed index (-1: not packed)
+  std::atomic<const float *> *gptr = nullptr; // granule -> host pointer once there
   std::unique_ptr<std::atomic<bool>[]> cready; // packed piece q has landed
   std::atomic<bool> first_ready{false};
   mutable std::atomic<int64_t> fallbacks{0};
+  std::atomic<int64_t> wait_us{0}, fetch_us{0}; // diagnostics: piece waits, on-demand fetches
   int64_t npacked = 0;
   std::function<const float *(int64_t)> present_fn = [this](int64_t g) { return present(g); };
   std::function<const float *(int64_t)> copied_fn = [this](int64_t g) -> const float * {
@@ -644,16 +692,20 @@ struct Prepass {
     } else if (cidx[g] >= 0) {
       const int q = (int)(cidx[g] * (int64_t)StreamCache::kPieces / std::max<int64_t>(npacked, 1));
       if (!cready[q].load(std::memory_order_acquire)) {
+        const auto t0 = std::chrono::steady_clock::now();
         (void)hipEventSynchronize(c->cpiece[q]);
         cready[q].store(true, std::memory_order_release);
+        wait_us += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
       }
       p = c->yc.as<float>() + (int64_t)cidx[g] * kGran;
     } else {
+      const auto t0 = std::chrono::steady_clock::now();
       std::lock_guard<std::mutex> lk(mu);
       if ((p = gptr[g].load(std::memory_order_acquire))) return p;
       const int64_t g1 = std::min(ng, g + 16);
       (void)hipMemcpy(c->yh.as<float>() + g * kGran, c->d_y.as<float>() + g * kGran,
                       sizeof(float) * (size_t)((g1 - g) * kGran), hipMemcpyDeviceToHost);
+      fetch_us += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
       fallbacks += g1 - g;
       for (int64_t k = g + 1; k < g1; ++k)
         if (!gptr[k].load(std::memory_order_acquire) && cidx[k] < 0)
@@ -672,6 +724,7 @@ struct Prepass {
   // receiver would stand after the frame detected there (window length F)
   int nbx = 0, nfr = 0;
   std::vector<amod::GapScan> gaps;
+  std::vector<GpuRefine> refs; // k_gap_refine's refinements, by pre_pos
   bool gap_launched = false;
   int gap_scan_launch(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int64_t cap) {
     gaps.clear();
@@ -683,6 +736,10 @@ struct Prepass {
         c->gaps_h.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
         amod_launch_gap_scan(c->d_y.as<float>(), n, lo, c->d_first.as<int64_t>(), c->d_barg.as<double2>(), nbx, nfr,
                              F, cap, nblocks, kGapBlocks, c->d_gaps.as<amod::GapScan>(), s_main) != hipSuccess ||
+        (dev_metrics && nmetric > 0 &&
+         amod_launch_gap_refine(c->d_gaps.as<amod::GapScan>(), nfr, lo, c->d_first.as<int64_t>(), c->d_base.as<int64_t>(),
+                                c->d_count.as<int64_t>(), nfr, c->d_metric.as<double>(), 3 * (int64_t)cfg->cp_len,
+                                s_main) != hipSuccess) ||
         hipMemcpyAsync(c->gaps_h.p, c->d_gaps.p, sizeof(amod::GapScan) * (size_t)nfr, hipMemcpyDeviceToHost,
                        s_main) != hipSuccess)
       return AMOD_ERR_HIP;
@@ -693,24 +750,41 @@ struct Prepass {
     if (!gap_launched) return AMOD_SUCCESS;
     if (hipStreamSynchronize(s_main) != hipSuccess) return AMOD_ERR_HIP;
     const amod::GapScan *g = c->gaps_h.as<amod::GapScan>();
-    for (int r = 0; r < nfr; ++r)
-      if (g[r].status == 1) gaps.push_back(g[r]);
+    refs.clear();
+    for (int r = 0; r < nfr; ++r) {
+      if (g[r].status != 1) continue;
+      gaps.push_back(g[r]);
+      if (dev_metrics && g[r].ref_ok) refs.push_back({g[r].pre_pos, g[r].ref_pos, g[r].ref_best});
+    }
     std::sort(gaps.begin(), gaps.end(), [](const amod::GapScan &a, const amod::GapScan &b) { return a.s0 < b.s0; });
+    std::sort(refs.begin(), refs.end(), [](const GpuRefine &a, const GpuRefine &b) { return a.pre_pos < b.pre_pos; });
     return AMOD_SUCCESS;
   }
 
+  double setup_ms[4] = {}; // diagnostics: marks, index, pointer table, gather + copies
   bool sparse_setup(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int nthreads) {
     if (!sparse || full_started) return false;
+    auto tick = [t = std::chrono::steady_clock::now()](double &acc) mutable {
+      const auto now = std::chrono::steady_clock::now();
+      acc = std::chrono::duration<double, std::milli>(now - t).count();
+      t = now;
+    };
     ng = n >> kGranLog;
-    first_g = (n / StreamCache::kPieces) >> kGranLog;
-    std::vector<uint8_t> need((size_t)ng, 0);
+    first_g = p0_end >> kGranLog;
+    std::vector<uint8_t> &need = c->sp_need;
+    need.assign((size_t)ng, 0);
+    // need[g]: 1 = read by the state machine, 2 = read first (a speculative segment's or the
+    // true run's first scan: packed at the front, so each thread waits for one piece only)
+    uint8_t mark_val = 1;
     auto mark = [&](int64_t a, int64_t b) { // local samples [a, b)
       a = std::max<int64_t>(a, first_g * kGran);
       b = std::min<int64_t>(b, n);
-      for (int64_t g = a >> kGranLog; a < b && g <= (b - 1) >> kGranLog; ++g) need[(size_t)g] = 1;
+      for (int64_t g = a >> kGranLog; a < b && g <= (b - 1) >> kGranLog; ++g)
+        need[(size_t)g] = std::max(need[(size_t)g], mark_val);
     };
     // hot regions (local), blocks less than 2 K samples apart merged
     std::vector<std::pair<int64_t, int64_t>> reg;
+    reg.reserve(ft.first.size());
     if (gap_launched) { // (the fine ranges: hot blocks +- 448 samples, merged)
       for (size_t r = 0; r < ft.first.size(); ++r) reg.push_back({ft.first[r] - lo + 448, ft.first[r] - lo + ft.count[r] - 448});
     } else {
@@ -731,25 +805,32 @@ struct Prepass {
       mark(p - 1024, it == reg.end() ? p + F + W : it->first);
     };
     for (size_t k = 0; k < reg.size(); ++k) {
-      if (gap_launched) { // the scans come from the GPU: the refinement window only
-        mark(reg[k].first - R, reg[k].second + R);
+      if (gap_launched) { // the scans come from the GPU: the refinement window only (and with
+        if (!dev_metrics) mark(reg[k].first - R, reg[k].second + R); // k_gap_refine, not even that)
         continue;
       }
       mark(reg[k].first - R - 1024, reg[k].second + R + W);
       scan_from(reg[k].first - R + F); // the scan after the frame detected in region k
     }
+    mark_val = 2;
     scan_from(start.ac_pos - lo);
     const int64_t span = nblocks - start.block; // run_parallel's speculative segments
     const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, span / 64));
     for (int k = 1; k < T; ++k) scan_from((start.block + span * k / T) * kBlock - 511 - lo - 1024);
+    tick(setup_ms[0]);
     std::vector<int32_t> src;
-    cidx.assign((size_t)ng, -1);
-    for (int64_t g = first_g; g < ng; ++g)
-      if (need[(size_t)g]) { cidx[(size_t)g] = (int32_t)src.size(); src.push_back((int32_t)g); }
+    c->sp_cidx.assign((size_t)ng, -1);
+    cidx = c->sp_cidx.data();
+    for (const uint8_t pass : {uint8_t(2), uint8_t(1)}) // the first scans' granules first
+      for (int64_t g = first_g; g < ng; ++g)
+        if (need[(size_t)g] == pass) { cidx[(size_t)g] = (int32_t)src.size(); src.push_back((int32_t)g); }
     if (2 * (int64_t)src.size() > ng - first_g) { start_full(); return false; } // not worth it
     npacked = (int64_t)src.size();
-    gptr.reset(new std::atomic<const float *>[(size_t)ng]);
+    tick(setup_ms[1]);
+    if (c->sp_gcap < (size_t)ng) { c->sp_gptr.reset(new std::atomic<const float *>[(size_t)ng]); c->sp_gcap = (size_t)ng; }
+    gptr = c->sp_gptr.get();
     for (int64_t g = 0; g < ng; ++g) gptr[g].store(nullptr, std::memory_order_relaxed);
+    tick(setup_ms[2]);
     cready.reset(new std::atomic<bool>[StreamCache::kPieces]);
     for (int q = 0; q < StreamCache::kPieces; ++q) cready[q].store(npacked == 0, std::memory_order_relaxed);
     if (npacked) {
@@ -770,6 +851,7 @@ struct Prepass {
       }
       if (!ok) { (void)hipStreamSynchronize(c->s2); start_full(); return false; }
     }
+    tick(setup_ms[3]);
     return true;
   }
 
@@ -831,8 +913,9 @@ struct Prepass {
     S_TRY(hipStreamWaitEvent(c->s2, c->ema_done, 0));
     s_main = s;
     full_started = false;
+    p0_end = sparse ? std::min<int64_t>(n / StreamCache::kPieces, kFirstPiece) : n / StreamCache::kPieces;
     if (sparse) { // the first piece now, the rest on demand (sparse_setup / start_full)
-      const int64_t b = n / StreamCache::kPieces;
+      const int64_t b = p0_end;
       if (b > 0)
         S_TRY(hipMemcpyAsync(c->yh.p, c->d_y.as<float>(), sizeof(float) * (size_t)b, hipMemcpyDeviceToHost, c->s2));
       S_TRY(hipEventRecord(c->piece[0], c->s2));
@@ -855,10 +938,10 @@ struct Prepass {
     };
     bool open = false;
     for (int64_t b = 0; b < nhot; ++b) {
-      if ((b & 7) == 0 && b + 8 <= nhot) { // eight quiet blocks at a time
-        uint64_t w8;
-        memcpy(&w8, hot + b, 8);
-        if (!w8) { b += 7; continue; }
+      if ((b & 63) == 0 && b + 64 <= nhot) { // 64 quiet blocks at a time
+        uint64_t w[8];
+        memcpy(w, hot + b, 64);
+        if (!((w[0] | w[1]) | (w[2] | w[3]) | (w[4] | w[5]) | (w[6] | w[7]))) { b += 63; continue; }
       }
       if (!hot[b]) continue;
       const int64_t za = 32 * b - pad, zb = 32 * b + 31 + pad;
@@ -876,11 +959,14 @@ struct Prepass {
       double p1e = 0.0; // this.pre1Energy (app.js:744-745)
       for (float v : p1) p1e += (double)v * (double)v;
       const int nr = (int)first_loc.size();
-      S_TRY(c->d_pre1.alloc(sizeof(float) * p1.size()));
+      nmetric = total;
+      if (dev_metrics) S_TRY(c->d_metric.alloc(sizeof(double) * (size_t)total));
+      std::vector<double> p1d(p1.begin(), p1.end()); // (exact: k_fine's fma operand)
+      S_TRY(c->d_pre1.alloc(sizeof(double) * p1.size()));
       S_TRY(c->d_first.alloc(sizeof(int64_t) * nr));
       S_TRY(c->d_base.alloc(sizeof(int64_t) * nr));
       S_TRY(c->d_count.alloc(sizeof(int64_t) * nr));
-      S_TRY(hipMemcpyAsync(c->d_pre1.p, p1.data(), sizeof(float) * p1.size(), hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(c->d_pre1.p, p1d.data(), sizeof(double) * p1d.size(), hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_first.p, first_loc.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
@@ -890,9 +976,10 @@ struct Prepass {
       S_TRY(c->d_barg.alloc(sizeof(double2) * (size_t)nr * nbx));
       for (int r0 = 0; r0 < nr; r0 += 65535) {
         const int k = std::min(65535, nr - r0);
-        S_TRY(amod_launch_fine(c->d_y.as<float>(), n, c->d_pre1.as<float>(), cfg->symbol_len, p1e,
+        S_TRY(amod_launch_fine(c->d_y.as<float>(), n, c->d_pre1.as<double>(), cfg->symbol_len, p1e,
                                c->d_first.as<int64_t>() + r0, c->d_base.as<int64_t>() + r0,
                                c->d_count.as<int64_t>() + r0, k, maxc, (double *)c->metric_h.dp,
+                               dev_metrics ? c->d_metric.as<double>() : nullptr,
                                c->d_barg.as<double2>() + (int64_t)r0 * nbx, s));
       }
     }
@@ -900,9 +987,11 @@ struct Prepass {
     S_TRY(hipEventRecord(ev[2], s));
     S_TRY(hipStreamSynchronize(s));
     if (getenv("AMOD_STREAM_DIAG"))
-      fprintf(stderr, "[stream] prepass: wait for EMA+screen %.3f ms, fine ranges + launch %.3f ms, k_fine wait %.3f ms\n",
+      fprintf(stderr, "[stream] prepass: wait for EMA+screen %.3f ms, fine ranges + launch %.3f ms (%zu ranges, %lld "
+              "positions, longest %lld), k_fine wait %.3f ms\n",
               std::chrono::duration<double, std::milli>(tq1 - tq0).count(),
-              std::chrono::duration<double, std::milli>(tq2 - tq1).count(),
+              std::chrono::duration<double, std::milli>(tq2 - tq1).count(), ft.first.size(), (long long)total,
+              (long long)(ft.count.empty() ? 0 : *std::max_element(ft.count.begin(), ft.count.end())),
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq2).count());
     float ta = 0, tb = 0;
     S_TRY(hipEventElapsedTime(&ta, ev[0], ev[1]));
@@ -918,13 +1007,10 @@ struct Prepass {
     rx.lo = lo; rx.nloc = n; rx.y = c->yh.p; rx.fine = &ft;
     rx.wait_y = &wait_fn;
     rx.avail = 0;
-    const int64_t nn = n;
-    rx.piece_end = [nn](int64_t g) { // end of the piece holding local sample g
-      for (int q = 0; q < StreamCache::kPieces; ++q) {
-        const int64_t b = nn * (q + 1) / StreamCache::kPieces;
-        if (g < b) return b;
-      }
-      return nn;
+    rx.piece_end = [this](int64_t g) { // end of the piece holding local sample g
+      for (int q = 0; q < StreamCache::kPieces; ++q)
+        if (g < pstart(q + 1)) return pstart(q + 1);
+      return n;
     };
     rx.cap = (int64_t)amod_estimate_frame_samples(cfg, 4096 + 16) * 3 + 8192; // RingBuffer capacity (app.js:711-714)
     rx.pre1.resize(cfg->symbol_len);
@@ -937,73 +1023,112 @@ struct Prepass {
 // Decodes frames' windows on the GPU (k_window peak normalisation + chunk-mode decode);
 // res[i] / payload row i for frame i (lost frames get AMOD_E_STREAM_LOST).
 struct WindowDecoder {
-  std::vector<amod_result> res; // frame i - a of the last run
+  std::vector<amod_result> res; // frame i - a of the last collected batch
   std::vector<int> slot;         // its row in the pinned payload (-1: lost)
   const uint8_t *ph = nullptr;   // pinned payload rows
   std::vector<uint8_t> zero_row;
   int64_t stride = 16;
   double t_ms = 0;
-  // payload row of frame i - a of the last run (zeros for a lost window)
+  // a batch in flight in buffer set k
+  struct Flight {
+    std::vector<int64_t> pos, woff; // (host arrays kept until the batch is collected)
+    std::vector<int32_t> len;
+    std::vector<int> slot;
+    int64_t stride = 16;
+    int nw = 0;
+    size_t a = 0, b = 0;
+    bool live = false;
+  } fl[2];
+  // payload row of frame i - a of the last collected batch (zeros for a lost window)
   const uint8_t *row(size_t k) const { return slot[k] < 0 ? zero_row.data() : ph + (size_t)stride * slot[k]; }
 
-  int run(amod_ctx *ctx, const amod_cfg *cfg, const Prepass &pp, const std::vector<FrameEv> &fr, size_t a, size_t b,
-          hipStream_t s) {
+  // enqueues frames [a, b)'s windows (k_window peak normalisation) and their decode on s
+  int launch(amod_ctx *ctx, const amod_cfg *cfg, const Prepass &pp, const std::vector<FrameEv> &fr, size_t a,
+             size_t b, hipStream_t s, int k) {
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<int64_t> pos, woff;
-    std::vector<int32_t> len;
-    slot.assign(b - a, -1);
+    Flight &f = fl[k];
+    f.pos.clear(); f.woff.clear(); f.len.clear();
+    f.slot.assign(b - a, -1);
+    f.a = a; f.b = b;
     int64_t tot = 0, maxlen = 0;
     for (size_t i = a; i < b; ++i) {
       if (fr[i].lost) continue;
-      slot[i - a] = (int)pos.size();
+      f.slot[i - a] = (int)f.pos.size();
       const int64_t L = fr[i].end - fr[i].pos;
-      pos.push_back(fr[i].pos - pp.lo); len.push_back((int32_t)L); woff.push_back(tot);
+      f.pos.push_back(fr[i].pos - pp.lo); f.len.push_back((int32_t)L); f.woff.push_back(tot);
       tot += (L + 3) & ~int64_t(3);
       maxlen = std::max(maxlen, L);
     }
-    const int nw = (int)pos.size();
-    stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
-    zero_row.assign((size_t)stride, 0);
+    const int nw = f.nw = (int)f.pos.size();
+    f.stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
     StreamCache &c = *pp.c;
-    DBuf &d_pos = c.w_pos, &d_len = c.w_len, &d_woff = c.w_woff, &d_win = c.w_win, &d_res = c.w_res, &d_pay = c.w_pay;
-    S_TRY(c.w_res_h.alloc(sizeof(amod_result) * (size_t)std::max(nw, 1)));
-    S_TRY(c.w_pay_h.alloc((size_t)stride * std::max(nw, 1)));
-    const amod_result *rh = c.w_res_h.as<amod_result>();
-    ph = c.w_pay_h.as<uint8_t>();
+    DBuf &d_pos = c.w_pos[k], &d_len = c.w_len[k], &d_woff = c.w_woff[k], &d_win = c.w_win[k], &d_res = c.w_res[k],
+         &d_pay = c.w_pay[k];
+    S_TRY(c.w_res_h[k].alloc(sizeof(amod_result) * (size_t)std::max(nw, 1)));
+    S_TRY(c.w_pay_h[k].alloc((size_t)f.stride * std::max(nw, 1)));
+    if (!c.w_done[k]) S_TRY(hipEventCreateWithFlags(&c.w_done[k], hipEventDisableTiming));
     if (nw) {
       S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
       S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
       S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
       S_TRY(d_res.alloc(sizeof(amod_result) * nw));
-      S_TRY(d_pay.alloc((size_t)stride * nw));
-      S_TRY(hipMemcpyAsync(d_pos.p, pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_len.p, len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(d_woff.p, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)stride * nw, s));
+      S_TRY(d_pay.alloc((size_t)f.stride * nw));
+      S_TRY(hipMemcpyAsync(d_pos.p, f.pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_len.p, f.len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemcpyAsync(d_woff.p, f.woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+      S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)f.stride * nw, s));
       S_TRY(amod_launch_window(pp.y(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
                                d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
       int rc = amod_reserve(ctx, cfg, nw, maxlen);
       if (rc) return rc;
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
-                              nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), stride, 0, s);
+                              nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), f.stride, 0, s);
       if (rc) return rc;
-      S_TRY(hipMemcpyAsync(c.w_res_h.p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
-      S_TRY(hipMemcpyAsync(c.w_pay_h.p, d_pay.p, (size_t)stride * nw, hipMemcpyDeviceToHost, s));
-      S_TRY(hipStreamSynchronize(s));
+      S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
+      S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, s));
     }
-    res.resize(b - a);
-    for (size_t i = a; i < b; ++i) {
-      amod_result &o = res[i - a];
-      if (slot[i - a] < 0) {
+    S_TRY(hipEventRecord(c.w_done[k], s));
+    f.live = true;
+    t_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return AMOD_SUCCESS;
+  }
+  // waits for batch k; res / row() then describe it
+  int collect(amod_ctx *ctx, const Prepass &pp, int k) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Flight &f = fl[k];
+    StreamCache &c = *pp.c;
+    S_TRY(hipEventSynchronize(c.w_done[k]));
+    f.live = false;
+    const amod_result *rh = c.w_res_h[k].as<amod_result>();
+    ph = c.w_pay_h[k].as<uint8_t>();
+    stride = f.stride;
+    if (zero_row.size() != (size_t)stride) zero_row.assign((size_t)stride, 0);
+    slot = f.slot;
+    res.resize(f.b - f.a);
+    for (size_t i = 0; i < res.size(); ++i) {
+      amod_result &o = res[i];
+      if (slot[i] < 0) {
         o = amod_result{};
         o.status = AMOD_E_STREAM_LOST; o.preamble_idx = -1; o.coarse_idx = -1; o.frame_type = -1;
       } else {
-        o = rh[slot[i - a]];
+        o = rh[slot[i]];
       }
     }
     t_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return AMOD_SUCCESS;
+  }
+  // a batch launched but not collected (dropped: a metadata frame changed what follows) is
+  // waited for, so its buffers can be reused
+  int drain(amod_ctx *ctx, const Prepass &pp) {
+    for (int k = 0; k < 2; ++k)
+      if (fl[k].live) { S_TRY(hipEventSynchronize(pp.c->w_done[k])); fl[k].live = false; }
+    return AMOD_SUCCESS;
+  }
+  int run(amod_ctx *ctx, const amod_cfg *cfg, const Prepass &pp, const std::vector<FrameEv> &fr, size_t a, size_t b,
+          hipStream_t s) {
+    const int rc = launch(ctx, cfg, pp, fr, a, b, s, 0);
+    return rc ? rc : collect(ctx, pp, 0);
   }
 };
 
@@ -1083,6 +1208,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   amod_stream_stats stt{};
   Prepass pp;
   pp.sparse = !getenv("AMOD_STREAM_FULLCOPY"); // (diagnostics: the whole cleaned stream to the host)
+  pp.dev_metrics = !getenv("AMOD_NO_GAP_SCAN");  // refinements of the gap scans' detections on the GPU
   {
     const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s, device);
     if (rc) return rc;
@@ -1111,9 +1237,18 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   // follows (its `after` updated), or -1
   auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
     changed = -1;
-    for (size_t c0 = a; c0 < b; c0 += kBatch) {
+    // batch j decodes (buffer set j & 1) while the host dispatches batch j - 1
+    if (a < b) {
+      const int rc = wd.launch(ctx, cfg, pp, fr, a, std::min(b, a + (size_t)kBatch), s, 0);
+      if (rc) return rc;
+    }
+    for (size_t c0 = a, j = 0; c0 < b; c0 += kBatch, ++j) {
       const size_t c1 = std::min(b, c0 + (size_t)kBatch);
-      const int rc = wd.run(ctx, cfg, pp, fr, c0, c1, s);
+      if (c1 < b) {
+        const int rc = wd.launch(ctx, cfg, pp, fr, c1, std::min(b, c1 + (size_t)kBatch), s, (int)((j + 1) & 1));
+        if (rc) return rc;
+      }
+      const int rc = wd.collect(ctx, pp, (int)(j & 1));
       if (rc) return rc;
       for (size_t i = c0; i < c1; ++i) {
         FrameEv &ev = fr[i];
@@ -1137,7 +1272,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
           const bool chg = upd.meta_received != ev.after.meta_received ||
                            (upd.meta_received && upd.chunk_size != ev.after.chunk_size);
           ev.after = upd;
-          if (chg) { changed = (int64_t)i; return AMOD_SUCCESS; }
+          if (chg) { changed = (int64_t)i; return wd.drain(ctx, pp); }
         } else if (r.frame_type == 0xFF) {
           const int c = amod_asm_chunk(assembler, r.seq_num, sl + r.data_off, r.data_len, r.crc_valid);
           if (c < 0) return amod_ctx_fail(ctx, "assembler store", c);
@@ -1173,15 +1308,18 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
         grc = pp.gap_scan_finish();
         if (grc) return amod_ctx_fail(ctx, "gap scan", grc);
         if (!pp.gaps.empty()) proto.gaps = &pp.gaps;
+        if (!pp.refs.empty()) proto.refs = &pp.refs;
         if (getenv("AMOD_STREAM_DIAG")) {
           int64_t smax = 0, ssum = 0;
           for (auto &g : pp.gaps) { smax = std::max(smax, g.scanned); ssum += g.scanned; }
-          fprintf(stderr, "[stream] sparse setup %.3f ms, then gap scan: %zu records (%lld positions, longest %lld), +%.3f ms\n",
-                  std::chrono::duration<double, std::milli>(tg1 - tg0).count(), pp.gaps.size(), (long long)ssum,
+          fprintf(stderr, "[stream] sparse setup %.3f ms (marks %.3f, index %.3f, pointers %.3f, copies %.3f), then gap scan: "
+                  "%zu records (%lld positions, longest %lld), +%.3f ms\n",
+                  std::chrono::duration<double, std::milli>(tg1 - tg0).count(), pp.setup_ms[0], pp.setup_ms[1],
+                  pp.setup_ms[2], pp.setup_ms[3], pp.gaps.size(), (long long)ssum,
                   (long long)smax, std::chrono::duration<double, std::milli>(clk::now() - tg1).count());
         }
         if (sp_ok) {
-          proto.gptr = pp.gptr.get(); proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
+          proto.gptr = pp.gptr; proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
         }
       }
       tr = run_parallel(proto, st, nblocks, nthreads, fine_host);
@@ -1221,8 +1359,10 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     stt.final_scan_pos = final_state.ac_pos;
     stt.fine_host_positions = fine_host;
     if (getenv("AMOD_STREAM_DIAG"))
-      fprintf(stderr, "[stream] sparse copy: %lld of %lld granules packed, %lld fetched on demand, full copy %d\n",
-              (long long)pp.npacked, (long long)pp.ng, (long long)pp.fallbacks.load(), (int)pp.full_started);
+      fprintf(stderr, "[stream] sparse copy: %lld of %lld granules packed, %lld fetched on demand (%.3f ms), piece waits "
+              "%.3f ms, full copy %d; fine positions on the host %lld\n",
+              (long long)pp.npacked, (long long)pp.ng, (long long)pp.fallbacks.load(), pp.fetch_us.load() * 1e-3,
+              pp.wait_us.load() * 1e-3, (int)pp.full_started, (long long)fine_host);
     stt.t_decode_ms = wd.t_ms;
     stt.t_total_ms = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
     stt.t_host_ms = std::chrono::duration<double, std::milli>(clk::now() - t_gpu_pre).count() - wd.t_ms;

@@ -131,7 +131,10 @@ def test_c4_shaped_stream_round_trip():
     assert frames["pos"].tolist() == [int(offs[0]) + pre_meta] + [int(o) + pre_chunk for o in offs[1:]]
     assert (frames["result"]["status"] == 0).all() and (frames["result"]["crc_valid"] == 1).all()
     assert frames["result"]["seq_num"][1:].tolist() == list(range(n))
-    assert stats["frames_decoded"] == n + 1 and stats["frame_errors"] == 0 and stats["ema_chunks_fixed"] == 0
+    assert stats["frames_decoded"] == n + 1 and stats["frame_errors"] == 0
+    # (the DC removal's short warm-up leaves some chunk chains unconverged; the fix passes
+    # recompute them: a cost, never a different sample — test_gpu_stream_ema pins that)
+    assert stats["ema_chunks_fixed"] < len(x) // 1024 // 2
     assert asm.is_complete() and asm.assemble_file() == data
 
 
