@@ -489,6 +489,8 @@ hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int s
 hipError_t amod_launch_gap_scan(const float *y, int64_t n, int64_t lo, const int64_t *first, const double2 *barg,
                                 int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks, int max_blocks,
                                 amod::GapScan *out, hipStream_t s);
+hipError_t amod_launch_ranges(const uint8_t *hot, int64_t nhot, int32_t *wg, int64_t *first, int64_t *count,
+                              hipStream_t s);
 hipError_t amod_launch_gap_refine(amod::GapScan *g, int nrec, int64_t lo, const int64_t *first, const int64_t *base,
                                   const int64_t *count, int nranges, const double *metric, int64_t radius, hipStream_t s);
 hipError_t amod_launch_window(const float *y, int64_t n, const int64_t *pos, const int32_t *len, const int64_t *woff,

@@ -339,6 +339,65 @@ __global__ __launch_bounds__(256) void k_sc_screen(const double2 *__restrict__ z
   hot[b] = (ra > 0.001 && rb > 0.001 && (p * p) / (ra * rb) >= (double)thresh) ? 1 : 0;
 }
 
+// Fine ranges from the hot flags (the host's merge of [32 b - 448, 32 b + 479] over hot
+// blocks b, in order): two hot blocks at most kMergeGap apart share a range, so a range
+// starts at a hot block with no hot block in the kMergeGap before it and ends at one with
+// none in the kMergeGap after it. (1) starts per workgroup, (2) their exclusive scan
+// (one workgroup), (3) each start's range written at its rank: ranges in stream order.
+constexpr int kMergeGap = 29; // 32 (b - b') <= 2 * 448 + 32
+__device__ __forceinline__ bool range_start(const uint8_t *hot, int64_t nhot, int64_t b) {
+  if (b >= nhot || !hot[b]) return false;
+  for (int64_t j = max<int64_t>(0, b - kMergeGap); j < b; ++j)
+    if (hot[j]) return false;
+  return true;
+}
+__global__ __launch_bounds__(256) void k_range_count(const uint8_t *__restrict__ hot, int64_t nhot,
+                                                     int32_t *__restrict__ wg_count) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = __popcll(__ballot(range_start(hot, nhot, b)));
+  __shared__ int wc[4];
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+// in place: wg_count[i] -> sum of wg_count[0 .. i); wg_count[nwg] = the total (one workgroup)
+__global__ __launch_bounds__(1024) void k_range_scan(int32_t *__restrict__ wg_count, int nwg) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, per = (nwg + 1023) / 1024, a = min(nwg, t * per), b = min(nwg, a + per);
+  int sum = 0;
+  for (int i = a; i < b; ++i) sum += wg_count[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) { // inclusive scan of the partials
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = a; i < b; ++i) { const int v = wg_count[i]; wg_count[i] = run; run += v; }
+  if (t == 1023) wg_count[nwg] = part[1023];
+}
+__global__ __launch_bounds__(256) void k_range_write(const uint8_t *__restrict__ hot, int64_t nhot,
+                                                     const int32_t *__restrict__ wg_off, int64_t *__restrict__ first,
+                                                     int64_t *__restrict__ count) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool st = range_start(hot, nhot, b);
+  const unsigned long long m = __ballot(st);
+  __shared__ int wc[4];
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (!st) return;
+  const int w = threadIdx.x >> 6;
+  int off = wg_off[blockIdx.x] + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1));
+  for (int k = 0; k < w; ++k) off += wc[k];
+  int64_t last = b; // the range's last hot block: none in the kMergeGap after it
+  for (int64_t j = b + 1; j < nhot && j - last <= kMergeGap; ++j)
+    if (hot[j]) last = j;
+  first[off] = 32 * b - 448;
+  count[off] = 32 * (last - b) + 32 + 2 * 448;
+}
+
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
 // base[r] + j; one lane per position
 constexpr int kFineMaxSym = 1024; // symbol_len bound of k_fine's LDS window (presets: 576 .. 768)
@@ -378,7 +437,7 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
     // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
     const double denom = sqrt(se * pre1_energy);
     const double v = denom > 0.001 ? corr / denom : __builtin_nan("");
-    out[base[r] + j] = v;
+    if (out) out[base[r] + j] = v;         // (mapped host memory: the host's lookups)
     if (out_dev) out_dev[base[r] + j] = v; // (the device copy k_gap_refine reads)
     if (v == v) m = v;
   }
@@ -731,6 +790,17 @@ hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double
   if (n % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(amod::k_sc_blocks, dim3((unsigned)((32 * nblk + 1023) / 1024)), dim3(256), 0, s, y, n, nblk, ze);
   hipLaunchKernelGGL(amod::k_sc_screen, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, ze, nblk, thresh, hot);
+  return hipGetLastError();
+}
+// the fine ranges of the hot flags: first[r], count[r] for r < *nranges (wg: nhot / 256 + 2
+// ints of scratch); first / count hold max_ranges entries
+hipError_t amod_launch_ranges(const uint8_t *hot, int64_t nhot, int32_t *wg, int64_t *first, int64_t *count,
+                              hipStream_t s) {
+  if (nhot <= 0) return hipMemsetAsync(wg, 0, sizeof(int32_t), s);
+  const int nwg = (int)((nhot + 255) / 256);
+  hipLaunchKernelGGL(amod::k_range_count, dim3((unsigned)nwg), dim3(256), 0, s, hot, nhot, wg);
+  hipLaunchKernelGGL(amod::k_range_scan, dim3(1), dim3(1024), 0, s, wg, nwg);
+  hipLaunchKernelGGL(amod::k_range_write, dim3((unsigned)nwg), dim3(256), 0, s, hot, nhot, wg, first, count);
   return hipGetLastError();
 }
 hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int sym, double pre1_energy,

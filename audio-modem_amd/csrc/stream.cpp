@@ -88,6 +88,7 @@ struct FineTable {
   const double *metric = nullptr; // k_fine's metrics (pinned), NaN where the reference skips
   // refine walks consecutive positions: `last` (the caller's cursor) is tried first
   bool lookup(int64_t d, double &m, size_t &last) const {
+    if (!metric) return false; // (the metrics stayed on the device)
     size_t r = last;
     if (r >= first.size() || d < first[r] || d >= first[r] + count[r]) {
       auto it = std::upper_bound(first.begin(), first.end(), d);
@@ -573,7 +574,7 @@ struct Pinned {
 // device and pinned buffers of the streaming receiver, kept per context (grow-only)
 struct StreamCache {
   DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
-  DBuf d_pre1, d_first, d_base, d_count, d_out, d_metric;
+  DBuf d_pre1, d_first, d_base, d_count, d_out, d_metric, d_rwg;
   // window decoder: two batches in flight (one decoding while the host dispatches the other)
   DBuf w_pos[2], w_len[2], w_woff[2], w_win[2], w_res[2], w_pay[2];
   hipEvent_t w_done[2] = {};
@@ -619,7 +620,15 @@ struct Prepass {
   int64_t lo = 0, n = 0, fixed = 0;
   bool dev_metrics = false; // k_fine also keeps its metrics on the device (k_gap_refine reads them)
   int64_t nmetric = 0;
-  std::vector<double> ema_end; // EMA state after each k_ema chunk (true states)
+  int64_t nhot = 0;            // 32-sample blocks screened (hot flags on the device)
+  // the EMA state after local chunk k (its true end state, read from the device)
+  double ema_end(amod_ctx *ctx, int64_t k) const {
+    double v = NAN;
+    if (k >= 0 && k < (n + kEmaChunk - 1) / kEmaChunk)
+      (void)hipMemcpy(&v, c->d_end.as<double>() + k, sizeof(double), hipMemcpyDeviceToHost);
+    (void)ctx;
+    return v;
+  }
   double t_ema = 0, t_fine = 0;
   const float *y() const { return c->d_y.as<float>(); }
   std::function<void(int64_t)> wait_fn = [this](int64_t g) { wait_y(g); };
@@ -788,6 +797,11 @@ struct Prepass {
     if (gap_launched) { // (the fine ranges: hot blocks +- 448 samples, merged)
       for (size_t r = 0; r < ft.first.size(); ++r) reg.push_back({ft.first[r] - lo + 448, ft.first[r] - lo + ft.count[r] - 448});
     } else {
+      if (c->hot_h.alloc((size_t)std::max<int64_t>(nhot, 1)) != hipSuccess ||
+          (nhot && hipMemcpy(c->hot_h.p, c->d_hot.p, (size_t)nhot, hipMemcpyDeviceToHost) != hipSuccess)) {
+        start_full();
+        return false;
+      }
       const uint8_t *hot = c->hot_h.as<uint8_t>();
       for (int64_t b = 0; b < n / 32; ++b) {
         if (!hot[b]) continue;
@@ -893,14 +907,19 @@ struct Prepass {
                           c->d_fixed.as<unsigned long long>(), s));
     S_TRY(hipEventRecord(ev[1], s));
     S_TRY(amod_launch_sc_screen(c->d_y.as<float>(), n, 0.25f, c->d_ze.as<double2>(), c->d_hot.as<uint8_t>(), s));
-    const int64_t nhot = n / 32;
-    S_TRY(c->hot_h.alloc((size_t)std::max<int64_t>(nhot, 1)));
-    const uint8_t *const hot = c->hot_h.as<uint8_t>();
-    if (nhot) S_TRY(hipMemcpyAsync(c->hot_h.p, c->d_hot.p, (size_t)nhot, hipMemcpyDeviceToHost, s));
-    ema_end.resize(nchunks);
+    // the fine ranges (every position within 448 samples of a hot block), built on the GPU
+    nhot = n / 32;
+    const int64_t max_ranges = nhot / (1 + 29) + 2; // starts are more than 29 blocks apart
+    S_TRY(c->d_rwg.alloc(sizeof(int32_t) * (size_t)(nhot / 256 + 4)));
+    S_TRY(c->d_first.alloc(sizeof(int64_t) * (size_t)max_ranges));
+    S_TRY(c->d_count.alloc(sizeof(int64_t) * (size_t)max_ranges));
+    S_TRY(amod_launch_ranges(c->d_hot.as<uint8_t>(), nhot, c->d_rwg.as<int32_t>(), c->d_first.as<int64_t>(),
+                             c->d_count.as<int64_t>(), s));
+    int32_t nr_dev = 0;
+    S_TRY(hipMemcpyAsync(&nr_dev, c->d_rwg.as<int32_t>() + (nhot > 0 ? (nhot + 255) / 256 : 0), sizeof(int32_t),
+                         hipMemcpyDeviceToHost, s));
     unsigned long long fx = 0;
     S_TRY(hipMemcpyAsync(&fx, c->d_fixed.p, 8, hipMemcpyDeviceToHost, s));
-    S_TRY(hipMemcpyAsync(ema_end.data(), c->d_end.p, sizeof(double) * nchunks, hipMemcpyDeviceToHost, s));
     // the cleaned stream to the host (pinned) on a second stream, in pieces, under the
     // screening / fine-sum work and the receiver's first segments
     S_TRY(c->yh.alloc(sizeof(float) * (size_t)std::max<int64_t>(n, 1)));
@@ -927,49 +946,36 @@ struct Prepass {
     S_TRY(hipStreamSynchronize(s));
     const auto tq1 = std::chrono::steady_clock::now();
     fixed = (int64_t)fx;
-    // fine ranges (local positions): every position within 448 samples of a hot block
-    const int64_t pad = 448;
-    int64_t rlo = -1, rhi = -1, total = 0;
-    std::vector<int64_t> first_loc;
-    auto flush = [&]() {
-      first_loc.push_back(rlo); ft.first.push_back(lo + rlo); ft.count.push_back(rhi - rlo + 1);
-      ft.base.push_back(total);
-      total += rhi - rlo + 1;
-    };
-    bool open = false;
-    for (int64_t b = 0; b < nhot; ++b) {
-      if ((b & 63) == 0 && b + 64 <= nhot) { // 64 quiet blocks at a time
-        uint64_t w[8];
-        memcpy(w, hot + b, 64);
-        if (!((w[0] | w[1]) | (w[2] | w[3]) | (w[4] | w[5]) | (w[6] | w[7]))) { b += 63; continue; }
-      }
-      if (!hot[b]) continue;
-      const int64_t za = 32 * b - pad, zb = 32 * b + 31 + pad;
-      if (open && za <= rhi + 1) rhi = std::max(rhi, zb);
-      else { if (open) flush(); rlo = za; rhi = zb; open = true; }
+    const int nr = nr_dev;
+    std::vector<int64_t> first_loc((size_t)nr);
+    ft.first.resize((size_t)nr); ft.count.resize((size_t)nr); ft.base.resize((size_t)nr);
+    if (nr) {
+      S_TRY(hipMemcpyAsync(first_loc.data(), c->d_first.p, sizeof(int64_t) * nr, hipMemcpyDeviceToHost, s));
+      S_TRY(hipMemcpyAsync(ft.count.data(), c->d_count.p, sizeof(int64_t) * nr, hipMemcpyDeviceToHost, s));
+      S_TRY(hipStreamSynchronize(s));
     }
-    if (open) flush();
-    // k_fine writes its metrics straight into mapped host memory (no copy queued behind
-    // the cleaned stream's transfer)
-    S_TRY(c->metric_h.alloc(sizeof(double) * (size_t)std::max<int64_t>(total, 1), true));
-    ft.metric = c->metric_h.as<double>();
+    int64_t total = 0;
+    for (int r = 0; r < nr; ++r) { ft.first[(size_t)r] = lo + first_loc[(size_t)r]; ft.base[(size_t)r] = total; total += ft.count[(size_t)r]; }
+    // without the GPU refinements k_fine writes its metrics straight into mapped host memory
+    // for the host's lookups (no copy queued behind the cleaned stream's transfer); with them
+    // they stay on the device, and the few refinements left to the host correlate there
+    ft.metric = nullptr;
+    if (!dev_metrics) {
+      S_TRY(c->metric_h.alloc(sizeof(double) * (size_t)std::max<int64_t>(total, 1), true));
+      ft.metric = c->metric_h.as<double>();
+    }
     if (total) {
       std::vector<float> p1(cfg->symbol_len);
       if (amod_preamble1(cfg, p1.data()) != AMOD_SUCCESS) return amod_ctx_fail(ctx, "invalid amod_cfg", AMOD_ERR_ARG);
       double p1e = 0.0; // this.pre1Energy (app.js:744-745)
       for (float v : p1) p1e += (double)v * (double)v;
-      const int nr = (int)first_loc.size();
       nmetric = total;
       if (dev_metrics) S_TRY(c->d_metric.alloc(sizeof(double) * (size_t)total));
       std::vector<double> p1d(p1.begin(), p1.end()); // (exact: k_fine's fma operand)
       S_TRY(c->d_pre1.alloc(sizeof(double) * p1.size()));
-      S_TRY(c->d_first.alloc(sizeof(int64_t) * nr));
       S_TRY(c->d_base.alloc(sizeof(int64_t) * nr));
-      S_TRY(c->d_count.alloc(sizeof(int64_t) * nr));
       S_TRY(hipMemcpyAsync(c->d_pre1.p, p1d.data(), sizeof(double) * p1d.size(), hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(c->d_first.p, first_loc.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
-      S_TRY(hipMemcpyAsync(c->d_count.p, ft.count.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
       nbx = (int)((maxc + 255) / 256);
       nfr = nr;
@@ -978,7 +984,7 @@ struct Prepass {
         const int k = std::min(65535, nr - r0);
         S_TRY(amod_launch_fine(c->d_y.as<float>(), n, c->d_pre1.as<double>(), cfg->symbol_len, p1e,
                                c->d_first.as<int64_t>() + r0, c->d_base.as<int64_t>() + r0,
-                               c->d_count.as<int64_t>() + r0, k, maxc, (double *)c->metric_h.dp,
+                               c->d_count.as<int64_t>() + r0, k, maxc, dev_metrics ? nullptr : (double *)c->metric_h.dp,
                                dev_metrics ? c->d_metric.as<double>() : nullptr,
                                c->d_barg.as<double2>() + (int64_t)r0 * nbx, s));
       }
@@ -1406,7 +1412,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
   if (ema) {
     auto state_after = [&](int64_t g) -> double { // EMA state after stream sample g (a chunk end)
       const int64_t k = (g + 1 - lo) / kEmaChunk - 1;
-      return (k >= 0 && k < (int64_t)pp.ema_end.size() && (g + 1 - lo) % kEmaChunk == 0) ? pp.ema_end[k] : NAN;
+      return (g + 1 - lo) % kEmaChunk == 0 ? pp.ema_end(ctx, k) : NAN;
     };
     ema[0] = own_lo > lo ? state_after(own_lo - 1) : NAN;
     ema[1] = own_hi > lo ? state_after(own_hi - 1) : NAN;
