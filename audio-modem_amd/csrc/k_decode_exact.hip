@@ -21,7 +21,7 @@ namespace amod {
 namespace {
 
 constexpr int XT = 256;     // threads per workgroup
-constexpr int CH = 4096;    // sample chunk staged in LDS for the sequential lanes
+constexpr int CH = 3072;    // sample chunk staged in LDS (XSmem <= 40 KB: four workgroups per CU)
 
 constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH doubles overlay the FFT arrays)
 #ifndef AMOD_SEG_G
@@ -29,7 +29,7 @@ constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH double
 #endif
 constexpr int kSegG = AMOD_SEG_G; // samples per certified segment of the mean (at least)
 
-struct alignas(16) XSmem {
+struct alignas(16) XSmem { // (static_assert below: four per CU fit the 160 KB of LDS)
   float chunk[CH + 520];
   union {
     struct {
@@ -47,6 +47,8 @@ struct alignas(16) XSmem {
   float xmn, xmx;
   int coarse, start, status, nonfin;
 };
+
+static_assert(sizeof(XSmem) <= 40 * 1024, "list A's exact workgroup must fit beside three k_demod ones");
 
 __device__ __forceinline__ double or_zero(float v) { return (v != v || v == 0.0f) ? 0.0 : (double)v; } // `x || 0`
 __device__ __forceinline__ int rev9(int i) { return (int)(__brev((unsigned)i) >> 23); }
@@ -183,11 +185,8 @@ __device__ int crosscorr_detect(const float *xs, int N, const DevCfg &cfg, XSmem
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-// WPE 3: list A's instance, capped at 168 VGPRs so its waves fit beside k_demod (45 VGPRs
-// spill to scratch); WPE 2: list B's, which runs alone after k_demod (222 VGPRs, no
-// scratch: its launch skips the scratch setup even when the list is empty)
-template <int WPE>
-__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_decode_exact(const DevCfg cfg, const DevWork w) {
+// the exact replica of one listed frame per workgroup iteration (kernels below)
+__device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) {
   __shared__ XSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // listed frames are latency-bound chains (sequential recurrences) that run beside the
@@ -208,6 +207,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     init_result(r);
     r.flags = flags0 | AMOD_FLAG_EXACT;
     XSTAMP(8);
+    if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + 1] = __builtin_amdgcn_s_memrealtime(); // (100 MHz)
     {
       const int64_t need_bits = (int64_t)(N / SYM) * cfg.ndata * cfg.bps;
       if ((int64_t)N > w.xs_stride || 2 * ((need_bits + 31) / 32) + 16 > w.bits_stride) {
@@ -426,23 +426,94 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           const DetRec dr = w.det[f];
           if (dr.sc_lo >= 0 && dr.sc_hi >= dr.sc_lo) { d_lo = dr.sc_lo; d_hi = min(dr.sc_hi, end); }
         }
+        if (w.stamps && tid == 0) // (diagnostics: the recurrence's range, slot 7)
+          w.stamps[(int64_t)f * 32 + 7] = ((unsigned long long)(uint32_t)d_lo << 32) | (uint32_t)d_hi;
         // lanes 0, 1, 2 carry the three independent recurrences p, ra, rb (each lane its
         // own array of increments -> states), so one instruction stream advances all three
         double acc = 0.0;
         double bm = 0.0;                     // > best = 0 like the reference's first test
         int bi = -1;
         double *const tp = sm.sc, *const tra = sm.sc + SCH, *const trb = sm.sc + 2 * SCH;
-        for (int c0 = 0; c0 <= d_hi; c0 += SCH) {
+        if (tid < 3) { // P(0), Ra(0), Rb(0) (modem.js:292-298), one sum per lane
+          for (int m = 0; m < half; ++m) {
+            const double a = xs[m], b = xs[m + half];
+            acc += tid == 0 ? a * b : (tid == 1 ? a * a : b * b);
+          }
+        }
+        // positions [0, P1) before the hull: only the running sums matter, in a pipeline of
+        // half-chunks (HB positions): wave 0's lanes 0-2 add the increments of half h while
+        // waves 1-3 form those of half h + 1 in the other half of the buffer
+        constexpr int HB = SCH / 2;
+        const int P1 = (d_lo / HB) * HB;
+        if (P1 > 0) {
+          const int nh = P1 / HB;
+          // increments of half h's positions from samples (a_out, mid, b_in), into buffer h & 1
+          auto put = [&](int h, int k, float a_out_f, float mid_f, float b_in_f) {
+            double *const bp = sm.sc + (h & 1) * 3 * HB;
+            const int d = h * HB + k;
+            double ip = 0.0, ia = 0.0, ib = 0.0;
+            if (d < end) {
+              const double a_out = a_out_f, mid = mid_f, b_in = b_in_f;
+              ip = mid * b_in - a_out * mid;
+              ia = mid * mid - a_out * a_out;
+              ib = b_in * b_in - mid * mid;
+            }
+            bp[k] = ip; bp[HB + k] = ia; bp[2 * HB + k] = ib;
+          };
+          auto ld = [&](int d) { return d < N ? xs[d] : 0.f; };
+          for (int k = tid; k < HB; k += XT) put(0, k, ld(k), ld(k + half), ld(k + 2 * half));
+          // waves 1-3: thread tt forms positions tt, tt + 192, tt + 384 of a half; its samples
+          // for half h + 2 are loaded while half h + 1's increments are formed from registers
+          constexpr int PT = (HB + XT - 65) / (XT - 64);
+          const int tt = tid - 64;
+          float ra[PT], rm[PT], rb[PT];
+          auto load_half = [&](int h) {
+#pragma unroll
+            for (int j = 0; j < PT; ++j) {
+              const int k = tt + (XT - 64) * j, d = h * HB + k;
+              const bool v = k < HB;
+              ra[j] = v ? ld(d) : 0.f; rm[j] = v ? ld(d + half) : 0.f; rb[j] = v ? ld(d + 2 * half) : 0.f;
+            }
+          };
+          if (wave > 0 && nh > 1) load_half(1);
+          __syncthreads();
+          for (int h = 0; h < nh; ++h) {
+            if (wave == 0) {
+              if (lane < 3) {
+                const double2 *const v = reinterpret_cast<const double2 *>(sm.sc + (h & 1) * 3 * HB + lane * HB);
+                // (the next eight pairs are read while these are added: the adds are the chain)
+                double2 t[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) t[j] = v[j];
+                for (int k = 0; k < HB / 2; k += 8) {
+                  double2 u[8];
+                  const int kn = k + 8 < HB / 2 ? k + 8 : k;
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) u[j] = v[kn + j];
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) { acc += t[j].x; acc += t[j].y; }
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) t[j] = u[j];
+                }
+              }
+            } else {
+              if (h + 1 < nh) {
+#pragma unroll
+                for (int j = 0; j < PT; ++j) {
+                  const int k = tt + (XT - 64) * j;
+                  if (k < HB) put(h + 1, k, ra[j], rm[j], rb[j]);
+                }
+              }
+              if (h + 2 < nh) load_half(h + 2);
+            }
+            __syncthreads();
+          }
+        }
+        for (int c0 = P1; c0 <= d_hi; c0 += SCH) {
           const int n = min(SCH, d_hi + 1 - c0);
           const int ns = n + 2 * half; // samples [c0, c0 + n + 512) <= N
           for (int i = tid; i < ns; i += XT) sm.chunk[i] = c0 + i < N ? xs[c0 + i] : 0.f;
           __syncthreads();
-          if (c0 == 0 && tid < 3) { // P(0), Ra(0), Rb(0) (modem.js:292-298), one sum per lane
-            for (int m = 0; m < half; ++m) {
-              const double a = sm.chunk[m], b = sm.chunk[m + half];
-              acc += tid == 0 ? a * b : (tid == 1 ? a * a : b * b);
-            }
-          }
           for (int k = tid; k < n; k += XT) {
             double ip = 0.0, ia = 0.0, ib = 0.0;
             if (c0 + k < end) {
@@ -532,18 +603,51 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int lo = max(0, coarse - R), hi = min(N - SYM, coarse + R);
         double bm = -__builtin_inf();
         int bi = 0x7fffffff;
-        for (int d = lo + tid; d <= hi; d += XT) {
+        // the window [lo, hi + SYM) staged in LDS (the S-C chunk buffer is free now); f32 x
+        // f32 products are exact in double, so fma(s, q, corr) is the reference's
+        // corr + s * q with its one rounding
+        const int wn = hi + SYM - lo;
+        const bool staged = wn > 0 && wn + SYM <= CH + 520 && (SYM & 7) == 0;
+        auto offset = [&](const float *win, const float *q, int d) {
           double corr = 0.0, se = 0.0;
-          for (int i = 0; i < SYM; ++i) {
-            const double sv = xs[d + i];
-            corr += sv * (double)cfg.t.pre1[i];
-            se += sv * sv;
+          if (staged) { // LDS: the next eight samples and coefficients are read under these
+            float a[8], c[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { a[j] = win[j]; c[j] = q[j]; }
+            for (int i = 0; i < SYM; i += 8) {
+              float an[8], cn[8];
+              const int in = i + 8 < SYM ? i + 8 : i;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) { an[j] = win[in + j]; cn[j] = q[in + j]; }
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const double sv = a[j];
+                corr = __builtin_fma(sv, (double)c[j], corr);
+                se = __builtin_fma(sv, sv, se);
+              }
+#pragma unroll
+              for (int j = 0; j < 8; ++j) { a[j] = an[j]; c[j] = cn[j]; }
+            }
+          } else {
+            for (int i = 0; i < SYM; ++i) {
+              const double sv = win[i];
+              corr = __builtin_fma(sv, (double)q[i], corr);
+              se = __builtin_fma(sv, sv, se);
+            }
           }
           const double den = sqrt(se * cfg.te);
           if (den > 0.001) {
             const double m = corr / den;
             if (m > bm) { bm = m; bi = d; }
           }
+        };
+        if (staged) {
+          for (int i = tid; i < wn; i += XT) sm.chunk[i] = xs[lo + i];
+          for (int i = tid; i < SYM; i += XT) sm.chunk[wn + i] = cfg.t.pre1[i];
+          __syncthreads();
+          for (int d = lo + tid; d <= hi; d += XT) offset(sm.chunk + (d - lo), sm.chunk + wn, d);
+        } else {
+          for (int d = lo + tid; d <= hi; d += XT) offset(xs + d, cfg.t.pre1, d);
         }
         // argmax over lanes: highest metric, then lowest offset (strict '>' in order)
         for (int o = 32; o > 0; o >>= 1) {
@@ -587,6 +691,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       __syncthreads();
       continue;
     }
+    XSTAMP(15); // (diagnostics: detection done)
+    if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + 2] = __builtin_amdgcn_s_memrealtime();
     if (replay) {
       // detection replay: preambleIdx (and the coarse index and fine metric the result
       // reports) now equal the reference's; the demodulation is k_demod's, under its own
@@ -732,6 +838,20 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 }
 
+// list A's instance, capped at 128 VGPRs: k_demod's waves hold 128 each, so with one of
+// its workgroups per CU yielded an exact wave fits on every SIMD beside three of them
+// (at 168 it waited for k_demod's waves to retire); list B's runs alone after k_demod
+// (no cap: its launch skips the scratch setup even when the list is empty)
+template <int WPE> __global__ void k_decode_exact(const DevCfg cfg, const DevWork w);
+template <> __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_exact<4>(const DevCfg cfg,
+                                                                                                            const DevWork w) {
+  exact_body(cfg, w);
+}
+template <> __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_exact<2>(const DevCfg cfg,
+                                                                                                            const DevWork w) {
+  exact_body(cfg, w);
+}
+
 } // namespace
 } // namespace amod
 
@@ -739,7 +859,7 @@ extern "C" hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::Dev
                                         bool beside_demod) {
   if (nslots <= 0) return hipSuccess;
   if (beside_demod)
-    hipLaunchKernelGGL(amod::k_decode_exact<3>, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
+    hipLaunchKernelGGL(amod::k_decode_exact<4>, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
   else
     hipLaunchKernelGGL(amod::k_decode_exact<2>, dim3(nslots), dim3(amod::XT), 0, s, cfg, w);
   return hipGetLastError();

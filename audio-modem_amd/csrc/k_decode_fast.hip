@@ -1292,7 +1292,8 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   return r;
 }
 constexpr int CRC_ILP = 4;
-__device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *t4l) {
+__device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, uint32_t *t4l,
+                                               unsigned long long *stp = nullptr) {
   const int lane = wave_lane();
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(t.crc_s4);
@@ -1305,6 +1306,7 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const D
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+  if (stp && lane == 0) stp[30] = __builtin_amdgcn_s_memtime(); // (diagnostics: table staged)
   const uint32_t *const t4 = t4l;
   const int nch = (L + kCrcChunk - 1) / kCrcChunk;
   const uint32_t r0 = t.crc_pre[(kCrcChunk - (L & (kCrcChunk - 1))) & (kCrcChunk - 1)];
@@ -1327,6 +1329,7 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const D
         c[k] = t4[768 + (x & 0xFF)] ^ t4[512 + ((x >> 8) & 0xFF)] ^ t4[256 + ((x >> 16) & 0xFF)] ^ t4[x >> 24];
       }
     }
+    if (stp && lane == 0 && q0 == 0) stp[31] = __builtin_amdgcn_s_memtime(); // (chunk registers)
 #pragma unroll
     for (int k = 0; k < CRC_ILP; ++k) {
       const int q = q0 + 64 * k + lane;
@@ -1869,7 +1872,8 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           if (crc_len >= 0) {
             // the slice-by-4 table goes to this wave's exchange buffer (the frame's FFTs are done)
             r.actual_crc = crc_len <= kCrcMats * kCrcChunk
-                               ? wave_crc32(v, crc_len, cfg.t, reinterpret_cast<uint32_t *>(X2))
+                               ? wave_crc32(v, crc_len, cfg.t, reinterpret_cast<uint32_t *>(X2),
+                                            w.stamps ? w.stamps + (int64_t)f * 32 : nullptr)
                                : wave_crc32_long(v, crc_len, cfg.t);
             r.crc_valid = r.expected_crc == r.actual_crc;
           }

@@ -28,6 +28,7 @@ for s in "$@"; do
     c5stamps) run c5stamps 300 env AMOD_STAMPS=1 python bench.py --config c5 --snr 10 --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 3 --warmup 1;;
     emaprof) for W in ${WARMS:-16 4}; do mkdir -p gpurun_out/emaprof_w$W && cd gpurun_out/emaprof_w$W && AMOD_EMA_WARM=$W timeout -k 10 300 rocprofv3 --kernel-trace --stats -d . -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/ema_probe.py ${NCHUNKS:-32000} > log.txt 2>&1; rc=$?; cd $GRAFT_REPO_ROOT; echo "emaprof w$W rc=$rc"; [ $rc -eq 0 ] || exit $rc; done;;
     emapmc) mkdir -p gpurun_out/emapmc && cd gpurun_out/emapmc && AMOD_EMA_WARM=2 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_LDS --kernel-trace -d . -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/ema_probe.py 8000 > log.txt 2>&1; rc=$?; cd $GRAFT_REPO_ROOT; echo "emapmc rc=$rc"; [ $rc -eq 0 ] || exit $rc;;
+    chunks) for C in ${CHUNKS:-1 2 4}; do run chunks_$C$BPC 300 env AMOD_CHUNKS=$C ${BPC:+AMOD_DEMOD_BPC=$BPC} python bench.py --config ${PMCCFG:-c2} --legs none --stream-chunks 0 --cpu-frames -1 --no-e2e --steps 50 --warmup 5 || exit 1; done;;
     listpc) run listpc 120 rocprofv3 -L;;
     ab) run ab 600 python tools/ab.py $(for v in ${VARIANTS}; do echo audio-modem_amd/lib/variants/$v/libamodem.so; done);;
   esac

@@ -33,7 +33,7 @@ def main():
     n = env.lib.amod_debug_stamps(wl.dm.ctx, st.ctypes.data, st.size)
     st = st[:n].reshape(-1, 32).astype(np.int64)
     print(f"{conf}: {wl.F} frames x {int(wl.dlens[0])} samples")
-    for seq in ([16, 17, 18, 19, 20, 21], [22, 23, 24, 25, 26]):
+    for seq in ([16, 17, 18, 19, 20, 21], [22, 23, 24, 25, 26], [24, 30, 31, 25]):
         for a, b in zip(seq, seq[1:]):
             ok = (st[:, a] != 0) & (st[:, b] != 0)
             d = st[ok, b] - st[ok, a]

@@ -5,7 +5,10 @@ kernels' durations, dispatch by dispatch), counters.txt (per-kernel means of eve
 counter), traffic.json (FETCH_SIZE x 2 and WRITE_SIZE per launch against the
 algorithmic bytes of bench.json, per kernel and for the chain).
 
-usage: python tools/profile_summary.py gpurun_out/r02a profiles/r02
+usage: python tools/profile_summary.py gpurun_out/r03/c2 profiles/r03/c2
+(a step is one k_detect launch, or one k_chunk_prep launch in chunk mode; traffic.json
+entries of several workloads are merged into profiles/<round>/traffic.json by
+tools/profile_merge.py)
 """
 import collections
 import csv
@@ -33,7 +36,8 @@ def counters(path):
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "ktrace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    for f in ("bench.json", "bench_under_rocprof.json", "bench_c5_20db.json", "bench_c5_10db.json"):
+    for f in ("bench.json", "bench_under_rocprof.json", "bench_c5_20db.json", "bench_c5_10db.json",
+              "bench_stream_under_rocprof.json"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
     if os.path.exists(os.path.join(src, "ktrace_stream", "run_kernel_stats.csv")):
@@ -76,6 +80,7 @@ def main(src, dst):
     rf = bench.get("roofline", {})
     if rf.get("kernel") == "k_demod":
         alg["k_demod"] = rf["algorithmic_bytes"]
+    step_k = "k_detect" if "k_detect" in all_c else "k_chunk_prep"
     out = {"workload": bench["config"]["workload"], "frames": frames, "samples_per_frame": spf,
            "note": "FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads) and WRITE_SIZE, KiB -> bytes, per launch",
            "kernels": {}}
@@ -83,11 +88,11 @@ def main(src, dst):
     # the pass; k_demod runs twice a step (the main launch and the detection-replay list
     # launch, usually empty), k_decode_exact three times
     tot_r = tot_w = 0.0
-    steps_f = all_c.get("k_detect", {}).get("FETCH_SIZE", (0, 1, 0))[1]
-    steps_w = all_c.get("k_detect", {}).get("WRITE_SIZE", (0, 1, 0))[1]
+    steps_f = all_c.get(step_k, {}).get("FETCH_SIZE", (0, 1, 0))[1]
+    steps_w = all_c.get(step_k, {}).get("WRITE_SIZE", (0, 1, 0))[1]
     out["note"] = ("FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads) and WRITE_SIZE, KiB -> bytes, per step "
-                   "(all of a kernel's dispatches in the pass / its k_detect dispatches)")
-    for k in ("k_detect", "k_demod", "k_decode_exact", "k_corr_scan"):
+                   "(all of a kernel's dispatches in the pass / its %s dispatches)" % step_k)
+    for k in ("k_detect", "k_chunk_prep", "k_demod", "k_decode_exact", "k_corr_scan"):
         c = all_c.get(k, {})
         if "FETCH_SIZE" not in c:
             continue
@@ -100,7 +105,7 @@ def main(src, dst):
             e["algorithmic_bytes"] = alg[k]
             e["read_over_algorithmic"] = rd / alg[k]
         out["kernels"][k] = e
-        if k in ("k_detect", "k_demod", "k_decode_exact"):
+        if k in ("k_detect", "k_chunk_prep", "k_demod", "k_decode_exact"):
             tot_r += rd
             tot_w += wr
     out["chain"] = {"read_bytes": tot_r, "write_bytes": tot_w, "algorithmic_bytes": alg_chain,
