@@ -192,7 +192,12 @@ __device__ __forceinline__ void pk_dft8(f2v (&v)[8]) {
 // 72 q2 + l1 resp. 72 q2 + 9 p1 (q2 < 4 inside a group) are distinct mod 32.
 constexpr int XROW = 72;
 constexpr int XCH_F2 = 8 * XROW; // float2 per wave
-__device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 5) & 1) << 2); }
+// spec_idx: bits 4-5 of n XOR-ed into bits 1-2. The pass-3 store of lane (p1, q2) writes
+// n = q2 + 8 p1 (+ 64 p2): in each 16-lane ds_write_b64 group (q2 in {2g, 2g + 1}) the
+// float2 slots mod 16 are then (q2 ^ 2 (p1 >> 1)) + 8 (p1 & 1), all distinct (the
+// round-2 swizzle, bit 5 into bit 2, left them 2-way); the band reads (consecutive n)
+// stay 2-way only in groups that straddle a 16-bin boundary
+__device__ __forceinline__ int spec_idx(int n) { return n ^ (((n >> 4) & 3) << 1); }
 
 // One wave: 512-pt complex FFT of z (lane l holds z[l + 64 m] in v[m]); X[n] is
 // left in the wave's exchange buffer X2 at spec_idx(n).
@@ -1511,14 +1516,24 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     if (j == 0) { s1 = -2; s2 = 0; }
     else { s1 = 2 * j - 1; s2 = 2 * j < F.T ? 2 * j : -1; }
   };
+  // the job's samples as buffer loads: the frame is the resource (SGPRs), the window start
+  // the scalar offset, 4 lane the vector offset and 256 m the instruction's immediate, so a
+  // job's 16 loads cost no address arithmetic (global loads took three VALU each)
+  int lane4 = 4 * lane;
+  asm volatile("" : "+v"(lane4));
   auto job_loads = [&](const FrameS &F, int j, f2v (&r)[8]) {
     int s1, s2;
     job_syms(F, j, s1, s2);
     const int data0 = F.start + 3 * SYM;
     const int p1 = (s1 == -2 ? F.start + 2 * SYM : data0 + s1 * SYM) + CP;
     const int p2 = s2 >= 0 ? data0 + s2 * SYM + CP : p1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)F.X, (short)0, 0x7FFFFFFF, 0x00020000);
+    int vo = lane4;
+    asm volatile("" : "+v"(vo)); // (one offset register: 256 m goes to the immediate, not 8 hoisted copies)
 #pragma unroll
-    for (int m = 0; m < 8; ++m) r[m] = f2v{F.X[p1 + lane + 64 * m], F.X[p2 + lane + 64 * m]};
+    for (int m = 0; m < 8; ++m)
+      r[m] = f2v{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 256 * m, 4 * p1, 0)),
+                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 256 * m, 4 * p2, 0))};
   };
 
   float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
@@ -1776,12 +1791,17 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
+      // (lane i reads its NQ 16-byte pieces starting at piece i / (16 / NQ) mod NQ: the 16
+      // lanes of each ds_read_b128 group then cover 16 distinct 16-byte bank slots; in
+      // order, lanes i and i + 16 / NQ hit the same slot: 4-way for QPSK)
+      constexpr int NQ = DPW / 4;
+      const int rot = (ln / (16 / NQ)) & (NQ - 1);
       for (int i = ln; i < (gend - g0) / DPW; i += 64) {
         const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
         uint32_t word = 0u;
 #pragma unroll
-        for (int k = 0; k < DPW / 4; ++k) {
-          const uint4 t = q[k];
+        for (int k = 0; k < NQ; ++k) {
+          const uint4 t = q[(k + rot) & (NQ - 1)];
           word |= (t.x | t.y) | (t.z | t.w);
         }
         atomicOr(bits + wfirst + i, word);

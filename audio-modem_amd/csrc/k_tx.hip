@@ -120,6 +120,13 @@ __global__ __launch_bounds__(TX_WG) void k_tx(const DevCfg cfg, const DevTxWork 
 
   float lmax = 0.f;
   double2 *const X = xch[wave];
+  // exchange layout: element e at e ^ ((e >> 3) & 7) ^ (bit 6 of e, at bit 3). The first
+  // store (lane l writes elements 8 l .. 8 l + 7) put every lane of an 8-lane
+  // ds_write_b128 group on the same four banks (8-way: 101 M conflict cycles per C2 batch
+  // against 38 M LDS-active) and the pass-2 read (64 G + r + 8 m) was 2-way; with the
+  // swizzle every ds_write_b128 group covers 8 distinct 16-byte slots and every
+  // ds_read_b128 group 16 (all four exchange patterns conflict-free)
+  auto sw = [](int e) { return e ^ ((e >> 3) & 7) ^ (((e >> 6) & 1) << 3); };
   for (int s = wave; s < nsym; s += TX_NWAVE) {
     double2 v[8];
     // bitReverse: a[8g + m] = X[rev9(8g + m)] = X[64 rev3(m) + rev6(g)], lane g
@@ -127,18 +134,18 @@ __global__ __launch_bounds__(TX_WG) void k_tx(const DevCfg cfg, const DevTxWork 
     for (int m = 0; m < 8; ++m) v[m] = spec(s, 64 * rev3(m) + rev6(lane));
     stages3(v, 0, 1, tw); // halves 1, 2, 4 inside aligned groups of 8
 #pragma unroll
-    for (int m = 0; m < 8; ++m) X[8 * lane + m] = v[m];
+    for (int m = 0; m < 8; ++m) X[sw(8 * lane + m)] = v[m];
     __builtin_amdgcn_wave_barrier();
     const int G = lane >> 3, r = lane & 7; // halves 8, 16, 32: index 64 G + r + 8 m
 #pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = X[64 * G + r + 8 * m];
+    for (int m = 0; m < 8; ++m) v[m] = X[sw(64 * G + r + 8 * m)];
     stages3(v, r, 8, tw);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int m = 0; m < 8; ++m) X[64 * G + r + 8 * m] = v[m];
+    for (int m = 0; m < 8; ++m) X[sw(64 * G + r + 8 * m)] = v[m];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = X[lane + 64 * m]; // halves 64, 128, 256: index t + 64 m
+    for (int m = 0; m < 8; ++m) v[m] = X[sw(lane + 64 * m)]; // halves 64, 128, 256: index t + 64 m
     stages3(v, lane, 64, tw);
     __builtin_amdgcn_wave_barrier();
     // ifft scale 1/n (exact) and the f32 store of addCP: out[CP + i] = td[i],

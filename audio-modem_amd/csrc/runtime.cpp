@@ -271,6 +271,9 @@ struct amod_ctx {
   std::vector<void *> retired; // buffers a captured graph may reference (freed at close)
   // host-path staging
   DevBuf h_samples, h_off, h_len, h_res, h_payload, h_dbg;
+  // amod_decode_host's pipeline: the upload stream and one event per uploaded piece
+  hipStream_t up = nullptr;
+  std::vector<hipEvent_t> up_ev;
   std::mutex mu;
   DevBuf stamps;
   DevBuf tx_pkt, tx_meta, tx_out; // amod_tx_host staging
@@ -450,6 +453,7 @@ int64_t max_bits_for(const amod_cfg *c, int64_t max_len) {
 }
 
 constexpr int64_t kFastMaxLen = int64_t(1) << 18; // longest frame the fast path takes (k_detect moments in LDS)
+constexpr int64_t kUpPiece = int64_t(16) << 20; // amod_decode_host: samples per uploaded piece (64 MB)
 
 // capacities of one fast-path launch over frames of up to max_len samples
 struct ChainDims {
@@ -852,6 +856,11 @@ int amod_close(amod_ctx *ctx) {
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &ev : ctx->ev_used) for (auto &e : ev) (void)hipEventDestroy(e);
+  if (ctx->up) {
+    (void)hipStreamSynchronize(ctx->up);
+    (void)hipStreamDestroy(ctx->up);
+  }
+  for (hipEvent_t e : ctx->up_ev) (void)hipEventDestroy(e);
   for (void *p : ctx->retired) (void)hipFree(p);
   for (auto &ev : ctx->ev_free) for (auto &e : ev) (void)hipEventDestroy(e);
   delete ctx;
@@ -953,17 +962,54 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   HIP_TRY(ctx->h_res.ensure(sizeof(amod_result) * (size_t)nframes));
   HIP_TRY(ctx->h_payload.ensure((size_t)payload_stride * (size_t)nframes));
   hipStream_t s = ctx->stream;
-  if (nsamples) HIP_TRY(hipMemcpyAsync(ctx->h_samples.p, samples, sizeof(float) * nsamples, hipMemcpyHostToDevice, s));
+  if (!ctx->up) HIP_TRY(hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking));
   HIP_TRY(hipMemcpyAsync(ctx->h_off.p, offsets, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(ctx->h_len.p, lengths, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, s));
   // the fast kernel writes only the decoded prefix of each slot: hand back zeros past it
   HIP_TRY(hipMemsetAsync(ctx->h_payload.p, 0, (size_t)payload_stride * (size_t)nframes, s));
-  int64_t max_len = 0;
-  for (int32_t i = 0; i < nframes; ++i) max_len = std::max<int64_t>(max_len, lengths[i]);
-  int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p,
-                       (const int32_t *)ctx->h_len.p, nframes, (amod_result *)ctx->h_res.p,
-                       (uint8_t *)ctx->h_payload.p, payload_stride, options, s, nullptr, max_len);
-  if (rc) return rc;
+  // The samples go up in pieces on the upload stream while the context stream decodes the
+  // frames whose samples have all landed: frames in index order, when their ends never
+  // decrease (a batch cut from one recording), else every frame after the last piece. A
+  // pageable copy returns once its piece is staged, so the decodes enqueued after it run
+  // on the GPU during the next piece's upload.
+  bool mono = true;
+  for (int32_t i = 1; i < nframes && mono; ++i) mono = offsets[i] + lengths[i] >= offsets[i - 1] + lengths[i - 1];
+  int64_t piece = kUpPiece;
+  if (const char *e = getenv("AMOD_UP_PIECE")) piece = std::max<int64_t>(1024, atoll(e)); // tests: many pieces
+  const int64_t npiece = (nsamples + piece - 1) / piece;
+  while ((int64_t)ctx->up_ev.size() < std::max<int64_t>(npiece, 1)) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->up_ev.push_back(e);
+  }
+  HIP_TRY(hipEventRecord(ctx->up_ev[0], s)); // the upload stream starts after the memset's stream order
+  HIP_TRY(hipStreamWaitEvent(ctx->up, ctx->up_ev[0], 0));
+  int32_t a = 0; // the first frame not yet enqueued
+  for (int64_t p = 0; p <= npiece; ++p) {
+    int64_t covered = nsamples;
+    if (p < npiece) {
+      const int64_t lo = p * piece, n = std::min(piece, nsamples - lo);
+      HIP_TRY(hipMemcpyAsync((float *)ctx->h_samples.p + lo, samples + lo, sizeof(float) * n, hipMemcpyHostToDevice,
+                             ctx->up));
+      HIP_TRY(hipEventRecord(ctx->up_ev[p], ctx->up));
+      HIP_TRY(hipStreamWaitEvent(s, ctx->up_ev[p], 0));
+      covered = lo + n;
+      if (!mono && p + 1 < npiece) continue;
+    }
+    int32_t b = a;
+    int64_t max_len = 0;
+    while (b < nframes && (p == npiece || offsets[b] + lengths[b] <= covered)) max_len = std::max<int64_t>(max_len, lengths[b++]);
+    if (b == a) continue;
+    const int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p + a,
+                               (const int32_t *)ctx->h_len.p + a, b - a, (amod_result *)ctx->h_res.p + a,
+                               (uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride, payload_stride, options, s,
+                               nullptr, max_len);
+    if (rc) {
+      (void)hipStreamSynchronize(ctx->up);
+      return rc;
+    }
+    a = b;
+  }
   HIP_TRY(hipMemcpyAsync(results, ctx->h_res.p, sizeof(amod_result) * nframes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(payload, ctx->h_payload.p, (size_t)payload_stride * nframes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

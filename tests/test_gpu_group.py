@@ -51,3 +51,30 @@ def test_group_equals_single_context(devices):
     assert np.array_equal(pay, rpay)
     assert np.array_equal(pay2[inv], rpay)
     assert (ref["status"] == 0).all()
+
+
+@pytest.mark.parametrize("piece", [40_000, 333_333])
+def test_host_pipeline_pieces(monkeypatch, piece):
+    """amod_decode_host uploads the samples in pieces on its upload stream and decodes the
+    frames whose samples have landed while the next piece goes up (frames in index order
+    when their ends never decrease, else after the last piece). Any piece size gives the
+    one-piece result: frames in order, permuted, and overlapping slices of one buffer."""
+    cfg, x, offs, lens = _batch()
+    dm = amodem.Demodulator(0)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    monkeypatch.setenv("AMOD_UP_PIECE", str(piece))
+    rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    perm = np.random.default_rng(2).permutation(len(offs))
+    rec2, pay2 = dm.decode_batch(x, offs[perm], lens[perm], cfg=cfg)
+    # every frame twice, the copies interleaved (non-decreasing ends, shared samples)
+    dup = np.repeat(np.arange(len(offs)), 2)
+    rec3, pay3 = dm.decode_batch(x, offs[dup], lens[dup], cfg=cfg)
+    dm.close()
+    inv = np.argsort(perm)
+    for n in amodem.RESULT_DTYPE.names:
+        assert (rec[n] == ref[n]).all(), n
+        assert (rec2[n][inv] == ref[n]).all(), n
+        assert (rec3[n] == ref[n][dup]).all(), n
+    assert np.array_equal(pay, rpay) and np.array_equal(pay2[inv], rpay)
+    assert np.array_equal(pay3, rpay[dup])
+    assert (ref["status"] == 0).all()
