@@ -218,6 +218,35 @@ int amod_asm_chunk(amod_assembler *a, int32_t seq, const uint8_t *data, int32_t 
   return 1;
 }
 
+// amod_asm_chunk whose bytes the caller copies: when the chunk goes to the file-layout
+// arena, *dst is where its len bytes belong and nothing is copied here (the streaming
+// receiver copies a batch's chunks on several threads, before any other assembler call);
+// otherwise the chunk is stored as amod_asm_chunk does and *dst is null
+int amod_asm_chunk_at(amod_assembler *a, int32_t seq, const uint8_t *data, int32_t len, int32_t crc_valid,
+                      uint8_t **dst) {
+  if (!dst) return AMOD_ERR_ARG;
+  *dst = nullptr;
+  if (!a || len < 0) return AMOD_ERR_ARG;
+  const bool arena = a->dir.empty() && seq >= 0 && (size_t)seq < a->dense.size() && a->farena.p && len <= a->chunk_size;
+  if (!arena) return amod_asm_chunk(a, seq, data, len, crc_valid);
+  if (!a->has_bitmap) return 0;
+  if (seq >= a->total_chunks) return 0;
+  if (!crc_valid) {
+    ++a->crc_errors;
+    return 0;
+  }
+  const int64_t byte = (int64_t)seq >> 3;
+  const int bit = seq & 7;
+  const bool inside = byte >= 0 && byte < (int64_t)a->bitmap.size();
+  if (inside && (a->bitmap[byte] & (1u << bit))) return 0; // duplicate
+  if (inside) a->bitmap[byte] |= (uint8_t)(1u << bit);
+  ++a->received;
+  const int64_t off = (int64_t)seq * a->chunk_size;
+  a->dense[(size_t)seq] = amod_assembler::Loc{off, len, true};
+  *dst = a->farena.p + off;
+  return 1;
+}
+
 // StreamingReceiver._demodulateFrame's dispatch (app.js:926-961) over n decode results
 int amod_asm_feed(amod_assembler *a, const amod_result *res, const uint8_t *payload, int64_t stride, int32_t n) {
   if (!a || n < 0 || (n && (!res || !payload))) return AMOD_ERR_ARG;
