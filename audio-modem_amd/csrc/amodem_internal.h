@@ -37,7 +37,6 @@ struct DevTables {
   const double2 *tw_exact; // [511] per-stage recurrence twiddles (fftIterative 34-44)
   const float *known;      // [nband] CE symbol values ±1 (generateChannelEstSymbol)
   const int16_t *band_di;  // [nband] data-subcarrier index, -1 for pilots
-  const int16_t *band_ord; // [nband] band position of k_demod's lane-order index: data subcarriers, then pilots
   const uint32_t *crc_s4;  // [4][256] slice-by-4 CRC tables
   const uint32_t *crc_m1;  // [32][4][256] shift-by-(16*q) zero-byte operators, q<32
   const uint32_t *crc_m2;  // [32][4][256] shift-by-(512*q) operators, q<32

@@ -139,12 +139,6 @@ __device__ __forceinline__ uint32_t qpsk_bits(float cr, float ci) {
   const uint32_t a = __float_as_uint(cr), b = __float_as_uint(ci);
   return (b & 0x80000000u) | (((a ^ b) >> 31) << 30);
 }
-// s_bitreplicate_b64_b32: bit i of a at bits 2i and 2i + 1 (scalar unit; a wave-uniform)
-__device__ __forceinline__ uint64_t s_bitrep(uint32_t a) {
-  uint64_t r;
-  asm("s_bitreplicate_b64_b32 %0, %1" : "=s"(r) : "s"(a));
-  return r;
-}
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
@@ -1493,31 +1487,27 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   uint32_t *const voted = bits + w.vote_off;
   float2 *const X2 = xch[wave];
   const float2 *const tw1 = twl - 64, *const tw2 = twl + 7 * 64;
-  // Lane order: slot rr of lane l holds ordered index o = l + 64 rr, the data subcarriers
-  // in data-index order (o < ndata: o is the data index) and then the pilots
-  // (ndata <= o < nband; at most AMOD_MAX_PILOTS = 32, so one per lane at most). A ballot
-  // over a slot's data lanes is then a run of 64 consecutive data indices, no pilot gaps.
-  // Per slot: the byte offsets in xch of its bins k and 512 - k (16 bits each; the band
-  // reads take them per job), the CE sign (bit rr of kn_neg), the pilot's slot (prr)
-  const char *const xbase = reinterpret_cast<const char *>(&xch[0][0]);
-  uint32_t bin_pk[4];
-  uint32_t kn_neg = 0;
-  int prr = -1;
-  {
-    const uint32_t xb = (uint32_t)(wave * XCH_F2 * sizeof(float2));
+  // per-lane band facts for its 4 subcarriers b = lane + 64 rr: the bit offset of its
+  // decision in a symbol, di * BPS (-1 pilot, -2 none; di = data index)
+  // (two 16-bit fields per register: registers bound k_demod's occupancy)
+  uint32_t di_pk[2] = {0u, 0u};
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int o = lane + 64 * rr;
-      uint32_t pk = xb | (xb << 16);
-      if (rr < NS && o < nband) {
-        const int b = cfg.t.band_ord[o], k = sub_start + b;
-        pk = (xb + 8u * (uint32_t)spec_idx(k)) | ((xb + 8u * (uint32_t)spec_idx(kFft - k)) << 16);
-        kn_neg |= (uint32_t)(cfg.t.known[b] < 0.f) << rr;
-        if (o >= ndata) prr = rr;
-      }
-      bin_pk[rr] = pk;
-    }
+  for (int rr = 0; rr < 4; ++rr) {
+    const int di = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
+    const int dib = di >= 0 ? di * BPS : di;
+    di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
   }
+  auto dib_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
+  // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
+  // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
+  int prr = -1, npl = 0;
+#pragma unroll
+  for (int rr = 3; rr >= 0; --rr)
+    if (dib_of(rr) == -1) { prr = rr; ++npl; }
+  const bool pil_multi = __ballot(npl > 1) != 0;
+  uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(lane + 64 * rr < nband && cfg.t.known[lane + 64 * rr] < 0.f) << rr;
 
   // next frame on the demodulation path at or after wave-iteration k (frames last-first).
   // A static stride: the dispatcher places the grid's workgroups round-robin over the CUs,
@@ -1654,9 +1644,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
       // per-job copies of the lane's slot facts: their comparisons are made where they are
       // used instead of held as lane masks across the loop (SGPR pairs that spill)
-      asm volatile("" : "+v"(prr), "+v"(kn_neg), "+v"(bin_pk[0]), "+v"(bin_pk[1]), "+v"(bin_pk[2]), "+v"(bin_pk[3]));
-      // the band: slot rr of lane ln is ordered index o = ln + 64 rr, its bins k and 512 - k
-      // at the slot's packed offsets
+      asm volatile("" : "+v"(prr), "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg));
+      // the band: slot rr of lane ln is subcarrier b = ln + 64 rr, bins k = k0 + 64 rr and
+      // 512 - k (spec_idx(n +- 64) = spec_idx(n) +- 64: one base per side, immediate offsets)
+      const int k0 = sub_start + ln;
+      const f2v *const zkp = reinterpret_cast<const f2v *>(X2 + spec_idx(k0));
+      const f2v *const znp = reinterpret_cast<const f2v *>(X2 + spec_idx(kFft - 192 - k0));
       float zm = 0.f;
       // twice the reference's X1, X2 (Z = x1 + i x2: X1 = (Z[k] + conj Z[-k]) / 2,
       // X2 = (Z[k] - conj Z[-k]) / 2i); the 1/2 is folded into G below (exact: powers of 2)
@@ -1665,8 +1658,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       for (int rr = 0; rr < 4; ++rr) {
         x1[rr] = x2[rr] = f2v{0.f, 0.f};
         if (rr >= NS) continue; // no subcarrier in this slot
-        const f2v zk = *reinterpret_cast<const f2v *>(xbase + (bin_pk[rr] & 0xFFFFu));
-        const f2v zn = *reinterpret_cast<const f2v *>(xbase + (bin_pk[rr] >> 16));
+        const f2v zk = zkp[64 * rr], zn = znp[64 * (3 - rr)];
         f2v a = pk_add_conj(zk, zn), c = pk_add_swap_neg(zk, zn);
         float zz = fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y));
         if (rr == NS - 1) { // the last slot may be partly filled
@@ -1696,10 +1688,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           ch |= b < nband && !const1 && m2 < 4.f * 1e-6f;
           gl[rr] = g;
           if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
-          if (DBG && b < nband) {
-            const int bb = cfg.t.band_ord[b];
-            D->h_re[bb] = 0.5f * h.x; D->h_im[bb] = 0.5f * h.y;
-          }
+          if (DBG && b < nband) { D->h_re[b] = 0.5f * h.x; D->h_im[b] = 0.5f * h.y; }
         }
         gmax = wmax_nn(gm); // half of max |G|
         if (__ballot(ch)) wflags |= AMOD_FLAG_CHANNEL;
@@ -1714,12 +1703,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         e1[rr] = pk_cmul(x1[rr], g);
         e2[rr] = pk_cmul(x2[rr], g);
         em = fmaxf(em, fmaxf(fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y)));
-        const int o = ln + 64 * rr;
-        if (DBG && o < nband && (s1 == 0 || s2 == 0)) {
+        const int b = ln + 64 * rr;
+        if (DBG && b < nband && (s1 == 0 || s2 == 0)) {
           const bool one = s1 == 0;
           const f2v xx = one ? x1[rr] : x2[rr], ee = one ? e1[rr] : e2[rr];
           const bool c = one ? const1 : const2;
-          const int b = cfg.t.band_ord[o];
           D->x_re[b] = c ? 0.f : 0.5f * xx.x; D->x_im[b] = c ? 0.f : 0.5f * xx.y;
           D->eq_re[b] = c ? 0.f : ee.x; D->eq_im[b] = c ? 0.f : ee.y;
         }
@@ -1731,7 +1719,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       d = wmax_nn(d) + 1e-12f;
       const bool live1 = !ce && !const1, live2 = s2 >= 0 && !const2;
       // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405);
-      // per lane its pilot (one per lane at most: slot prr)
+      // per lane its pilot (at most one per lane: pil_multi takes the per-slot loop)
       float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f;
       int pc1 = 0, pc2 = 0, pflag1 = 0, pflag2 = 0;
       auto pilot = [&](bool pil, f2v q1e, f2v q2e) {
@@ -1749,7 +1737,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         pflag1 |= pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f;
         pflag2 |= pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f;
       };
-      {
+      if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
         f2v p1 = e1[0], p2 = e2[0];
 #pragma unroll
         for (int rr = 1; rr < 4; ++rr) {
@@ -1757,6 +1745,9 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           p2 = prr == rr ? e2[rr] : p2;
         }
         pilot(prr >= 0, p1, p2);
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) pilot(dib_of(rr) == -1, e1[rr], e2[rr]);
       }
       if (!KO(4)) { ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); }
       else { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
@@ -1774,139 +1765,71 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         if (s2 >= 0 && s2 < AMOD_DBG_SYMS) D->phase[s2] = const2 ? 0.f : ph2;
       }
       // a constant FFT window has an all-zero spectrum in the reference: every data
-      // subcarrier takes the origin decision (ties resolve to the first point)
+      // subcarrier takes the origin decision (ties resolve to the first point).
+      // The job's decisions (symbols s1, s2: a contiguous run [gs, ge) of the frame's
+      // decision sequence) go to the exchange buffer, free again once the band is in
+      // registers: one dword per decision (conflict-free ds_write_b32, consecutive data
+      // indices on consecutive lanes), its bits already at their place in the stream word
+      // (BPS divides 32, so a decision never straddles a word; v_lshrrev takes the
+      // position mod 32). Word wfirst + i of the stream is then the OR of dwords
+      // [DPW i, DPW i + DPW), one lane per word, one ds_or into the stream (the first
+      // word's top bits belong to the previous job).
+      constexpr int DPW = 32 / BPS; // decisions per stream word
+      uint32_t *const dec = reinterpret_cast<uint32_t *>(X2);
+      const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
+      const int wfirst = gs / DPW, g0 = wfirst * DPW, gend = (ge + DPW - 1) / DPW * DPW;
+      asm volatile("" ::: "memory"); // (the band reads above are float2 accesses of the same LDS)
+      if (ln < DPW) { // the first and last words' dwords outside [gs, ge)
+        if (g0 + ln < gs) dec[ln] = 0u;
+        if (ge + ln < gend) dec[ge - g0 + ln] = 0u;
+      }
+      const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
       int dflag1 = 0, dflag2 = 0;
-      if constexpr (MOD != AMOD_QAM16) {
-        // BPSK / QPSK: decisions straight to stream words. The lanes of data slot rr hold
-        // data indices 64 rr .. 64 rr + 63 in order, so the ballot of a decision bit is a run
-        // of the symbol's bit plane; the scalar unit interleaves the planes (QPSK:
-        // s_bitreplicate), bit-reverses them into the symbol's MSB-first words and funnels
-        // each to the symbol's stream position (one 64-bit shift); lane j receives word j
-        // (v_writelane) and one ds_or_b32 ORs the words into the stream. Round 2 stored one
-        // dword per decision and gathered them back (9-15 LDS instructions per job).
 #pragma unroll
-        for (int which = 0; which < 2; ++which) {
-          const int sidx = which == 0 ? s1 : s2;
-          if (sidx < 0 || KO(2)) continue; // wave-uniform
-          const bool live = which == 0 ? live1 : live2;
-          const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
-          const float tau = which == 0 ? tau1 : tau2;
-          const int sbase = sidx * per_sym, sh = sbase & 31, w0 = sbase >> 5;
-          const int nout = ((sbase + per_sym - 1) >> 5) - w0 + 1; // stream words the symbol touches
-          uint32_t outv = 0u, prev = 0u;
-          int j = 0, unc_any = 0;
-          auto emit = [&](uint32_t wd) {
-            const uint32_t o = (uint32_t)((((uint64_t)prev << 32) | wd) >> sh);
-            // (lane select in M0: a VALU instruction reads one SGPR on gfx950; M0 is declared
-            // clobbered, and k_demod has no other M0 use)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-            asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(outv) : "s"(o), "s"(j) : "m0");
-#pragma clang diagnostic pop
-            prev = wd;
-            ++j;
-          };
+      for (int which = 0; which < 2; ++which) {
+        const int sidx = which == 0 ? s1 : s2;
+        if (sidx < 0 || KO(2)) continue; // wave-uniform
+        const bool live = which == 0 ? live1 : live2;
+        const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
+        const float tau = which == 0 ? tau1 : tau2;
+        const int sbase = sidx * per_sym;
+        int unc_any = 0;
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int nd = ndata - 64 * rr; // data lanes of this slot (wave-uniform)
-            if (rr >= NS || nd <= 0) continue;
-            const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
-            uint64_t mA, mB = 0;
-            float margin;
-            if (MOD == AMOD_QPSK) { // [im < 0], [re < 0] xor [im < 0] (sign bits, Gray)
-              mA = __ballot(__float_as_int(c.y) < 0);
-              mB = __ballot(__float_as_int(c.x) < 0) ^ mA;
-              margin = fminf(fabsf(c.x), fabsf(c.y));
-            } else { // BPSK: first strict argmin, 1 iff re < 0
-              mA = __ballot(c.x < 0.f);
-              margin = fabsf(c.x);
-            }
-            unc_any |= !KO(0xFFFF) && ln < nd && live && margin <= tau;
-            if (!live) {
-              mA = (origin_idx >> (BPS - 1)) & 1 ? ~0ull : 0ull;
-              mB = origin_idx & 1 ? ~0ull : 0ull;
-            }
-            const uint64_t vm = nd >= 64 ? ~0ull : (1ull << nd) - 1ull;
-            mA &= vm;
-            mB &= vm;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              if (32 * h >= nd) break; // wave-uniform
-              const uint32_t a = (uint32_t)(mA >> (32 * h));
-              if (MOD == AMOD_QPSK) {
-                const uint32_t b = (uint32_t)(mB >> (32 * h));
-                const uint64_t il = (s_bitrep(a) & 0x5555555555555555ull) | (s_bitrep(b) & 0xAAAAAAAAAAAAAAAAull);
-                emit(__builtin_bitreverse32((uint32_t)il));
-                if (32 * h + 16 < nd) emit(__builtin_bitreverse32((uint32_t)(il >> 32)));
-              } else {
-                emit(__builtin_bitreverse32(a));
-              }
-            }
+        for (int rr = 0; rr < 4; ++rr) {
+          if (rr >= NS) continue;
+          const int dib = dib_of(rr);
+          const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
+          uint32_t db;
+          float margin;
+          if (MOD == AMOD_QPSK) {
+            db = qpsk_bits(c.x, c.y);
+            margin = fminf(fabsf(c.x), fabsf(c.y));
+          } else {
+            db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
           }
-          emit(0u); // the last word's spill into the next stream word
-          if (ln < nout) atomicOr(bits + w0 + ln, outv);
-          if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
+          db = live ? db : org_bits;
+          unc_any |= !KO(0xFFFF) && dib >= 0 && live && margin <= tau;
+          const int pos = sbase + dib;
+          if (dib >= 0) dec[pos / BPS - g0] = db >> (pos & 31);
         }
-      } else {
-        // 16-QAM: the job's decisions (symbols s1, s2: a contiguous run [gs, ge) of the
-        // frame's decision sequence) go to the exchange buffer, free again once the band is
-        // in registers: one dword per decision (consecutive data indices on consecutive
-        // lanes), its bits already at their place in the stream word (BPS divides 32, so a
-        // decision never straddles a word; v_lshrrev takes the position mod 32). Word
-        // wfirst + i of the stream is then the OR of dwords [DPW i, DPW i + DPW), one lane
-        // per word, one ds_or into the stream (the first word's top bits belong to the
-        // previous job).
-        constexpr int DPW = 32 / BPS; // decisions per stream word
-        uint32_t *const dec = reinterpret_cast<uint32_t *>(X2);
-        const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
-        const int wfirst = gs / DPW, g0 = wfirst * DPW, gend = (ge + DPW - 1) / DPW * DPW;
-        asm volatile("" ::: "memory"); // (the band reads above are float2 accesses of the same LDS)
-        if (ln < DPW) { // the first and last words' dwords outside [gs, ge)
-          if (g0 + ln < gs) dec[ln] = 0u;
-          if (ge + ln < gend) dec[ge - g0 + ln] = 0u;
-        }
-        const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
+        if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      // (lane i reads its NQ 16-byte pieces starting at piece i / (16 / NQ) mod NQ: the 16
+      // lanes of each ds_read_b128 group then cover 16 distinct 16-byte bank slots; in
+      // order, lanes i and i + 16 / NQ hit the same slot: 4-way for QPSK)
+      constexpr int NQ = DPW / 4;
+      const int rot = (ln / (16 / NQ)) & (NQ - 1);
+      for (int i = ln; i < (KO(2) ? 0 : (gend - g0) / DPW); i += 64) {
+        const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
+        uint32_t word = 0u;
 #pragma unroll
-        for (int which = 0; which < 2; ++which) {
-          const int sidx = which == 0 ? s1 : s2;
-          if (sidx < 0 || KO(2)) continue; // wave-uniform
-          const bool live = which == 0 ? live1 : live2;
-          const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
-          const float tau = which == 0 ? tau1 : tau2;
-          const int sbase = sidx * per_sym;
-          int unc_any = 0;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            if (rr >= NS) continue;
-            const int o = ln + 64 * rr;
-            const int dib = o < ndata ? o * BPS : -1;
-            const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
-            float margin;
-            uint32_t db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
-            db = live ? db : org_bits;
-            unc_any |= !KO(0xFFFF) && dib >= 0 && live && margin <= tau;
-            const int pos = sbase + dib;
-            if (dib >= 0) dec[pos / BPS - g0] = db >> (pos & 31);
-          }
-          if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
+        for (int k = 0; k < NQ; ++k) {
+          const uint4 t = q[(k + rot) & (NQ - 1)];
+          word |= (t.x | t.y) | (t.z | t.w);
         }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        // (lane i reads its NQ 16-byte pieces starting at piece i / (16 / NQ) mod NQ: the 16
-        // lanes of each ds_read_b128 group then cover 16 distinct 16-byte bank slots; in
-        // order, lanes i and i + 16 / NQ hit the same slot)
-        constexpr int NQ = DPW / 4;
-        const int rot = (ln / (16 / NQ)) & (NQ - 1);
-        for (int i = ln; i < (KO(2) ? 0 : (gend - g0) / DPW); i += 64) {
-          const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
-          uint32_t word = 0u;
-#pragma unroll
-          for (int k = 0; k < NQ; ++k) {
-            const uint4 t = q[(k + rot) & (NQ - 1)];
-            word |= (t.x | t.y) | (t.z | t.w);
-          }
-          atomicOr(bits + wfirst + i, word);
-        }
+        atomicOr(bits + wfirst + i, word);
       }
       asm volatile("" ::: "memory"); // (the next FFT rewrites the buffer)
       {

@@ -395,12 +395,6 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
       known[b] = (float)known_full[k];
       band_di[b] = is_pilot(*c, k) ? (int16_t)-1 : (int16_t)di++;
     }
-    // k_demod's lane order: the data subcarriers in data-index order, then the pilots
-    std::vector<int16_t> band_ord;
-    for (int b = 0; b < nband; ++b)
-      if (band_di[b] >= 0) band_ord.push_back((int16_t)b);
-    for (int b = 0; b < nband; ++b)
-      if (band_di[b] < 0) band_ord.push_back((int16_t)b);
     std::vector<float> tw1(2 * 8 * 64), tw2(2 * 8 * 8);
     for (int q = 0; q < 8; ++q)
       for (int l = 0; l < 64; ++l) {
@@ -419,7 +413,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     size_t off = 0;
     auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_pre1 = carve(sym * 4), o_tw1 = carve(tw1.size() * 4), o_tw2 = carve(tw2.size() * 4),
-                 o_twx = carve(twx.size() * 8), o_known = carve(nband * 4), o_di = carve(nband * 2), o_ord = carve(nband * 2),
+                 o_twx = carve(twx.size() * 8), o_known = carve(nband * 4), o_di = carve(nband * 2),
                  o_pts = carve(pts.size() * 8), o_twi = carve(twi.size() * 8), o_tmpl = carve(tmpl.size() * 4);
     if (ts->buf.ensure(off) != hipSuccess) return fail(ctx, "hipMalloc(tables)", AMOD_ERR_NOMEM);
     char *base = (char *)ts->buf.p;
@@ -429,7 +423,6 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     HIP_TRY(hipMemcpy(base + o_twx, twx.data(), twx.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_known, known.data(), nband * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_di, band_di.data(), nband * 2, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(base + o_ord, band_ord.data(), nband * 2, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_pts, pts.data(), pts.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_twi, twi.data(), twi.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(base + o_tmpl, tmpl.data(), tmpl.size() * 4, hipMemcpyHostToDevice));
@@ -439,7 +432,6 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.t.tw_exact = (const double2 *)(base + o_twx);
     d.t.known = (const float *)(base + o_known);
     d.t.band_di = (const int16_t *)(base + o_di);
-    d.t.band_ord = (const int16_t *)(base + o_ord);
     d.t.points = (const double2 *)(base + o_pts);
     d.t.tw_inv = (const double2 *)(base + o_twi);
     d.t.tmpl = (const float *)(base + o_tmpl);

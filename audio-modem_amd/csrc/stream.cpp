@@ -1093,7 +1093,7 @@ struct WindowDecoder {
   const uint8_t *ph = nullptr;   // pinned payload rows
   std::vector<uint8_t> zero_row;
   int64_t stride = 16;
-  double t_ms = 0;
+  double t_ms = 0, t_launch = 0; // host time in launch + collect (t_launch: launch alone)
   // a batch in flight in buffer set k
   struct Flight {
     std::vector<int64_t> pos, woff; // (host arrays kept until the batch is collected)
@@ -1155,7 +1155,9 @@ struct WindowDecoder {
     }
     S_TRY(hipEventRecord(c.w_done[k], s));
     f.live = true;
-    t_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    t_ms += dt;
+    t_launch += dt;
     return AMOD_SUCCESS;
   }
   // waits for batch k; res / row() then describe it
@@ -1297,6 +1299,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   std::vector<int64_t> fails_out;
   WindowDecoder wd;
   CopyPool copies(std::max(0, std::min(8, nthreads) - 1));
+  double t_loop = 0, t_copy = 0; // (diagnostics: the dispatch's per-frame loop and its copies)
 
   // decode frames[a, b) and dispatch them in order (_demodulateFrame, app.js:907-972);
   // `changed`: the first frame whose metadata result changed the window length of what
@@ -1316,6 +1319,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
       }
       const int rc = wd.collect(ctx, pp, (int)(j & 1));
       if (rc) return rc;
+      const auto tl0 = clk::now();
       for (size_t i = c0; i < c1; ++i) {
         FrameEv &ev = fr[i];
         const amod_result &r = wd.res[i - c0];
@@ -1347,7 +1351,11 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
           if (dst && r.data_len > 0) copies.items.push_back({dst, sl + r.data_off, (size_t)r.data_len});
         }
       }
+      const auto tl1 = clk::now();
       copies.run(); // before the next batch reuses this one's payload rows
+      const auto tl2 = clk::now();
+      t_loop += std::chrono::duration<double, std::milli>(tl1 - tl0).count();
+      t_copy += std::chrono::duration<double, std::milli>(tl2 - tl1).count();
     }
     return AMOD_SUCCESS;
   };
@@ -1399,9 +1407,10 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     const int rc = decode_dispatch(tr.frames, 0, tr.frames.size(), chg);
     if (rc) return rc;
     if (getenv("AMOD_STREAM_DIAG"))
-      fprintf(stderr, "[stream] decode_dispatch of %zu frames: %.3f ms (since prepass %.3f ms)\n", tr.frames.size(),
+      fprintf(stderr, "[stream] decode_dispatch of %zu frames: %.3f ms (since prepass %.3f ms; window decoder %.3f ms (launches %.3f), "
+              "per-frame loop %.3f ms, chunk copies %.3f ms so far)\n", tr.frames.size(),
               std::chrono::duration<double, std::milli>(clk::now() - t_dd).count(),
-              std::chrono::duration<double, std::milli>(t_dd - t_gpu_pre).count());
+              std::chrono::duration<double, std::milli>(t_dd - t_gpu_pre).count(), wd.t_ms, wd.t_launch, t_loop, t_copy);
     if (chg >= 0) {
       // keep what happened up to that frame; re-run the rest with the new window length
       const RxState after = tr.frames[chg].after;
