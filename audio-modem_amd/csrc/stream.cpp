@@ -50,7 +50,8 @@ namespace {
 // receiver's host phase). run() returns once every copy is done.
 struct CopyPool {
   struct Item { uint8_t *dst; const uint8_t *src; size_t n; };
-  std::vector<Item> items;
+  std::vector<Item> items; // being filled (the next start() hands them to the workers)
+  std::vector<Item> work;  // being copied
   std::vector<std::thread> th;
   std::mutex m;
   std::condition_variable go, done;
@@ -67,7 +68,7 @@ struct CopyPool {
     for (auto &t : th) t.join();
   }
   void drain() {
-    for (size_t i; (i = next.fetch_add(1)) < items.size();) std::memcpy(items[i].dst, items[i].src, items[i].n);
+    for (size_t i; (i = next.fetch_add(1)) < work.size();) std::memcpy(work[i].dst, work[i].src, work[i].n);
   }
   void worker() {
     uint64_t seen = 0;
@@ -83,18 +84,31 @@ struct CopyPool {
       done.notify_one();
     }
   }
-  void run() {
+  // the copies handed over by the last start() are done
+  void wait() {
+    std::unique_lock<std::mutex> lk(m);
+    done.wait(lk, [&] { return busy == 0; });
+    work.clear();
+  }
+  // hands `items` to the workers and returns (after the previous batch's copies are done)
+  void start() {
+    wait();
     if (items.empty()) return;
-    if (items.size() < 64 || th.empty()) { // not worth a wake-up
+    if (th.empty()) {
       for (auto &it : items) std::memcpy(it.dst, it.src, it.n);
-    } else {
-      next = 0;
-      { std::lock_guard<std::mutex> lk(m); busy = (int)th.size(); ++gen; }
-      go.notify_all();
-      drain();
-      std::unique_lock<std::mutex> lk(m);
-      done.wait(lk, [&] { return busy == 0; });
+      items.clear();
+      return;
     }
+    work.swap(items);
+    items.clear();
+    next = 0;
+    { std::lock_guard<std::mutex> lk(m); busy = (int)th.size(); ++gen; }
+    go.notify_all();
+  }
+  // every copy enqueued so far done, on this thread too
+  void run() {
+    wait();
+    for (auto &it : items) std::memcpy(it.dst, it.src, it.n);
     items.clear();
   }
 };
@@ -634,14 +648,17 @@ struct Pinned {
 struct StreamCache {
   DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
   DBuf d_pre1, d_first, d_base, d_count, d_out, d_metric, d_rwg;
-  // window decoder: two batches in flight (one decoding while the host dispatches the other)
-  DBuf w_pos[2], w_len[2], w_woff[2], w_win[2], w_res[2], w_pay[2];
-  hipEvent_t w_done[2] = {};
+  // window decoder: three buffer sets (one batch decoding, one dispatched by the host, one
+  // whose chunk bytes the copy pool is still moving into the assembler)
+  static constexpr int kSets = 3;
+  DBuf w_pos[kSets], w_len[kSets], w_woff[kSets], w_win[kSets], w_res[kSets], w_pay[kSets];
+  hipEvent_t w_done[kSets] = {}, w_kern[kSets] = {};
+  hipStream_t s3 = nullptr; // window decoder: results and payload rows to the host, beside the next batch's kernels
   DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
   DBuf d_barg, d_gaps;                      // k_fine's per-workgroup argmax, k_gap_scan's records
   Pinned gaps_h;
   Pinned yh, yc, hot_h, metric_h;
-  Pinned w_res_h[2], w_pay_h[2];            // window decoder: results and payload rows (pinned D2H)
+  Pinned w_res_h[kSets], w_pay_h[kSets];    // window decoder: results and payload rows (pinned D2H)
   // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
   std::vector<uint8_t> sp_need;
   std::vector<int32_t> sp_cidx;
@@ -653,6 +670,9 @@ struct StreamCache {
   hipEvent_t ema_done = nullptr, gathered = nullptr, piece[kPieces] = {}, cpiece[kPieces] = {};
   ~StreamCache() {
     if (s2) { (void)hipStreamSynchronize(s2); (void)hipStreamDestroy(s2); }
+    if (s3) { (void)hipStreamSynchronize(s3); (void)hipStreamDestroy(s3); }
+    for (auto e : w_kern)
+      if (e) (void)hipEventDestroy(e);
     if (ema_done) (void)hipEventDestroy(ema_done);
     if (gathered) (void)hipEventDestroy(gathered);
     for (auto e : piece)
@@ -1103,7 +1123,7 @@ struct WindowDecoder {
     int nw = 0;
     size_t a = 0, b = 0;
     bool live = false;
-  } fl[2];
+  } fl[StreamCache::kSets];
   // payload row of frame i - a of the last collected batch (zeros for a lost window)
   const uint8_t *row(size_t k) const { return slot[k] < 0 ? zero_row.data() : ph + (size_t)stride * slot[k]; }
 
@@ -1132,6 +1152,8 @@ struct WindowDecoder {
     S_TRY(c.w_res_h[k].alloc(sizeof(amod_result) * (size_t)std::max(nw, 1)));
     S_TRY(c.w_pay_h[k].alloc((size_t)f.stride * std::max(nw, 1)));
     if (!c.w_done[k]) S_TRY(hipEventCreateWithFlags(&c.w_done[k], hipEventDisableTiming));
+    if (!c.w_kern[k]) S_TRY(hipEventCreateWithFlags(&c.w_kern[k], hipEventDisableTiming));
+    if (!c.s3) S_TRY(hipStreamCreateWithFlags(&c.s3, hipStreamNonBlocking));
     if (nw) {
       S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
@@ -1150,10 +1172,16 @@ struct WindowDecoder {
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
                               nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), f.stride, 0, s);
       if (rc) return rc;
-      S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, s));
-      S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, s));
+      // the rows go to the host on s3, so the next batch's kernels on s do not queue behind
+      // them (a batch's 9 MB of rows took as long as its kernels)
+      S_TRY(hipEventRecord(c.w_kern[k], s));
+      S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
+      S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, c.s3));
+      S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
+      S_TRY(hipEventRecord(c.w_done[k], c.s3));
+    } else {
+      S_TRY(hipEventRecord(c.w_done[k], s));
     }
-    S_TRY(hipEventRecord(c.w_done[k], s));
     f.live = true;
     const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     t_ms += dt;
@@ -1188,7 +1216,7 @@ struct WindowDecoder {
   // a batch launched but not collected (dropped: a metadata frame changed what follows) is
   // waited for, so its buffers can be reused
   int drain(amod_ctx *ctx, const Prepass &pp) {
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < StreamCache::kSets; ++k)
       if (fl[k].live) { S_TRY(hipEventSynchronize(pp.c->w_done[k])); fl[k].live = false; }
     return AMOD_SUCCESS;
   }
@@ -1306,7 +1334,8 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   // follows (its `after` updated), or -1
   auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
     changed = -1;
-    // batch j decodes (buffer set j & 1) while the host dispatches batch j - 1
+    // batch j + 1 decodes (buffer set (j + 1) % 3) while the host dispatches batch j and the
+    // copy pool moves batch j - 1's chunks
     if (a < b) {
       const int rc = wd.launch(ctx, cfg, pp, fr, a, std::min(b, a + (size_t)kBatch), s, 0);
       if (rc) return rc;
@@ -1314,10 +1343,10 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     for (size_t c0 = a, j = 0; c0 < b; c0 += kBatch, ++j) {
       const size_t c1 = std::min(b, c0 + (size_t)kBatch);
       if (c1 < b) {
-        const int rc = wd.launch(ctx, cfg, pp, fr, c1, std::min(b, c1 + (size_t)kBatch), s, (int)((j + 1) & 1));
+        const int rc = wd.launch(ctx, cfg, pp, fr, c1, std::min(b, c1 + (size_t)kBatch), s, (int)((j + 1) % 3));
         if (rc) return rc;
       }
-      const int rc = wd.collect(ctx, pp, (int)(j & 1));
+      const int rc = wd.collect(ctx, pp, (int)(j % 3));
       if (rc) return rc;
       const auto tl0 = clk::now();
       for (size_t i = c0; i < c1; ++i) {
@@ -1343,7 +1372,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
           const bool chg = upd.meta_received != ev.after.meta_received ||
                            (upd.meta_received && upd.chunk_size != ev.after.chunk_size);
           ev.after = upd;
-          if (chg) { changed = (int64_t)i; return wd.drain(ctx, pp); }
+          if (chg) { changed = (int64_t)i; copies.wait(); return wd.drain(ctx, pp); }
         } else if (r.frame_type == 0xFF) {
           uint8_t *dst = nullptr;
           const int c = amod_asm_chunk_at(assembler, r.seq_num, sl + r.data_off, r.data_len, r.crc_valid, &dst);
@@ -1352,11 +1381,12 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
         }
       }
       const auto tl1 = clk::now();
-      copies.run(); // before the next batch reuses this one's payload rows
+      copies.start(); // (batch j - 1's copies done first: its buffer set is the next launch's)
       const auto tl2 = clk::now();
       t_loop += std::chrono::duration<double, std::milli>(tl1 - tl0).count();
       t_copy += std::chrono::duration<double, std::milli>(tl2 - tl1).count();
     }
+    copies.run();
     return AMOD_SUCCESS;
   };
 
