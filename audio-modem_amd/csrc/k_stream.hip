@@ -42,6 +42,7 @@ constexpr int kL = 1024;                       // EMA chunk (one lane each in k_
 constexpr int kWarmDefault = 4;                // warm-up chunks before each chunk (the parallel fix
                                                // rounds settle the chunks whose chains had not met)
 constexpr int kEmaRounds = 6;                  // parallel fix rounds before the serial safety net
+constexpr int kPerDefault = 8;                 // output chunks per k_ema_out lane
 constexpr int kTile = 32;                      // samples per lane per LDS tile (36.9 KB per workgroup:
                                                // four per CU; 16 with 8 waves per SIMD measured slower)
 constexpr int kLPR = kTile / 4;                // lanes per tile row in the coalesced loads / stores
@@ -77,17 +78,19 @@ __global__ __launch_bounds__(256) void k_ema_contrib(const float *__restrict__ x
 // chain reaches the true one bit for bit), then chunk k with its outputs. The samples move
 // through a per-wave LDS tile (64 lanes x 64 samples): rows loaded coalesced one tile
 // ahead (registers), each lane walking its own row, output rows stored coalesced.
-// warm[k] = the state reached at chunk k's start.
+// warm[k] = the state reached at chunk k's start. A lane outputs `per` consecutive chunks
+// after one warm-up (per = 1 read every sample kWarm + 1 times, from HBM: the re-reads are
+// other lanes' chunks, long evicted; per = 2 reads them (kWarm + 2) / 2 times).
 constexpr int kRow = kTile + 4; // row stride (floats): 16-byte rows for ds_read_b128
 __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, int64_t nx, int64_t n,
                                                  const double *__restrict__ c,
                                                  double A, float *__restrict__ y, double *__restrict__ warm,
-                                                 double *__restrict__ end, int64_t nch, int kWarm) {
+                                                 double *__restrict__ end, int64_t nch, int kWarm, int per) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kRow];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t k0 = ((int64_t)blockIdx.x * 4 + wv) * 64; // the wave's first chunk
+  const int64_t k0 = ((int64_t)blockIdx.x * 4 + wv) * 64 * per; // the wave's first chunk
   if (k0 >= nch) return;
-  const int64_t k = k0 + lane;
+  const int64_t k = k0 + (int64_t)per * lane;                    // the lane's first output chunk
   const int64_t kw = k - kWarm > 0 ? k - kWarm : 0;           // first warm-up chunk
   double m = 0.0;                                             // zero start: the true one
   if (k < nch && kw > 0) {
@@ -95,9 +98,9 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
     for (int64_t j = kw - 1; j >= 0 && j > kw - 41; --j) { m += p * c[j]; p *= A; }
   }
   float *const T = tile[wv];
-  // lane l's row at step j covers samples [(k0 + l - kWarm) L + 64 j, + 64) (warm-up
-  // chunks first, then chunk k0 + l); rows before the stream start are skipped
-  const int steps = (kWarm + 1) * kL / kTile, wsteps = kWarm * kL / kTile;
+  // lane l's row at step j covers samples [(k - kWarm) L + kTile j, + kTile) (warm-up
+  // chunks first, then chunks k .. k + per - 1); rows before the stream start are skipped
+  const int steps = (kWarm + per) * kL / kTile, wsteps = kWarm * kL / kTile;
   const int rr = lane / kLPR, c4 = lane % kLPR; // load/store slot: rows rr + kRPI q, column 4 c4
   // the wave's window as raw buffers: out-of-range dwords read 0 / are not written, so no
   // load or store sits under a branch (offsets before the stream start wrap out of range)
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
   auto load = [&](int j) {
 #pragma unroll
     for (int q = 0; q < kLPR; ++q) {
-      const int64_t g = (k0 + rr + kRPI * q - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
+      const int64_t g = (k0 + (int64_t)per * (rr + kRPI * q) - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * g), 0, 0);
       pf[q] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
@@ -124,8 +127,12 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
     __builtin_amdgcn_wave_barrier();
     if (j + 1 < steps) load(j + 1); // in flight under this tile's recurrence
     const int64_t row0 = (k - kWarm) * kL + (int64_t)kTile * j; // first sample of this lane's row
-    const bool out = j >= wsteps;                                // chunk k itself
-    if (j == wsteps && k < nch) warm[k] = m;
+    const bool out = j >= wsteps;                                // chunks k .. k + per - 1
+    if (out && (j - wsteps) % (kL / kTile) == 0) { // an output chunk starts
+      const int64_t kc = k + (j - wsteps) / (kL / kTile);
+      if (kc > k && kc - 1 < nch) end[kc - 1] = m;
+      if (kc < nch) warm[kc] = m;
+    }
     float *const R = T + lane * kRow;
     if (row0 >= kw * kL) { // warm-up from the chunk kw (its approximate seed), then chunk k
       if (row0 + kTile <= n) {
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
 #pragma unroll
       for (int q = 0; q < kLPR; ++q) {
         const int r = rr + kRPI * q;
-        const int64_t g = r * kL + (int64_t)kTile * (j - wsteps) + 4 * c4;
+        const int64_t g = (int64_t)per * r * kL + (int64_t)kTile * (j - wsteps) + 4 * c4;
         const float4 v = *reinterpret_cast<const float4 *>(T + r * kRow + 4 * c4);
         __amdgpu_buffer_rsrc_t yrr = yr;
         typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -168,7 +175,8 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
       }
     }
   }
-  if (k < nch) end[k] = m;
+  const int64_t kl = k + per - 1 < nch ? k + per - 1 : nch - 1; // the lane's last chunk
+  if (kl >= k) end[kl] = m;
 }
 
 // (3) chunks whose start state is not bit-equal to the previous chunk's end state
@@ -759,8 +767,12 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
     const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
     return e ? std::max(0, atoi(e)) : amod::kWarmDefault;
   }();
-  hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, x, nx, n, scr, A, y, warm,
-                     end, nch, warm_chunks);
+  static const int per = [] {
+    const char *e = getenv("AMOD_EMA_PER"); // experiments: output chunks per lane
+    return e ? std::max(1, atoi(e)) : amod::kPerDefault;
+  }();
+  hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((nch + 256 * per - 1) / (256 * per))), dim3(256), 0, s, x, nx, n,
+                     scr, A, y, warm, end, nch, warm_chunks, per);
   // parallel fix rounds: each round checks every chunk's start state against its
   // predecessor's end and recomputes the listed runs in parallel; after kEmaRounds rounds
   // the serial fix settles anything left (normally nothing: runs are a chunk or two long)
