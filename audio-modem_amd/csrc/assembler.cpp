@@ -19,6 +19,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <thread>
@@ -52,6 +53,7 @@ struct FileArena {
 #ifdef MADV_HUGEPAGE
     (void)madvise(p, n, MADV_HUGEPAGE);
 #endif
+    if (getenv("AMOD_ASM_NO_POPULATE")) return true; // (experiments: first-touch faults in the copies)
     filler = std::thread([q = p, len = n] {
       constexpr int kPopulateWrite = 23; // MADV_POPULATE_WRITE (Linux 5.14)
       // one huge page per call: each call holds the address-space lock (read) while it
