@@ -1616,25 +1616,26 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       job_syms(cur, jcur, s1, s2);
       const bool ce = s1 == -2;
       const float first1 = rlane(c[0].x, 0), first2 = rlane(c[0].y, 0);
-      int ne1 = 0, ne2 = 0, nf = 0;
       f2v v[8];
       // no second symbol: A = B = 0 zeroes the imaginary half (its samples are finite: the
       // last job re-reads the first symbol's, checked below in chunk mode)
       const f2v Av = {cur.A, s2 >= 0 ? cur.A : 0.f}, Bv = {cur.B, s2 >= 0 ? cur.B : 0.f};
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        if (!KO(8)) {
-          ne1 |= c[m].x != first1;
-          ne2 |= c[m].y != first2;
-          if (chunk_mode) nf |= !isfinite(c[m].x) || !isfinite(c[m].y); // received: stage 0 saw them
-        } else {
-          ne1 = ne2 = 1;
+      for (int m = 0; m < 8; ++m) v[m] = __builtin_elementwise_fma(c[m], Av, Bv);
+      // a window is constant iff every raw sample equals its first one (all-zero spectrum).
+      // One sample per lane settles it for any real signal (some lane differs); only when
+      // all 64 agree are the other 448 compared (wave-uniform branch)
+      bool const1 = false, const2 = false;
+      if (!KO(8)) {
+        int ne1 = c[0].x != first1, ne2 = c[0].y != first2;
+        const bool q1 = __ballot(ne1) == 0, q2 = __ballot(ne2) == 0;
+        if (q1 || q2) {
+#pragma unroll
+          for (int m = 1; m < 8; ++m) { ne1 |= c[m].x != first1; ne2 |= c[m].y != first2; }
+          const1 = q1 && __ballot(ne1) == 0;
+          const2 = q2 && __ballot(ne2) == 0;
         }
-        v[m] = __builtin_elementwise_fma(c[m], Av, Bv);
       }
-      // a window is constant iff every raw sample equals its first one (all-zero spectrum)
-      const bool const1 = __ballot(ne1) == 0, const2 = __ballot(ne2) == 0;
-      if (__ballot(nf)) wflags |= AMOD_FLAG_NONFINITE; // chunk mode: `x || 0` semantics on the exact path
       DSTAMP(16, jcur == 1);
       DSTAMP(27, jcur == 2); // (job 2 samples ready: minus mark 21 = the wait for its loads)
       issue_next(); // the samples are in v: the next job's loads fly under this FFT too
@@ -1661,6 +1662,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         const f2v zk = zkp[64 * rr], zn = znp[64 * (3 - rr)];
         f2v a = pk_add_conj(zk, zn), c = pk_add_swap_neg(zk, zn);
         float zz = fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y));
+        // chunk mode, `x || 0` semantics on the exact path: a NaN/Inf sample makes every bin
+        // of Z non-finite (each bin is a sum over all 512 inputs with non-zero weights, and
+        // Inf * 0 is NaN), so one bin pair per lane stands in for the 1024 samples
+        if (rr == 0 && chunk_mode && !KO(8) && __ballot(!isfinite(zk.x + zk.y + zn.x + zn.y)))
+          wflags |= AMOD_FLAG_NONFINITE;
         if (rr == NS - 1) { // the last slot may be partly filled
           const bool in = ln + 64 * rr < nband;
           a = in ? a : f2v{0.f, 0.f};
