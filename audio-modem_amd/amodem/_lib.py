@@ -119,6 +119,7 @@ SIGNATURES = {
     "amod_set_profiling": (C.c_int, [_P, C.c_int]),
     "amod_kernel_breakdown": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "amod_kernel_stages": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int64)]),
+    "amod_aux_overlap": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "amod_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int64)]),
     "amod_decode_device_debug": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,

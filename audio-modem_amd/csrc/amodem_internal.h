@@ -136,6 +136,32 @@ struct DevWork {
   // counter set the previous decode used (decodes alternate between two sets of 32), so
   // the next decode needs no memset dispatch (null: no reset)
   int32_t *fb_reset;
+  // profiled decodes only (amod_aux_overlap): device real-time marks, [0] the first listed
+  // frame list A's replica took (min), [1] the last k_demod wave's end (max), [2] the first
+  // k_demod wave's start (min); k_detect / k_chunk_prep's workgroup 0 initialises them
+  unsigned long long *tl;
+};
+
+// Diagnostic / experiment knobs, read from the environment once when a context opens
+// (never per decode): a context's routing and grid shapes stay fixed for its lifetime.
+struct Knobs {
+  float guard_scale = 1.f;  // AMOD_GUARD_SCALE: fast-path guard bands (tests)
+  int stop_after = 99;      // AMOD_STOP_AFTER: fast kernel stops after this stage (k_corr_scan)
+  int demod_mcap = 0;       // AMOD_DEMOD_MCAP: cap k_demod's symbol capacity (0: none)
+  bool stamps = false;      // AMOD_STAMPS: per-frame s_memtime marks
+  int demod_bpc = 0;        // AMOD_DEMOD_BPC: k_demod workgroups per CU (0: occupancy)
+  int chunks = 0;           // AMOD_CHUNKS: detect/demod chunks over two streams (0: 1)
+  int xslots = 0;           // AMOD_XSLOTS: cap the exact grid (0: none)
+  bool no_replay = false;   // AMOD_NO_REPLAY: listed frames demodulate in the replica too
+  bool exact_serial = false;// AMOD_EXACT_SERIAL: list A after k_demod on the launch stream
+  int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
+  // streaming receiver (stream.cpp)
+  int stream_minseg = 0;    // AMOD_STREAM_MINSEG
+  bool stream_diag = false; // AMOD_STREAM_DIAG
+  bool no_gap_scan = false; // AMOD_NO_GAP_SCAN
+  int stream_threads = -1;  // AMOD_STREAM_THREADS (-1: unset)
+  bool stream_fullcopy = false; // AMOD_STREAM_FULLCOPY
+  int ema_warm = 0, ema_per = 0, ema_rounds = 0; // AMOD_EMA_WARM / _PER / _ROUNDS (0: default)
 };
 
 // k_gap_scan -> streaming receiver: the scan that follows the frame of fine range r, run
@@ -458,6 +484,13 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
   }
 }
 
+// a profiled decode's timeline slot (DevWork::tl), set by the first launch of the decode
+__device__ inline void tl_init(const DevWork &w) {
+  if (w.tl && blockIdx.x == 0 && threadIdx.x == 0) {
+    w.tl[0] = ~0ull; w.tl[1] = 0ull; w.tl[2] = ~0ull; w.tl[3] = 0ull;
+  }
+}
+
 __device__ inline void init_result(amod_result &r) {
   r.status = AMOD_OK; r.preamble_idx = -1; r.coarse_idx = -1; r.frame_type = -1; r.aux = 0;
   r.nbytes = 0; r.name_off = 0; r.name_len = 0; r.data_off = 0; r.data_len = 0;
@@ -499,6 +532,7 @@ hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float 
 // runtime.cpp: a context's device and stream for the host-side orchestrators
 int amod_ctx_device(const amod_ctx *ctx);
 hipStream_t amod_ctx_stream(const amod_ctx *ctx);
+const amod::Knobs *amod_ctx_knobs(const amod_ctx *ctx); // read once at amod_open
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code);
 // per-context state owned by another module (slot: 0 = streaming receiver): *amod_ctx_ext
 // holds it; free_fn runs at amod_close, after the context's streams are drained

@@ -207,6 +207,7 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     init_result(r);
     r.flags = flags0 | AMOD_FLAG_EXACT;
     XSTAMP(8);
+    if (w.tl && tid == 0 && item == (int)blockIdx.x) atomicMin(w.tl, (unsigned long long)wall_clock64());
     if (w.stamps && tid == 0) w.stamps[(int64_t)f * 32 + 1] = __builtin_amdgcn_s_memrealtime(); // (100 MHz)
     {
       const int64_t need_bits = (int64_t)(N / SYM) * cfg.ndata * cfg.bps;

@@ -1236,7 +1236,7 @@ to_exact:
 // ------------------------------------------------------------ detection kernels
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_detect(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
-  (void)w_arg;
+  tl_init(w_arg);
   detect<false, false>();
 }
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_detect_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
@@ -1255,6 +1255,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_SCAN_WP
 // decodeChunkFrame (modem.js:770-786): no preprocessing, the frame starts at pre1;
 // one thread per window writes its detection record (or its geometry error)
 __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWork w) {
+  tl_init(w);
   const int f = w.f0 + (int)(blockIdx.x * WG + threadIdx.x);
   if (f >= w.f1) return;
   const int N = w.len[f], SYM = cfg.sym;
@@ -1973,6 +1974,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   if (ka >= nfr) return;
   const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
+  if (w.tl && lane == 0) atomicMin(w.tl + 2, (unsigned long long)wall_clock64());
   f2v r[8];
   loads(fa, ja, r);
   for (;;) {
@@ -1983,6 +1985,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     fa = fb; ka = kb; ja = jb;
   }
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
+  if (w.tl && lane == 0) atomicMax(w.tl + 1, (unsigned long long)wall_clock64());
 }
 template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;

@@ -233,6 +233,7 @@ std::vector<int32_t> cfg_key(const amod_cfg &c) {
 
 } // namespace
 
+constexpr int kTlSlots = 256;    // profiled decodes whose timeline marks are kept between harvests
 constexpr int kMaxChunks = 16;   // frame chunks of one decode (two-stream overlap)
 constexpr int kOverlapChunks = 1; // default chunk count (measured: overlap slows both launches)
 
@@ -284,9 +285,40 @@ struct amod_ctx {
   // the end of the second stream's chain (list A's exact kernel + replay k_demod), after
   // the launch stream has joined it, after list B's exact kernel
   std::vector<std::array<hipEvent_t, 6>> ev_used, ev_free;
+  // the device timeline marks of profiled decodes (amod_aux_overlap): kTlSlots slots of 4,
+  // one per decode in ring order; tl_of[i] is ev_used[i]'s slot
+  DevBuf tl;
+  int64_t tl_next = 0;
+  std::vector<int64_t> tl_of;
+  int64_t ov_listed = 0, ov_beside = 0;
+  double ov_lead_us = 0.0;
+  amod::Knobs knobs; // read once at amod_open
 };
 
 namespace {
+
+int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+// the diagnostic / experiment knobs (amod::Knobs), read once per context at amod_open
+void read_knobs(amod::Knobs &k) {
+  if (const char *g = getenv("AMOD_GUARD_SCALE")) k.guard_scale = (float)atof(g);
+  k.stop_after = env_int("AMOD_STOP_AFTER", 99);
+  k.demod_mcap = std::max(0, env_int("AMOD_DEMOD_MCAP", 0));
+  k.stamps = getenv("AMOD_STAMPS") != nullptr;
+  k.demod_bpc = std::max(0, env_int("AMOD_DEMOD_BPC", 0));
+  k.chunks = std::max(0, env_int("AMOD_CHUNKS", 0));
+  k.xslots = std::max(0, env_int("AMOD_XSLOTS", 0));
+  k.no_replay = getenv("AMOD_NO_REPLAY") != nullptr;
+  k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
+  if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
+  k.stream_minseg = std::max(0, env_int("AMOD_STREAM_MINSEG", 0));
+  k.stream_diag = getenv("AMOD_STREAM_DIAG") != nullptr;
+  k.no_gap_scan = getenv("AMOD_NO_GAP_SCAN") != nullptr;
+  k.stream_threads = env_int("AMOD_STREAM_THREADS", -1);
+  k.stream_fullcopy = getenv("AMOD_STREAM_FULLCOPY") != nullptr;
+}
 
 int fail(amod_ctx *ctx, const std::string &msg, int code) {
   g_last_error = msg;
@@ -360,10 +392,8 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.mod = c->modulation; d.rep = c->repetition;
     for (int i = 0; i < c->npilots; ++i) d.pilots[i] = c->pilots[i];
     d.origin_idx = demap_exact(c->modulation, 0.0, 0.0);
-    const char *g = getenv("AMOD_GUARD_SCALE");
-    d.guard = g ? (float)atof(g) : 1.0f;
-    const char *sa = getenv("AMOD_STOP_AFTER"); // stage-cost diagnostics; results are not written
-    d.stop_after = sa ? atoi(sa) : 99;
+    d.guard = ctx->knobs.guard_scale;
+    d.stop_after = ctx->knobs.stop_after; // stage-cost diagnostics; results are not written
     // host images
     std::vector<float> pre1(sym), ce(sym), tmpl(3 * (size_t)sym);
     double known_full[amod::kFft] = {0};
@@ -555,7 +585,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   rc = ensure_chain(ctx, nframes);
   if (rc) return rc;
   w.nb_cap = dims.nb_cap; w.fine_cap = dims.fine_cap; w.mcap = dims.mcap; w.fast_len = dims.fast_len;
-  if (const char *mc = getenv("AMOD_DEMOD_MCAP")) w.mcap = std::min(w.mcap, std::max(1, atoi(mc))); // experiments
+  if (ctx->knobs.demod_mcap > 0) w.mcap = std::min(w.mcap, ctx->knobs.demod_mcap); // experiments
   amod_demod_stream_words(d, w.mcap, &w.stream_words, &w.vote_off);
   w.det = (amod::DetRec *)ctx->det.p;
   if (!ctx->cu_count) {
@@ -563,7 +593,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     HIP_TRY(hipGetDeviceProperties(&prop, ctx->device));
     ctx->cu_count = prop.multiProcessorCount;
   }
-  if (getenv("AMOD_STAMPS")) { // diagnostics: per-frame s_memtime marks of the fast kernel
+  if (ctx->knobs.stamps) { // diagnostics: per-frame s_memtime marks of the fast kernel
     HIP_TRY(ctx->stamps.ensure(sizeof(unsigned long long) * 32 * (size_t)nframes));
     HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, sizeof(unsigned long long) * 32 * (size_t)nframes, s));
     w.stamps = (unsigned long long *)ctx->stamps.p;
@@ -594,29 +624,37 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
     ctx->demod_bpc = amod_demod_blocks_per_cu(d, lds);
   }
   int64_t per_cu = ctx->demod_bpc;
-  if (const char *g = getenv("AMOD_DEMOD_BPC")) per_cu = std::max(1, atoi(g)); // diagnostics: grid size
+  if (ctx->knobs.demod_bpc > 0) per_cu = ctx->knobs.demod_bpc; // diagnostics: grid size
   auto demod_blocks = [&](int n) { return (int)std::min<int64_t>(((int64_t)n + 3) / 4, (int64_t)ctx->cu_count * per_cu); };
   // Frames in chunks over two streams: k_detect of chunk c + 1 (HBM-bound) runs on `s`
   // while k_demod of chunk c (latency-bound FFT jobs) runs on the context's second
   // stream, so the demodulation hides under the next chunk's stream pass.
   int nchunk = 1;
   if (demod && !debug && nframes >= 2048) nchunk = kOverlapChunks;
-  if (const char *oc = getenv("AMOD_CHUNKS")) nchunk = std::max(1, std::min(kMaxChunks, atoi(oc)));
+  if (ctx->knobs.chunks > 0) nchunk = std::min(kMaxChunks, ctx->knobs.chunks);
   if (!demod || debug) nchunk = 1;
   nchunk = std::min(nchunk, std::max(1, nframes));
+  // this decode's timeline slot (profiling; one-chunk decodes with a k_demod launch): set by
+  // k_detect, list A's replica and the main k_demod launch only
+  unsigned long long *tl = nullptr;
+  int64_t tl_slot = -1;
+  if (ctx->profiling && demod && !debug && nchunk == 1 && !ctx->knobs.exact_serial) {
+    HIP_TRY(ctx->tl.ensure(sizeof(unsigned long long) * 4 * kTlSlots));
+    tl_slot = ctx->tl_next++ % kTlSlots;
+    tl = (unsigned long long *)ctx->tl.p + 4 * tl_slot;
+  }
+  w.tl = tl;
   amod::DevWork wb = w; // every field as w, list B
+  wb.tl = nullptr;
   wb.fb_count = fb + 1; wb.fb_list = fb_base + 64 + 2 * nframes; wb.fb_flags = fb_base + 64 + 3 * nframes;
-  if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-  for (auto &e : ctx->chunk_ev)
-    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // exact-kernel grid: persistent workgroups over the listed frames (usually none: the
   // launch then costs its dispatch, so two per CU, not one per slot)
   int xslots = std::min({ctx->nslots, nframes, 2 * std::max(1, ctx->cu_count)});
-  if (const char *xs = getenv("AMOD_XSLOTS")) xslots = std::max(1, std::min(xslots, atoi(xs))); // experiments
+  if (ctx->knobs.xslots > 0) xslots = std::min(xslots, ctx->knobs.xslots); // experiments
   // list A's exact kernel, then (detection replay) k_demod over the frames it only
   // detected: a frame listed for COARSE / FINE / THRESH alone gets its preambleIdx from
   // the fp64 replica and its symbols from the fast path (AMOD_NO_REPLAY: diagnostics)
-  const bool replay = demod && !debug && mode == AMOD_MODE_RECEIVED && !getenv("AMOD_NO_REPLAY");
+  const bool replay = demod && !debug && mode == AMOD_MODE_RECEIVED && !ctx->knobs.no_replay;
   auto exact_a = [&](hipStream_t st) -> int {
     amod::DevWork wa = w;
     wa.f0 = 0; wa.f1 = nframes;
@@ -639,7 +677,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       // list A is complete: the exact replica of the frames detection listed (long
       // sequential recurrences) runs on the second stream, under k_demod
       // (AMOD_EXACT_SERIAL, diagnostics: after it, on the same stream)
-      if (getenv("AMOD_EXACT_SERIAL")) {
+      if (ctx->knobs.exact_serial) {
         wb.f0 = 0; wb.f1 = nframes;
         HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
         HIP_TRY(mark(2));
@@ -658,6 +696,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
         // the exact kernel needs a wave slot and its registers on every SIMD it runs on:
         // with frames listed, k_demod leaves one workgroup per CU free
         amod::DevWork wm = wb;
+        wm.tl = tl;
         const int nb = demod_blocks(nframes);
         if (per_cu >= 2 && nb >= (int)(ctx->cu_count * per_cu)) {
           wm.yield_count = fb;
@@ -697,7 +736,10 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   ctx->fb_zeroed = xslots > 0 && !ctx->fb_captured;
   if (!ctx->fb_captured) ctx->fb_parity ^= 1;
   HIP_TRY(mark(5));
-  if (ctx->profiling) ctx->ev_used.push_back(ev);
+  if (ctx->profiling) {
+    ctx->ev_used.push_back(ev);
+    ctx->tl_of.push_back(tl_slot);
+  }
   return AMOD_SUCCESS;
 }
 
@@ -810,6 +852,9 @@ extern "C" {
 
 int amod_abi_version(void) { return AMOD_ABI_VERSION; }
 
+int amod_close(amod_ctx *ctx);
+const amod::Knobs *amod_ctx_knobs(const amod_ctx *ctx) { return ctx ? &ctx->knobs : nullptr; }
+
 int amod_ctx_device(const amod_ctx *ctx) { return ctx ? ctx->device : 0; }
 hipStream_t amod_ctx_stream(const amod_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code) { return fail(ctx, msg, code); }
@@ -836,9 +881,20 @@ int amod_open(int device, amod_ctx **out) {
     b->keep = &ctx->fb_captured;
     b->retired = &ctx->retired;
   }
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return fail(nullptr, "hipStreamCreate failed", AMOD_ERR_HIP);
+  read_knobs(ctx->knobs);
+  // The second stream, created here at the device's highest priority: it then draws its
+  // hardware queue from the high-priority pool, never the caller's stream's queue, so
+  // list A's replica (enqueued on it before k_demod) runs beside k_demod instead of
+  // ahead of it on a shared queue (a lazily created default-
+  // priority stream landed on the caller's queue in one of GPU_MAX_HW_QUEUES' rotations)
+  int prio_least = 0, prio_greatest = 0;
+  bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+  for (auto &e : ctx->chunk_ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    amod_close(ctx);
+    return fail(nullptr, "hipStreamCreate / hipEventCreate failed", AMOD_ERR_HIP);
   }
   *out = ctx;
   return AMOD_SUCCESS;
@@ -847,8 +903,10 @@ int amod_open(int device, amod_ctx **out) {
 int amod_close(amod_ctx *ctx) {
   if (!ctx) return AMOD_SUCCESS;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+  }
   if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
   for (int i = 0; i < 4; ++i)
     if (ctx->ext[i] && ctx->ext_free[i]) ctx->ext_free[i](ctx->ext[i]);
@@ -975,7 +1033,7 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   bool mono = true;
   for (int32_t i = 1; i < nframes && mono; ++i) mono = offsets[i] + lengths[i] >= offsets[i - 1] + lengths[i - 1];
   int64_t piece = kUpPiece;
-  if (const char *e = getenv("AMOD_UP_PIECE")) piece = std::max<int64_t>(1024, atoll(e)); // tests: many pieces
+  if (ctx->knobs.up_piece > 0) piece = std::max<int64_t>(1024, ctx->knobs.up_piece); // tests: many pieces
   const int64_t npiece = (nsamples + piece - 1) / piece;
   while ((int64_t)ctx->up_ev.size() < std::max<int64_t>(npiece, 1)) {
     hipEvent_t e;
@@ -1037,6 +1095,25 @@ int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n) {
   // the slots: {from event, to event} (amod.h AMOD_STAGE_*)
   static const int span[AMOD_STAGE_COUNT][2] = {{0, 1}, {1, 2}, {4, 5}, {1, 3}, {2, 4}, {1, 4}};
   double acc[AMOD_STAGE_COUNT] = {0};
+  // the timeline marks of the (at most kTlSlots) latest profiled decodes
+  std::vector<unsigned long long> tlh;
+  if (ctx->tl.p && !ctx->ev_used.empty()) {
+    HIP_TRY(hipEventSynchronize(ctx->ev_used.back()[5]));
+    tlh.resize(4 * (size_t)kTlSlots);
+    HIP_TRY(hipMemcpy(tlh.data(), ctx->tl.p, sizeof(unsigned long long) * tlh.size(), hipMemcpyDeviceToHost));
+    const size_t n = ctx->tl_of.size(), from = n > (size_t)kTlSlots ? n - kTlSlots : 0;
+    for (size_t i = from; i < n; ++i) {
+      const int64_t sl = ctx->tl_of[i];
+      if (sl < 0) continue;
+      const unsigned long long a_start = tlh[4 * sl], d_end = tlh[4 * sl + 1];
+      if (a_start == ~0ull || d_end == 0) continue; // list A took no frame / no k_demod wave ran
+      ctx->ov_listed += 1;
+      const double lead = ((double)(long long)(d_end - a_start)) / 100.0; // 100 MHz real-time clock
+      ctx->ov_beside += a_start < d_end;
+      ctx->ov_lead_us += lead;
+    }
+  }
+  ctx->tl_of.clear();
   for (auto &ev : ctx->ev_used) {
     HIP_TRY(hipEventSynchronize(ev[5]));
     for (int i = 0; i < AMOD_STAGE_COUNT; ++i) {
@@ -1049,6 +1126,17 @@ int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n) {
   for (int i = 0; i < nslots; ++i) ms[i] = i < AMOD_STAGE_COUNT ? acc[i] : 0.0;
   if (n) *n = (int64_t)ctx->ev_used.size();
   ctx->ev_used.clear();
+  return AMOD_SUCCESS;
+}
+
+int amod_aux_overlap(amod_ctx *ctx, int64_t *listed, int64_t *beside, double *lead_us) {
+  if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (listed) *listed = ctx->ov_listed;
+  if (beside) *beside = ctx->ov_beside;
+  if (lead_us) *lead_us = ctx->ov_lead_us;
+  ctx->ov_listed = ctx->ov_beside = 0;
+  ctx->ov_lead_us = 0.0;
   return AMOD_SUCCESS;
 }
 

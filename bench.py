@@ -313,6 +313,8 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
     lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))
     lib.amod_set_profiling(wl.dm.ctx, 0)
+    ov_l, ov_b, ov_lead = C.c_int64(), C.c_int64(), C.c_double()
+    lib.amod_aux_overlap(wl.dm.ctx, C.byref(ov_l), C.byref(ov_b), C.byref(ov_lead))
     st_ms = [kms[i] / max(1, kn.value) for i in range(L.STAGE_COUNT)]  # per decode (amod_kernel_stages)
     # the launches: k_detect, k_demod alone (the second stream's exact chain beside it is
     # reported on its own), list B's exact kernel
@@ -378,6 +380,10 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
                   "ms_avg": chain_s * 1e3, "achieved": algo_bytes / chain_s / 1e9, "peak": HBM_PEAK_GBS,
                   "unit": "GB/s", "frac": algo_bytes / chain_s / 1e9 / HBM_PEAK_GBS,
                   "kernels_ms_avg": dict(zip(names + ["k_decode_exact"], stage_ms)),
+                  "aux_overlap": {"what": "timed decodes whose list A had a frame; of those, the ones whose replica "
+                                          "started before k_demod's last wave ended (device real-time clock)",
+                                  "decodes_listed": ov_l.value, "beside": ov_b.value,
+                                  "lead_us_avg": ov_lead.value / max(1, ov_l.value)},
                   "symbols_demodulated_per_frame": "all" if wl.chunk else
                   "header..CRC symbols only (trailing silence skipped, SURVEY.md 8d)"},
     }

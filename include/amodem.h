@@ -199,6 +199,13 @@ enum {
   AMOD_STAGE_COUNT = 6
 };
 int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n);
+/* whether list A's exact chain ran beside k_demod (profiled decodes only, collected by
+   amod_kernel_stages): of the decodes since the last call, *listed had a frame on list A
+   (detection listed it), *beside started that frame's replica before k_demod's last wave
+   ended, and *lead_us sums k_demod's end minus the replica's start (device real-time
+   clock, microseconds; positive = beside). Resets. Not a reference function: the
+   scheduling evidence for the second stream. */
+int amod_aux_overlap(amod_ctx *ctx, int64_t *listed, int64_t *beside, double *lead_us);
 
 /* parity-test view of one frame's intermediates (filled when debug != NULL) */
 #define AMOD_DBG_BAND 256

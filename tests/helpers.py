@@ -54,6 +54,22 @@ def frame(name):
     raise KeyError(name)
 
 
+def open_with_env(device=0, **env):
+    """A Demodulator opened under the given AMOD_* knobs (libamodem reads them once,
+    when a context opens: amod::Knobs); the process environment is restored after."""
+    import amodem
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return amodem.Demodulator(device)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def sha(x: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
 

@@ -13,7 +13,7 @@ the fast path lists frames with ambiguous coarse decisions)."""
 import numpy as np
 import pytest
 
-from helpers import ref_dict, struct_to_dict
+from helpers import open_with_env, ref_dict, struct_to_dict
 
 import amodem
 from amodem import _lib as L
@@ -70,19 +70,11 @@ def test_forced_exact_matches_oracle_under_noise(snr_db, tiny):
     _check_against_oracle("acoustic", "BPSK", 3, x, offs, lens, rec, pay)
 
 
-def _wide_guard_demodulator(cfg, x, offs, lens):
-    """A context whose guard bands for cfg are 50x the default (AMOD_GUARD_SCALE, read
-    when the context builds cfg's tables at its first decode): at these SNRs ambiguous
-    coarse / fine decisions, and so the listed paths, become common instead of a few per
-    10^4 frames."""
-    import os
-    dm = amodem.Demodulator(0)
-    os.environ["AMOD_GUARD_SCALE"] = "50"
-    try:
-        dm.decode_batch(x, offs[:1], lens[:1], cfg=cfg)
-    finally:
-        del os.environ["AMOD_GUARD_SCALE"]
-    return dm
+def _wide_guard_demodulator(cfg, x, offs, lens, **env):
+    """A context whose guard bands are 50x the default (AMOD_GUARD_SCALE, read when the
+    context opens): at these SNRs ambiguous coarse / fine decisions, and so the listed
+    paths, become common instead of a few per 10^4 frames."""
+    return open_with_env(0, AMOD_GUARD_SCALE=50, **env)
 
 
 @pytest.mark.parametrize("preset,snr_db", [("acoustic", 6), ("standard", 7)])
@@ -139,15 +131,12 @@ def test_replayed_detection_equals_full_exact_path(preset, snr_db):
     detection from the fp64 replica and its symbols from k_demod (AMOD_FLAG_REPLAY);
     every result field and payload byte equals the whole-frame replica's
     (AMOD_NO_REPLAY) and the oracle's."""
-    import os
     cfg, x, offs, lens = _noisy_batch(preset, "BPSK", 3, 48, 64, snr_db, seed=11)
     dm = _wide_guard_demodulator(cfg, x, offs, lens)
     rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
-    os.environ["AMOD_NO_REPLAY"] = "1"
-    try:
-        ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
-    finally:
-        del os.environ["AMOD_NO_REPLAY"]
+    dm.close()
+    dm = _wide_guard_demodulator(cfg, x, offs, lens, AMOD_NO_REPLAY=1)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
     dm.close()
     replayed = (rec["flags"] & L.FLAG_REPLAY) != 0
     if preset == "acoustic":  # (standard at 7 dB: ambiguous coarse decisions end in detection errors)

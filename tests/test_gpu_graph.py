@@ -3,13 +3,13 @@ capture) and replayed: every replay, and an eager decode after the replays, retu
 eager decode's records and payload. Frames are listed for the exact kernel (wide guard
 bands), so the exact-list counters — zeroed by a memset inside a captured decode, by
 the previous decode's list-B launch otherwise — are exercised across replays."""
-import os
 
 import numpy as np
 import pytest
 
 import amodem
 from amodem import _lib as L
+from helpers import open_with_env
 
 pytestmark = pytest.mark.gpu
 
@@ -31,22 +31,18 @@ def test_captured_decode_replays_equal_eager():
     res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
     pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
 
-    dm = amodem.Demodulator(0)
-    os.environ["AMOD_GUARD_SCALE"] = "50"  # read when the context builds cfg's tables
-    try:
-        dm.reserve(cfg, F, N)
-        s = torch.cuda.Stream()
+    dm = open_with_env(0, AMOD_GUARD_SCALE=50)  # knobs are read when a context opens
+    dm.reserve(cfg, F, N)
+    s = torch.cuda.Stream()
 
-        def decode():
-            dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
-                             res.data_ptr(), pay.data_ptr(), stride, stream=torch.cuda.current_stream().cuda_stream)
+    def decode():
+        dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
+                         res.data_ptr(), pay.data_ptr(), stride, stream=torch.cuda.current_stream().cuda_stream)
 
-        with torch.cuda.stream(s):
-            decode()
-            decode()
-        torch.cuda.synchronize()
-    finally:
-        del os.environ["AMOD_GUARD_SCALE"]
+    with torch.cuda.stream(s):
+        decode()
+        decode()
+    torch.cuda.synchronize()
     ref_res, ref_pay = res.cpu().numpy().copy(), pay.cpu().numpy().copy()
     rec = np.frombuffer(ref_res.tobytes(), amodem.RESULT_DTYPE)
     assert ((rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY)) != 0).sum() > 0, np.unique(rec["flags"])

@@ -62,7 +62,9 @@ def test_host_pipeline_pieces(monkeypatch, piece):
     cfg, x, offs, lens = _batch()
     dm = amodem.Demodulator(0)
     ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
-    monkeypatch.setenv("AMOD_UP_PIECE", str(piece))
+    dm.close()
+    monkeypatch.setenv("AMOD_UP_PIECE", str(piece))  # read when a context opens
+    dm = amodem.Demodulator(0)
     rec, pay = dm.decode_batch(x, offs, lens, cfg=cfg)
     perm = np.random.default_rng(2).permutation(len(offs))
     rec2, pay2 = dm.decode_batch(x, offs[perm], lens[perm], cfg=cfg)
