@@ -94,6 +94,13 @@ class StreamStats(C.Structure):
                                           "final_scan_pos", "ema_chunks_fixed", "fine_host_positions")] + \
                [(n, C.c_double) for n in ("t_ema_ms", "t_fine_ms", "t_decode_ms", "t_host_ms", "t_total_ms")]
 
+class Shard(C.Structure):
+    """amod_shard: one group member's device-resident batch (include/amodem.h)."""
+    _fields_ = [("samples", C.c_void_p), ("offsets", C.c_void_p), ("lengths", C.c_void_p), ("results", C.c_void_p),
+                ("payload", C.c_void_p), ("payload_stride", C.c_int64), ("stream", C.c_void_p),
+                ("nframes", C.c_int32), ("reserved", C.c_int32)]
+
+
 class LiveStats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in ("total_written", "frames_decoded", "frame_errors", "refine_fails",
                                           "last_refine_fail", "fine_host_positions")]
@@ -165,6 +172,12 @@ SIGNATURES = {
     "amod_group_context": (_P, [_P, C.c_int32]),
     "amod_group_decode_host": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P, _P,
                                          C.c_int64, C.c_uint32, _P]),
+    "amod_group_decode_device": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_uint32]),
+    "amod_group_synchronize": (C.c_int, [_P]),
+    "amod_group_upload": (C.c_int, [_P, C.POINTER(Cfg), _P, C.c_int64, _P, _P, C.c_int32, C.POINTER(_P)]),
+    "amod_resident_decode": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, C.c_uint32, _P, _P, C.c_int64]),
+    "amod_resident_frames": (C.c_int32, [_P, _P]),
+    "amod_resident_free": (C.c_int, [_P]),
     "amod_live_open": (C.c_int, [_P, C.POINTER(Cfg), _P, C.POINTER(_P)]),
     "amod_live_process_block": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_int32)]),
     "amod_live_state": (C.c_int, [_P, C.POINTER(StreamState), C.POINTER(LiveStats)]),

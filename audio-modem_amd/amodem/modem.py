@@ -491,9 +491,74 @@ class DeviceGroup:
                                                split.ctypes.data))
         return rec, pay, split.tolist()
 
+    def decode_device(self, cfg: L.Cfg, mode: int, shards, options: int = 0):
+        """Enqueue every member's decode of its device-resident shard (amod_group_decode_device).
+        shards: one dict per member with device pointers samples / offsets / lengths /
+        results / payload (ints, e.g. torch .data_ptr()), nframes, payload_stride and an
+        optional stream (hipStream_t as int, 0 = the member context's). Returns without
+        synchronising (synchronize())."""
+        arr = (L.Shard * len(self.devices))()
+        for k, sh in enumerate(shards):
+            arr[k] = L.Shard(sh.get("samples", 0), sh.get("offsets", 0), sh.get("lengths", 0), sh.get("results", 0),
+                             sh.get("payload", 0), int(sh.get("payload_stride", 16)), sh.get("stream", 0) or None,
+                             int(sh.get("nframes", 0)), 0)
+        L.check(self._L.amod_group_decode_device(self._h, C.byref(cfg), mode, arr, options))
+
+    def synchronize(self):
+        L.check(self._L.amod_group_synchronize(self._h))
+
+    def upload(self, samples, offsets, lengths, cfg: L.Cfg) -> "ResidentBatch":
+        """Make a host batch resident across the group once (amod_group_upload); decode it
+        from HBM as often as needed with ResidentBatch.decode."""
+        return ResidentBatch(self, samples, offsets, lengths, cfg)
+
     def close(self):
         if self._h:
             self._L.amod_group_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ResidentBatch:
+    """A host batch resident across a DeviceGroup (amod_group_upload: contiguous frame
+    ranges of about equal sample counts, one per member); decode() runs every member's
+    device-path decode at once and returns records and payload rows in frame order."""
+
+    def __init__(self, group: DeviceGroup, samples, offsets, lengths, cfg: L.Cfg):
+        self._L = group._L
+        self._group = group  # (the group must outlive its resident batches)
+        x = np.ascontiguousarray(samples, np.float32)
+        off = np.ascontiguousarray(offsets, np.int64)
+        ln = np.ascontiguousarray(lengths, np.int32)
+        self.n = len(off)
+        self.max_len = int(ln.max()) if self.n else 1
+        h = C.c_void_p()
+        L.check(self._L.amod_group_upload(group._h, C.byref(cfg), x.ctypes.data, len(x), off.ctypes.data,
+                                          ln.ctypes.data, self.n, C.byref(h)))
+        self._h = h
+
+    def frames_per_device(self):
+        out = np.zeros(len(self._group.devices), np.int32)
+        self._L.amod_resident_frames(self._h, out.ctypes.data)
+        return out.tolist()
+
+    def decode(self, cfg: L.Cfg, mode: int = L.MODE_RECEIVED, options: int = 0):
+        """-> (RESULT_DTYPE records, payload uint8 [n, stride])."""
+        stride = payload_stride(cfg, self.max_len)
+        rec = np.zeros(self.n, RESULT_DTYPE)
+        pay = np.zeros((self.n, stride), np.uint8)
+        L.check(self._L.amod_resident_decode(self._h, C.byref(cfg), mode, options, rec.ctypes.data, pay.ctypes.data,
+                                             stride))
+        return rec, pay
+
+    def close(self):
+        if self._h:
+            self._L.amod_resident_free(self._h)
             self._h = None
 
     def __del__(self):

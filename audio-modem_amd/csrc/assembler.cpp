@@ -19,6 +19,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <string>
@@ -28,17 +29,25 @@
 #include "amodem.h"
 
 // The file-layout store: totalChunks x chunkSize bytes, chunk seq at seq * chunkSize, mapped
-// at the metadata frame with huge pages where the kernel offers them, and populated by a
-// helper thread (MADV_POPULATE_WRITE, contents untouched) while the receiver is still
-// scanning, so the chunk stores that follow do not pay first-touch faults one page at a
-// time (32k 2 KB chunks: 65 MB).
+// at the metadata frame (address space only: MAP_NORESERVE, huge pages where the kernel
+// offers them). A helper thread pre-faults the first kPopulateMax bytes of it
+// (MADV_POPULATE_WRITE, contents untouched) while the receiver is still scanning, so the
+// chunk stores that follow do not pay first-touch faults one page at a time (32k 2 KB
+// chunks: 65 MB); pages past that window fault in as chunks arrive, so a header that
+// claims a large file commits memory only for the chunks actually received (the reference
+// allocates the file only in assembleFile, app.js:668). release() stops the helper at its
+// next step instead of waiting for the whole window.
 struct FileArena {
+  static constexpr size_t kPopulateMax = size_t(256) << 20;
   uint8_t *p = nullptr;
   size_t n = 0;
   std::thread filler;
+  std::atomic<bool> stop{false};
   ~FileArena() { release(); }
   void release() {
+    stop.store(true, std::memory_order_relaxed);
     if (filler.joinable()) filler.join();
+    stop.store(false, std::memory_order_relaxed);
     if (p) munmap(p, n);
     p = nullptr;
     n = 0;
@@ -46,7 +55,7 @@ struct FileArena {
   bool map(size_t bytes) {
     release();
     if (!bytes) return false;
-    void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
     if (q == MAP_FAILED) return false;
     p = (uint8_t *)q;
     n = bytes;
@@ -54,12 +63,12 @@ struct FileArena {
     (void)madvise(p, n, MADV_HUGEPAGE);
 #endif
     if (getenv("AMOD_ASM_NO_POPULATE")) return true; // (experiments: first-touch faults in the copies)
-    filler = std::thread([q = p, len = n] {
+    filler = std::thread([q = p, len = std::min(n, kPopulateMax), halt = &stop] {
       constexpr int kPopulateWrite = 23; // MADV_POPULATE_WRITE (Linux 5.14)
       // one huge page per call: each call holds the address-space lock (read) while it
       // zeroes, and the receiver's own mappings (thread stacks, vectors) wait for it
       constexpr size_t kStep = size_t(2) << 20;
-      for (size_t o = 0; o < len; o += kStep) {
+      for (size_t o = 0; o < len && !halt->load(std::memory_order_relaxed); o += kStep) {
         const size_t m = std::min(kStep, len - o);
         if (madvise(q + o, m, kPopulateWrite) != 0) { // older kernels: touch every page, value kept
           for (size_t b = o; b < o + m; b += 4096) __atomic_fetch_add(q + b, (uint8_t)0, __ATOMIC_RELAXED);

@@ -21,6 +21,10 @@
  *   txTestSignal(cfg) -> Float32Array                                   modem.js:914-973
  *   estimateFrameSamples(cfg, payloadBytes) -> number                   modem.js:863-874
  *   numDataSubs(cfg) -> number, payloadStride(cfg, maxLen) -> number, abiVersion() -> number
+ *   residentUpload(samples, offsets, lengths, cfg, ndevices) -> { handle, nframes, maxLen,
+ *          framesPerDevice }: the batch made resident across GPUs 0 .. n-1 (amod_group_upload)
+ *   residentDecodeAsync(handle, cfg, mode, options) -> Promise of { results, payload, stride }
+ *          (amod_resident_decode: every GPU decodes its resident shard, no upload)
  *
  * cfg = { fft_size, cp_len, symbol_len, sample_rate, sub_start, sub_end,
  *         pilots: number[], modulation: 0|1|2, repetition }
@@ -131,11 +135,35 @@ static int is_nullish(napi_env env, napi_value v) {
   return napi_typeof(env, v, &t) == napi_ok && (t == napi_null || t == napi_undefined);
 }
 
+/* the group of GPUs 0 .. n-1, opened on first use (AMODEM_GROUP_DEVICES="0,0": the device
+   list to use instead, tests on one GPU); throws and returns NULL on failure */
+static amod_group *get_group(napi_env env, int32_t ndev) {
+  if (ndev < 1 || ndev > MAX_DEVICES) {
+    napi_throw_range_error(env, NULL, "devices out of range");
+    return NULL;
+  }
+  if (!g_group[ndev]) {
+    int32_t ids[MAX_DEVICES];
+    for (int32_t i = 0; i < ndev; ++i) ids[i] = i;
+    const char *lst = getenv("AMODEM_GROUP_DEVICES");
+    for (int32_t i = 0; lst && *lst && i < ndev; ++i) {
+      ids[i] = (int32_t)strtol(lst, (char **)&lst, 10);
+      if (*lst == ',') ++lst;
+    }
+    if (amod_group_open(ids, ndev, &g_group[ndev]) != AMOD_SUCCESS) {
+      throw_msg(env, amod_last_error(NULL));
+      return NULL;
+    }
+  }
+  return g_group[ndev];
+}
+
 /* ------------------------------------------------------------------ decode */
 typedef struct {
   amod_ctx *ctx;
   amod_cfg cfg;
   amod_group *group; /* decodeBatch(..., {devices: n > 1}): the batch split across n GPUs */
+  amod_resident *resident; /* residentDecodeAsync: a batch already resident on the GPUs */
   int32_t mode, nframes;
   uint32_t options;
   const float *samples;
@@ -182,19 +210,8 @@ static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_va
   int32_t ndev = 1;
   if (argc >= 8 && !is_nullish(env, argv[7]) && napi_get_value_int32(env, argv[7], &ndev) != napi_ok) ndev = 1;
   if (ndev > 1) {
-    if (ndev > MAX_DEVICES) return napi_throw_range_error(env, NULL, "devices out of range"), 0;
-    if (!g_group[ndev]) {
-      int32_t ids[MAX_DEVICES];
-      for (int32_t i = 0; i < ndev; ++i) ids[i] = i;
-      /* AMODEM_GROUP_DEVICES="0,0": the device list to use instead (tests on one GPU) */
-      const char *lst = getenv("AMODEM_GROUP_DEVICES");
-      for (int32_t i = 0; lst && *lst && i < ndev; ++i) {
-        ids[i] = (int32_t)strtol(lst, (char **)&lst, 10);
-        if (*lst == ',') ++lst;
-      }
-      if (amod_group_open(ids, ndev, &g_group[ndev]) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(NULL)), 0;
-    }
-    j->group = g_group[ndev];
+    j->group = get_group(env, ndev);
+    if (!j->group) return 0;
   } else {
     j->ctx = get_ctx(env, device);
     if (!j->ctx) return 0;
@@ -254,7 +271,10 @@ static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_va
 }
 
 static void run_decode(decode_job *j) {
-  if (j->group)
+  if (j->resident)
+    j->rc = amod_resident_decode(j->resident, &j->cfg, j->mode, j->options, (amod_result *)j->results,
+                                 (uint8_t *)j->payload, j->stride);
+  else if (j->group)
     j->rc = amod_group_decode_host(j->group, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths,
                                    j->nframes, (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options,
                                    NULL);
@@ -262,7 +282,7 @@ static void run_decode(decode_job *j) {
     j->rc = amod_decode_host(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths, j->nframes,
                              (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options);
   if (j->rc != AMOD_SUCCESS) {
-    const char *e = amod_last_error(j->group ? NULL : j->ctx);
+    const char *e = amod_last_error(j->group || j->resident ? NULL : j->ctx);
     snprintf(j->err, sizeof j->err, "libamodem error %d: %s", j->rc, e ? e : "");
   }
 }
@@ -345,6 +365,123 @@ static napi_value js_decode_async(napi_env env, napi_callback_info info) {
   napi_value promise, name;
   NAPI_TRY(env, napi_create_promise(env, &j->deferred, &promise));
   NAPI_TRY(env, napi_create_string_utf8(env, "amodem.decode", NAPI_AUTO_LENGTH, &name));
+  NAPI_TRY(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
+  NAPI_TRY(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+/* ------------------------------------------------------- resident batches */
+typedef struct {
+  amod_resident *r;
+  int32_t nframes, max_len;
+} resident_box;
+
+static void resident_finalize(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  resident_box *b = (resident_box *)data;
+  amod_resident_free(b->r);
+  free(b);
+}
+
+static napi_value js_resident_upload(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 5)
+    return napi_throw_type_error(env, NULL, "residentUpload(samples, offsets, lengths, cfg, ndevices)"), NULL;
+  void *sp, *op, *lp;
+  size_t ns, no, nl;
+  if (!typed(env, argv[0], napi_float32_array, &sp, &ns) || !typed(env, argv[1], napi_float64_array, &op, &no) ||
+      !typed(env, argv[2], napi_int32_array, &lp, &nl) || no != nl || no > INT32_MAX)
+    return napi_throw_type_error(env, NULL, "samples: Float32Array, offsets: Float64Array, lengths: Int32Array"), NULL;
+  amod_cfg cfg;
+  if (!to_cfg(env, argv[3], &cfg)) return NULL;
+  int32_t ndev = 1;
+  if (napi_get_value_int32(env, argv[4], &ndev) != napi_ok) ndev = 1;
+  amod_group *g = get_group(env, ndev);
+  if (!g) return NULL;
+  int64_t *offs = (int64_t *)malloc(sizeof(int64_t) * (no ? no : 1));
+  if (!offs) return throw_msg(env, "out of memory");
+  const double *od = (const double *)op;
+  const int32_t *ld = (const int32_t *)lp;
+  int32_t max_len = 0;
+  for (size_t i = 0; i < no; ++i) {
+    if (!(od[i] >= 0) || od[i] != (double)(int64_t)od[i] || ld[i] < 0 || (int64_t)od[i] + ld[i] > (int64_t)ns) {
+      free(offs);
+      return napi_throw_range_error(env, NULL, "frame slice outside the sample buffer"), NULL;
+    }
+    offs[i] = (int64_t)od[i];
+    if (ld[i] > max_len) max_len = ld[i];
+  }
+  resident_box *b = (resident_box *)calloc(1, sizeof *b);
+  if (!b) {
+    free(offs);
+    return throw_msg(env, "out of memory");
+  }
+  const int rc = amod_group_upload(g, &cfg, (const float *)sp, (int64_t)ns, offs, ld, (int32_t)no, &b->r);
+  free(offs);
+  if (rc != AMOD_SUCCESS) {
+    free(b);
+    return throw_msg(env, amod_last_error(NULL));
+  }
+  b->nframes = (int32_t)no;
+  b->max_len = max_len;
+  napi_value out, h, v, arr;
+  if (napi_create_external(env, b, resident_finalize, NULL, &h) != napi_ok) {
+    resident_finalize(env, b, NULL);
+    return throw_msg(env, "napi_create_external failed");
+  }
+  NAPI_TRY(env, napi_create_object(env, &out));
+  NAPI_TRY(env, napi_set_named_property(env, out, "handle", h));
+  NAPI_TRY(env, napi_create_int32(env, b->nframes, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "nframes", v));
+  NAPI_TRY(env, napi_create_int32(env, max_len, &v));
+  NAPI_TRY(env, napi_set_named_property(env, out, "maxLen", v));
+  int32_t per[MAX_DEVICES];
+  amod_resident_frames(b->r, per);
+  NAPI_TRY(env, napi_create_array_with_length(env, (size_t)ndev, &arr));
+  for (int32_t k = 0; k < ndev; ++k) {
+    NAPI_TRY(env, napi_create_int32(env, per[k], &v));
+    NAPI_TRY(env, napi_set_element(env, arr, (uint32_t)k, v));
+  }
+  NAPI_TRY(env, napi_set_named_property(env, out, "framesPerDevice", arr));
+  return out;
+}
+
+static napi_value js_resident_decode_async(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 4)
+    return napi_throw_type_error(env, NULL, "residentDecodeAsync(handle, cfg, mode, options)"), NULL;
+  resident_box *b = NULL;
+  if (napi_get_value_external(env, argv[0], (void **)&b) != napi_ok || !b || !b->r)
+    return napi_throw_type_error(env, NULL, "handle must come from residentUpload"), NULL;
+  decode_job *j = (decode_job *)calloc(1, sizeof *j);
+  if (!j) return throw_msg(env, "out of memory");
+  if (!to_cfg(env, argv[1], &j->cfg)) {
+    free(j);
+    return NULL;
+  }
+  if (napi_get_value_int32(env, argv[2], &j->mode) != napi_ok) {
+    free(j);
+    return napi_throw_type_error(env, NULL, "mode must be a number"), NULL;
+  }
+  if (napi_get_value_uint32(env, argv[3], &j->options) != napi_ok) j->options = 0;
+  j->resident = b->r;
+  j->nframes = b->nframes;
+  j->stride = amod_payload_stride(&j->cfg, b->max_len);
+  if (napi_create_arraybuffer(env, (size_t)j->nframes * sizeof(amod_result), &j->results, &j->res_ab) != napi_ok ||
+      napi_create_arraybuffer(env, (size_t)j->nframes * (size_t)j->stride, &j->payload, &j->pay_ab) != napi_ok) {
+    free(j);
+    return throw_msg(env, "cannot allocate decode outputs");
+  }
+  /* keep the handle (and so the resident batch) alive until the decode completes */
+  napi_create_reference(env, argv[0], 1, &j->refs[0]);
+  napi_create_reference(env, j->res_ab, 1, &j->res_ref);
+  napi_create_reference(env, j->pay_ab, 1, &j->pay_ref);
+  napi_value promise, name;
+  NAPI_TRY(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_TRY(env, napi_create_string_utf8(env, "amodem.residentDecode", NAPI_AUTO_LENGTH, &name));
   NAPI_TRY(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
   NAPI_TRY(env, napi_queue_async_work(env, j->work));
   return promise;
@@ -846,6 +983,8 @@ static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor props[] = {
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decodeAsync", NULL, js_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"residentUpload", NULL, js_resident_upload, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"residentDecodeAsync", NULL, js_resident_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"loopback", NULL, js_loopback, NULL, NULL, NULL, napi_enumerable, NULL},
       {"crc32", NULL, js_crc32, NULL, NULL, NULL, napi_enumerable, NULL},
       {"preamble1", NULL, js_preamble1, NULL, NULL, NULL, napi_enumerable, NULL},

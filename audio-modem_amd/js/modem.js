@@ -267,8 +267,8 @@ function utf8(bytes, off, len) {
 
 // one amod_result record (+ its payload slot) -> the reference's return object.
 // share = false: `data` is a fresh Uint8Array (bytes.slice, modem.js:636,837); share =
-// true (decodeBatch): `data` is a view of the call's own payload buffer (every frame's
-// range its own, nothing else holds the buffer), which spares one allocation per frame
+// true (decodeBatch's opt-in shareBuffers): `data` is a view of the call's own payload
+// buffer (every frame's range its own), which spares one allocation per frame
 function formatResult(view, i, payload, stride, viaLegacy, share, u8) {
   const o = i * REC;
   const status = view.getInt32(o, true);
@@ -336,26 +336,60 @@ function decodeChunkFrame(frameSamples, modName, repetition) {
   return decodeOne(frameSamples, modName, repetition, MODE_CHUNK);
 }
 
-// decodeBatch(samples, frameOffsets, frameLens, modName, rep, {device, devices, mode})
-// -> Promise<result[]>: many frames of one buffer in one GPU launch (additive API);
-// devices: n > 1 splits the batch into contiguous frame ranges over GPUs 0 .. n-1,
-// decoded concurrently (amod_group_decode_host), results in frame order.
+// decodeBatch(samples, frameOffsets, frameLens, modName, rep, {device, devices, mode,
+// shareBuffers}) -> Promise<result[]>: many frames of one buffer in one GPU launch
+// (additive API); devices: n > 1 splits the batch into contiguous frame ranges over GPUs
+// 0 .. n-1, decoded concurrently (amod_group_decode_host), results in frame order.
+// samples may also be a DeviceBatch (uploadBatch): its frames are decoded from HBM on the
+// GPUs they were uploaded to (amod_resident_decode), frameOffsets / frameLens ignored.
+// Every result's `data` is a fresh Uint8Array, as the reference's (bytes.slice,
+// modem.js:636,837); shareBuffers: true makes them views of one payload buffer per call
+// instead (no per-frame copy; `data.buffer` then holds every frame's bytes, and keeping
+// one result keeps that buffer alive).
 function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
   const o = opts || {};
   const mode = o.mode === 'chunk' || o.mode === MODE_CHUNK ? MODE_CHUNK : MODE_RECEIVED;
   const cfg = nativeCfg(modName, rep);
+  const share = o.shareBuffers === true;
+  if (samples instanceof DeviceBatch) {
+    return native.residentDecodeAsync(samples.handle, cfg, mode, o.forceExact ? 1 : 0)
+      .then((out) => formatBatch(out.results, out.payload, out.stride, samples.nframes, mode === MODE_RECEIVED, share));
+  }
   const offs = frameOffsets instanceof Float64Array ? frameOffsets : Float64Array.from(frameOffsets);
   const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
   return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0,
     Math.max(1, o.devices | 0))
-    .then((out) => formatBatch(out.results, out.payload, out.stride, lens.length, mode === MODE_RECEIVED));
+    .then((out) => formatBatch(out.results, out.payload, out.stride, lens.length, mode === MODE_RECEIVED, share));
+}
+
+// A batch made resident on GPUs 0 .. devices-1 once (amod_group_upload: contiguous frame
+// ranges of about equal sample counts), for decodeBatch to decode from HBM as often as
+// needed (a Node host driving several GPUs without one upload per decode).
+class DeviceBatch {
+  constructor(up, devices) {
+    this.handle = up.handle;
+    this.nframes = up.nframes;
+    this.maxLen = up.maxLen;
+    this.devices = devices;
+    this.framesPerDevice = up.framesPerDevice;
+  }
+}
+
+// uploadBatch(samples, frameOffsets, frameLens, modName, rep, {devices}) -> DeviceBatch
+function uploadBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
+  const o = opts || {};
+  const devices = Math.max(1, o.devices | 0);
+  const offs = frameOffsets instanceof Float64Array ? frameOffsets : Float64Array.from(frameOffsets);
+  const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
+  return new DeviceBatch(native.residentUpload(asFloat32(samples), offs, lens, nativeCfg(modName, rep), devices),
+    devices);
 }
 
 // every record of a batch -> the reference's result objects, in frame order
-function formatBatch(results, payload, stride, n, viaLegacy) {
+function formatBatch(results, payload, stride, n, viaLegacy, share) {
   const view = new DataView(results), u8 = new Uint8Array(payload);
   const res = new Array(n);
-  for (let i = 0; i < n; i++) res[i] = formatResult(view, i, payload, stride, viaLegacy, true, u8);
+  for (let i = 0; i < n; i++) res[i] = formatResult(view, i, payload, stride, viaLegacy, share === true, u8);
   return res;
 }
 
@@ -536,7 +570,8 @@ const api = {
   fft, OFDM_CONFIGS, OFDM, setOFDMConfig, Constellations, generatePreambleSymbol1, buildTransmitSignal,
   decodeReceivedSignal, FRAME_META, FRAME_DATA, buildMetadataFrame, buildDataChunkFrame, decodeChunkFrame,
   estimateFrameSamples, generateSweepTone, generateTestSignal, analyzeLoopback,
-  decodeBatch, crc32: (data) => native.crc32(toBytes(data)), native, ChunkAssembler, receiveStream,
+  decodeBatch, uploadBatch, DeviceBatch, crc32: (data) => native.crc32(toBytes(data)), native, ChunkAssembler,
+  receiveStream,
   StreamingReceiver, RECV_STATE, _formatBatch: formatBatch,
 };
 

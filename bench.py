@@ -572,6 +572,66 @@ def host_api_leg(env: Env, wl: Workload, reps=3):
     return out
 
 
+def c1_latency_leg(env: Env, calls=200):
+    """The drop-in as its caller uses it (app.js:513): ONE C1 recording (QPSK 1 KB legacy
+    frame, 35,874 samples) through the synchronous decodeReceivedSignal, per-call latency
+    (host samples in: H2D, launches, sync, D2H, the result object), from Node.js
+    (js/modem.js -> N-API -> amod_decode_host) and from Python (amod_decode_host), next to
+    the JS restatement of the reference decoding the same frame on one core
+    (oracle/rx_cpu.js; BASELINE.md: modem.js 2.75 ms per C1 frame in the build container)."""
+    amodem = env.amodem
+    cfg = amodem.preset("standard", "QPSK", 1)
+    data = amodem.synth_payload(0x9E3779B9, PAYLOAD)
+    sig = np.ascontiguousarray(amodem.build_transmit_signal(data, file_name="f.bin", cfg=cfg), np.float32)
+    out = {"workload": f"C1: one QPSK 1 KB legacy frame ({len(sig)} samples), decodeReceivedSignal"}
+    dm = amodem.Demodulator(env.local)
+    try:
+        for _ in range(20):
+            r = dm.decode_received_signal(sig, "QPSK", 1)
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            r = dm.decode_received_signal(sig, "QPSK", 1)
+            ts.append((time.perf_counter() - t0) * 1e3)
+    finally:
+        dm.close()
+    ts.sort()
+    out["python_decode_received_signal"] = {"median_ms": ts[len(ts) // 2], "p90_ms": ts[int(0.9 * len(ts))],
+                                            "calls": calls, "crcValid": bool(r.get("crcValid")) and r.get("data") == data}
+    node = shutil_which("node")
+    with tempfile.TemporaryDirectory() as tmp:
+        xf = os.path.join(tmp, "c1.f32")
+        sig.tofile(xf)
+        if node and os.path.exists(os.path.join(ROOT, "audio-modem_amd", "lib", "amodem.node")):
+            spec = os.path.join(tmp, "lat.json")
+            with open(spec, "w") as f:
+                json.dump({"samples": xf, "preset": "standard", "mod": "QPSK", "rep": 1, "warmup": 20,
+                           "calls": calls}, f)
+            r = subprocess.run([node, os.path.join(ROOT, "tools", "node_latency.js"), spec], capture_output=True,
+                               text=True, timeout=300)
+            out["node_decode_received_signal"] = json.loads(r.stdout) if r.returncode == 0 else {"error": r.stderr[-400:]}
+        if node:  # the CPU baseline: the same frame, one thread (test infrastructure under oracle/)
+            spec = os.path.join(tmp, "cpu.json")
+            with open(spec, "w") as f:
+                json.dump({"samples": xf, "offsets": [0], "lengths": [len(sig)], "preset": "standard", "mod": "QPSK",
+                           "rep": 1, "chunk": False, "threads": 1, "seconds": 0.5, "single_frames": 1,
+                           "single_seconds": 2.0}, f)
+            r = subprocess.run([node, os.path.join(ROOT, "oracle", "rx_cpu.js"), "bench", spec], capture_output=True,
+                               text=True, timeout=300)
+            if r.returncode == 0:
+                j = json.loads(r.stdout)
+                out["cpu_js_one_core"] = {"ms_per_call": len(sig) / j["single_core"] * 1e3, "kind": "port",
+                                          "what": "oracle/rx_cpu.js (JS restatement of modem.js) on one thread, the "
+                                                  "same frame repeated for 2 s", "calibration": calibration_note("c2")}
+            else:
+                out["cpu_js_one_core"] = {"error": r.stderr[-400:]}
+    nl = out.get("node_decode_received_signal", {})
+    cj = out.get("cpu_js_one_core", {})
+    if "median_ms" in nl and "ms_per_call" in cj:
+        out["speedup_vs_cpu_js"] = cj["ms_per_call"] / nl["median_ms"]
+    return out
+
+
 def shutil_which(name):
     import shutil
     return shutil.which(name)
@@ -764,8 +824,11 @@ def run_leg(env: Env, conf: str, args, frames=0, snr=20.0, primary=False):
         out["gather"] = gather_leg(env, wl)
     if primary and not args.no_e2e:
         out["e2e"] = e2e_leg(env, wl)
-        if env.rank == 0 and env.world == 1:
-            out["host_api"] = host_api_leg(env, wl)
+    # the host entries (Python amod_decode_host, Node decodeBatch) on the batches a host can
+    # hold in one Float32Array comfortably (C3's 12 GB is device-path only)
+    if not args.no_e2e and conf != "c3" and env.rank == 0 and env.world == 1:
+        progress(f"{conf}: host API legs (amod_decode_host from Python, decodeBatch from Node)")
+        out["host_api"] = host_api_leg(env, wl)
     if env.rank == 0 and env.world == 1 and args.cpu_frames >= 0:
         progress(f"{conf}: CPU legs (C oracle over the whole batch, JS baseline on worker_threads)")
         js_frames = args.cpu_frames or (640 if conf != "c5" else 192)
@@ -788,7 +851,7 @@ def main():
                          "256 B frames + AWGN (--snr)")
     ap.add_argument("--legs", default="auto",
                     help="extra legs after the primary one: comma list of c3,c4,c5 (c5 at 10 dB), 'none'; "
-                         "auto = c4,c5 with --config c2")
+                         "auto = c3,c4,c5 with --config c2")
     ap.add_argument("--snr", type=float, default=20.0, help="c5: AWGN SNR in dB (active-sample power)")
     ap.add_argument("--soft", action="store_true", help="c5: also decode once with AMOD_OPT_SOFT_COMBINE")
     ap.add_argument("--frames", type=int, default=0,
@@ -818,13 +881,17 @@ def main():
     if args.stream_chunks < 0:
         args.stream_chunks = 32000 if args.config == "c2" else 0
     legs = [] if args.legs == "none" else (
-        (["c4", "c5"] if args.config == "c2" else []) if args.legs == "auto" else args.legs.split(","))
+        (["c3", "c4", "c5"] if args.config == "c2" else []) if args.legs == "auto" else args.legs.split(","))
     # the streaming receiver first (its host phases idle the GPU; rank 0 only)
     if args.stream_chunks > 0 and env.rank == 0:
         progress(f"streaming receiver over {args.stream_chunks} chunks")
     stream_res = stream_leg(env, args.stream_chunks) if (args.stream_chunks > 0 and env.rank == 0) else None
     env.barrier()
     prim = run_leg(env, args.config, args, frames=args.frames, snr=args.snr, primary=True)
+    lat = None
+    if env.rank == 0 and env.world == 1 and not args.no_e2e:
+        progress("c1_latency: one frame through the synchronous drop-in")
+        lat = c1_latency_leg(env)
     extra = {}
     for lg in legs:
         name = lg if lg != "c5" else "c5_10db"
@@ -840,6 +907,8 @@ def main():
         out["devices"] = env.devices_used
         out["stream"] = stream_res
         out["legs"] = extra
+        if lat is not None:
+            out["legs"]["c1_latency"] = lat
         print(json.dumps(out), flush=True)
     if env.world > 1:
         env.dist.destroy_process_group()

@@ -322,6 +322,41 @@ int amod_group_decode_host(amod_group *g, const amod_cfg *cfg, int32_t mode, con
                            const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
                            uint8_t *payload, int64_t payload_stride, uint32_t options, int32_t *frames_per_device);
 
+/* Device-resident shards, one per group member (frames independent: modem.js:557,770, so
+ * no exchange between devices). Shard k's pointers are memory on member k's device (as
+ * amod_decode_device: samples 16-byte aligned, frames [offsets[i], offsets[i]+lengths[i])
+ * of its own buffer); stream = a hipStream_t of that device, NULL = the member context's
+ * stream. Every member's decode is enqueued from the calling thread and the call returns
+ * without synchronising (amod_group_synchronize waits for the members' own streams).
+ * Shards with nframes == 0 are skipped. */
+typedef struct amod_shard {
+  const float *samples;
+  const int64_t *offsets;
+  const int32_t *lengths;
+  amod_result *results;
+  uint8_t *payload;
+  int64_t payload_stride;
+  void *stream;
+  int32_t nframes;
+  int32_t reserved;
+} amod_shard;
+int amod_group_decode_device(amod_group *g, const amod_cfg *cfg, int32_t mode, const amod_shard *shards,
+                             uint32_t options);
+int amod_group_synchronize(amod_group *g);
+
+/* A host batch made resident across a group once (the split of amod_group_decode_host:
+ * contiguous frame ranges of about equal sample counts) and decoded from HBM as often as
+ * the caller likes: amod_resident_decode runs amod_group_decode_device over the resident
+ * shards and copies every member's records and payload rows into the caller's host arrays
+ * at their frame index (one D2H per member, no gather), then synchronises. */
+typedef struct amod_resident amod_resident;
+int amod_group_upload(amod_group *g, const amod_cfg *cfg, const float *samples, int64_t nsamples,
+                      const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_resident **out);
+int amod_resident_decode(amod_resident *r, const amod_cfg *cfg, int32_t mode, uint32_t options,
+                         amod_result *results, uint8_t *payload, int64_t payload_stride);
+int32_t amod_resident_frames(const amod_resident *r, int32_t *frames_per_device);
+int amod_resident_free(amod_resident *r);
+
 /* ---- streaming receive: app.js StreamingReceiver (706-998) over a recorded stream ----
  * The stream is cut into 4096-sample blocks (the ScriptProcessor size; a last partial
  * block is completed with zeros) and run through the reference's receiver: EMA DC

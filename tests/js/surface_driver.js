@@ -48,8 +48,22 @@ async function main() {
         case 'decode': r = M.decodeReceivedSignal(f32(j.file), j.mod, j.rep); break;
         case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
         case 'loopback': r = M.analyzeLoopback(f32(j.file), j.mod, j.rep, Uint8Array.from(j.testData)); break;
-        case 'decode_batch': r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep,
-          { mode: j.mode, devices: j.devices }); break;
+        case 'decode_batch': {
+          r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep,
+            { mode: j.mode, devices: j.devices, shareBuffers: j.share === true });
+          // data ownership: fresh arrays (the reference's bytes.slice) unless shareBuffers
+          const own = r.every((x) => !x.data || (x.data.byteOffset === 0 && x.data.buffer.byteLength === x.data.length));
+          r = { results: r, ownData: own };
+          break;
+        }
+        case 'decode_resident': {
+          // uploadBatch once, decodeBatch(DeviceBatch) twice: both from HBM
+          const b = M.uploadBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { devices: j.devices });
+          const r1 = await M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode });
+          const r2 = await M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode });
+          r = { first: r1, second: r2, framesPerDevice: b.framesPerDevice, isDeviceBatch: b instanceof M.DeviceBatch };
+          break;
+        }
         case 'asm': {
           // one ChunkAssembler scenario (tests/golden/assembler.json ops); state after each op
           const a = new M.ChunkAssembler(j.directory ? { directory: j.directory } : undefined);

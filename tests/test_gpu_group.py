@@ -80,3 +80,73 @@ def test_host_pipeline_pieces(monkeypatch, piece):
     assert np.array_equal(pay, rpay) and np.array_equal(pay2[inv], rpay)
     assert np.array_equal(pay3, rpay[dup])
     assert (ref["status"] == 0).all()
+
+
+def _assert_same(rec, pay, ref, rpay):
+    for n in amodem.RESULT_DTYPE.names:
+        if n == "reserved":
+            continue
+        assert (rec[n] == ref[n]).all(), n
+    assert np.array_equal(pay, rpay)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_resident_group_equals_single_context(devices):
+    """amod_group_upload + amod_resident_decode: the batch resident across the group's
+    members once, decoded from HBM twice (device path on every member at once, one D2H
+    per member): whole records and payload rows equal the single-context decode."""
+    cfg, x, offs, lens = _batch()
+    dm = amodem.Demodulator(0)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    dm.close()
+    g = amodem.DeviceGroup(devices)
+    rb = g.upload(x, offs, lens, cfg)
+    split = rb.frames_per_device()
+    rec, pay = rb.decode(cfg)
+    rec2, pay2 = rb.decode(cfg)
+    rb.close()
+    g.close()
+    assert sum(split) == len(offs) and len(split) == len(devices)
+    _assert_same(rec, pay, ref, rpay)
+    _assert_same(rec2, pay2, ref, rpay)
+
+
+def test_group_decode_device_torch_shards():
+    """amod_group_decode_device over caller-owned device buffers (torch tensors) and a
+    caller stream: member k decodes its own shard; records equal the single-context
+    decode of the same frames."""
+    import torch
+    cfg, x, offs, lens = _batch()
+    dm = amodem.Demodulator(0)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    dm.close()
+    dev = torch.device("cuda", 0)
+    stride = amodem.payload_stride(cfg, int(lens.max()))
+    halves = [(0, len(offs) // 2), (len(offs) // 2, len(offs))]
+    g = amodem.DeviceGroup([0, 0])
+    keep, shards = [], []
+    s = torch.cuda.Stream(dev)
+    for k, (a, b) in enumerate(halves):
+        lo = int(offs[a]) & ~3
+        hi = int((offs[a:b] + lens[a:b]).max())
+        xs = torch.zeros(hi - lo + 16, dtype=torch.float32, device=dev)
+        xs[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
+        d_off = torch.from_numpy((offs[a:b] - lo).astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens[a:b].astype(np.int32)).to(dev)
+        res = torch.zeros((b - a) * 96, dtype=torch.uint8, device=dev)
+        pay = torch.zeros((b - a) * stride, dtype=torch.uint8, device=dev)
+        g_ctx = L.load().amod_group_context(g._h, k)
+        L.check(L.load().amod_reserve(g_ctx, L.C.byref(cfg), b - a, int(lens[a:b].max())))
+        keep += [xs, d_off, d_len, res, pay]
+        shards.append({"samples": xs.data_ptr(), "offsets": d_off.data_ptr(), "lengths": d_len.data_ptr(),
+                       "results": res.data_ptr(), "payload": pay.data_ptr(), "payload_stride": stride,
+                       "nframes": b - a, "stream": s.cuda_stream if k == 0 else 0})
+    torch.cuda.synchronize()
+    g.decode_device(cfg, L.MODE_RECEIVED, shards)
+    g.synchronize()
+    s.synchronize()
+    rec = np.concatenate([np.frombuffer(keep[5 * k + 3].cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
+                          for k in range(2)])
+    pay = np.concatenate([keep[5 * k + 4].cpu().numpy().reshape(-1, stride) for k in range(2)])
+    g.close()
+    _assert_same(rec, pay, ref, rpay)

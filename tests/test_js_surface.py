@@ -53,7 +53,7 @@ def ok(res, key):
 
 def test_exports(tmp_path):
     names = ok(run([{"op": "exports", "id": "e"}], tmp_path), "e")
-    for g in GLOBALS + ["decodeBatch"]:
+    for g in GLOBALS + ["decodeBatch", "uploadBatch", "DeviceBatch"]:
         assert g in names, g
 
 
@@ -198,9 +198,35 @@ def test_decode_batch_through_js(tmp_path):
     fn = tmp_path / "batch.f32"
     np.concatenate(xs).astype(np.float32).tofile(fn)
     res = run([{"op": "decode_batch", "config": "standard", "file": str(fn), "offsets": offs,
-                "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1, "id": "b"}], tmp_path)
+                "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1, "id": "b"},
+               {"op": "decode_batch", "config": "standard", "file": str(fn), "offsets": offs,
+                "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1, "share": True, "id": "s"}], tmp_path)
     got = ok(res, "b")
-    assert got == [f["result"] for f in sel]
+    assert got["results"] == [f["result"] for f in sel]
+    assert got["ownData"]  # every `data` a fresh Uint8Array, as bytes.slice (modem.js:636,837)
+    shared = ok(res, "s")  # shareBuffers: the same results, views of one payload buffer
+    assert shared["results"] == got["results"] and not shared["ownData"]
+
+
+@pytest.mark.gpu
+def test_resident_batch_through_js(tmp_path):
+    """uploadBatch (amod_group_upload) makes the batch resident on two GPU contexts
+    (device 0 twice on the one-GPU box) once; decodeBatch(DeviceBatch) decodes it from
+    HBM (amod_resident_decode), twice: the reference result objects in frame order."""
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["mod"] == "QPSK"
+           and f["rep"] == 1]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    res = run([{"op": "decode_resident", "config": "standard", "file": str(fn), "offsets": offs,
+                "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1, "devices": 2, "id": "r"}], tmp_path,
+              env={"AMODEM_GROUP_DEVICES": "0,0"})
+    got = ok(res, "r")
+    want = [f["result"] for f in sel]
+    assert got["isDeviceBatch"] and sum(got["framesPerDevice"]) == len(sel)
+    assert got["first"] == want and got["second"] == want
 
 
 def _lb_num(v):
@@ -376,4 +402,4 @@ def test_decode_batch_devices_through_js(tmp_path):
                      "lengths": [len(xs[i]) for i in idx], "mod": mod, "rep": 1, "devices": 2, "id": mod})
     res = run(jobs, tmp_path, env={"AMODEM_GROUP_DEVICES": "0,0"})
     for mod, idx in groups.items():
-        assert ok(res, mod) == [sel[i]["result"] for i in idx], mod
+        assert ok(res, mod)["results"] == [sel[i]["result"] for i in idx], mod
