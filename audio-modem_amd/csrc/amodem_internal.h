@@ -27,7 +27,8 @@ constexpr int kMaxBand = 256;  // sub_end < fft/2
 constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
 constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
-constexpr int kCrcMats = 512;  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+constexpr int kCrcMats = 512;
+constexpr int kTlHead = 4;     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
 
 // Device-resident tables, built once per configuration by the runtime.
 struct DevTables {
@@ -137,8 +138,10 @@ struct DevWork {
   // the next decode needs no memset dispatch (null: no reset)
   int32_t *fb_reset;
   // profiled decodes only (amod_aux_overlap): device real-time marks, [0] the first listed
-  // frame list A's replica took (min), [1] the last k_demod wave's end (max), [2] the first
-  // k_demod wave's start (min); k_detect / k_chunk_prep's workgroup 0 initialises them
+  // frame list A's replica took (atomic min over the few workgroups that take one; k_detect
+  // / k_chunk_prep's workgroup 0 initialises it), [kTlHead + i] the end of k_demod's wave i
+  // (a plain store per wave, 0 for a wave that took no frame: no contended atomics in the
+  // timed launch); the host reduces them when it collects the stage times
   unsigned long long *tl;
 };
 
@@ -155,6 +158,8 @@ struct Knobs {
   bool no_replay = false;   // AMOD_NO_REPLAY: listed frames demodulate in the replica too
   bool exact_serial = false;// AMOD_EXACT_SERIAL: list A after k_demod on the launch stream
   int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
+  int aux_priority = 1;     // AMOD_AUX_PRIORITY: the second stream at the device's highest (1) or
+                            // default (0) priority (experiments)
   // streaming receiver (stream.cpp)
   int stream_minseg = 0;    // AMOD_STREAM_MINSEG
   bool stream_diag = false; // AMOD_STREAM_DIAG
@@ -487,7 +492,7 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
 // a profiled decode's timeline slot (DevWork::tl), set by the first launch of the decode
 __device__ inline void tl_init(const DevWork &w) {
   if (w.tl && blockIdx.x == 0 && threadIdx.x == 0) {
-    w.tl[0] = ~0ull; w.tl[1] = 0ull; w.tl[2] = ~0ull; w.tl[3] = 0ull;
+    w.tl[0] = ~0ull; w.tl[1] = 0ull; w.tl[2] = 0ull; w.tl[3] = 0ull;
   }
 }
 

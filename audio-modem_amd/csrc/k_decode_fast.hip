@@ -1517,7 +1517,10 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   int nblk = (int)gridDim.x;
   if (w.yield_blocks > 0 && w.yield_blocks < nblk && __builtin_amdgcn_readfirstlane(*w.yield_count) > 0)
     nblk = w.yield_blocks;
-  if ((int)blockIdx.x >= nblk) return; // (before any frame: the grid's frames are strided over nblk)
+  if ((int)blockIdx.x >= nblk) { // (before any frame: the grid's frames are strided over nblk)
+    if (w.tl && lane == 0) w.tl[kTlHead + (int)blockIdx.x * NWAVE + wave] = 0ull;
+    return;
+  }
   const int wstride = nblk * NWAVE;
   auto next_frame = [&](int k, FrameS &F) -> int {
     FRESH_ARGS;
@@ -1971,10 +1974,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // the sample registers are refilled with the next job as soon as the FFT input is formed
   FrameS fa, fb;
   int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
-  if (ka >= nfr) return;
+  if (ka >= nfr) {
+    if (w.tl && lane == 0) w.tl[kTlHead + (int)blockIdx.x * NWAVE + wave] = 0ull;
+    return;
+  }
   const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
-  if (w.tl && lane == 0) atomicMin(w.tl + 2, (unsigned long long)wall_clock64());
   f2v r[8];
   loads(fa, ja, r);
   for (;;) {
@@ -1985,7 +1990,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     fa = fb; ka = kb; ja = jb;
   }
   if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
-  if (w.tl && lane == 0) atomicMax(w.tl + 1, (unsigned long long)wall_clock64());
+  if (w.tl && lane == 0) w.tl[kTlHead + (int)blockIdx.x * NWAVE + wave] = (unsigned long long)wall_clock64();
 }
 template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;

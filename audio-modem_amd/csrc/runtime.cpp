@@ -233,7 +233,7 @@ std::vector<int32_t> cfg_key(const amod_cfg &c) {
 
 } // namespace
 
-constexpr int kTlSlots = 256;    // profiled decodes whose timeline marks are kept between harvests
+constexpr int kTlSlots = 64;     // profiled decodes whose timeline marks are kept between harvests
 constexpr int kMaxChunks = 16;   // frame chunks of one decode (two-stream overlap)
 constexpr int kOverlapChunks = 1; // default chunk count (measured: overlap slows both launches)
 
@@ -285,11 +285,12 @@ struct amod_ctx {
   // the end of the second stream's chain (list A's exact kernel + replay k_demod), after
   // the launch stream has joined it, after list B's exact kernel
   std::vector<std::array<hipEvent_t, 6>> ev_used, ev_free;
-  // the device timeline marks of profiled decodes (amod_aux_overlap): kTlSlots slots of 4,
-  // one per decode in ring order; tl_of[i] is ev_used[i]'s slot
+  // the device timeline marks of profiled decodes (amod_aux_overlap): kTlSlots slots of
+  // tl_words each (amod::kTlHead + one per k_demod wave), one per decode in ring order;
+  // tl_of[i] is ev_used[i]'s (slot, k_demod waves)
   DevBuf tl;
-  int64_t tl_next = 0;
-  std::vector<int64_t> tl_of;
+  int64_t tl_next = 0, tl_words = 0;
+  std::vector<std::pair<int64_t, int64_t>> tl_of;
   int64_t ov_listed = 0, ov_beside = 0;
   double ov_lead_us = 0.0;
   amod::Knobs knobs; // read once at amod_open
@@ -313,6 +314,7 @@ void read_knobs(amod::Knobs &k) {
   k.no_replay = getenv("AMOD_NO_REPLAY") != nullptr;
   k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
   if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
+  k.aux_priority = env_int("AMOD_AUX_PRIORITY", 1);
   k.stream_minseg = std::max(0, env_int("AMOD_STREAM_MINSEG", 0));
   k.stream_diag = getenv("AMOD_STREAM_DIAG") != nullptr;
   k.no_gap_scan = getenv("AMOD_NO_GAP_SCAN") != nullptr;
@@ -637,11 +639,16 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // this decode's timeline slot (profiling; one-chunk decodes with a k_demod launch): set by
   // k_detect, list A's replica and the main k_demod launch only
   unsigned long long *tl = nullptr;
-  int64_t tl_slot = -1;
+  int64_t tl_slot = -1, tl_waves = 0;
   if (ctx->profiling && demod && !debug && nchunk == 1 && !ctx->knobs.exact_serial) {
-    HIP_TRY(ctx->tl.ensure(sizeof(unsigned long long) * 4 * kTlSlots));
+    tl_waves = 4 * (int64_t)demod_blocks(nframes); // k_demod: 4 waves per workgroup
+    if (amod::kTlHead + tl_waves > ctx->tl_words) { // a new layout: the marks kept so far are void
+      ctx->tl_words = amod::kTlHead + std::max<int64_t>(tl_waves, 4 * 4 * (int64_t)std::max(1, ctx->cu_count));
+      HIP_TRY(ctx->tl.ensure(sizeof(unsigned long long) * (size_t)(ctx->tl_words * kTlSlots)));
+      for (auto &e : ctx->tl_of) e.first = -1;
+    }
     tl_slot = ctx->tl_next++ % kTlSlots;
-    tl = (unsigned long long *)ctx->tl.p + 4 * tl_slot;
+    tl = (unsigned long long *)ctx->tl.p + ctx->tl_words * tl_slot;
   }
   w.tl = tl;
   amod::DevWork wb = w; // every field as w, list B
@@ -738,7 +745,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   HIP_TRY(mark(5));
   if (ctx->profiling) {
     ctx->ev_used.push_back(ev);
-    ctx->tl_of.push_back(tl_slot);
+    ctx->tl_of.emplace_back(tl_slot, tl_waves);
   }
   return AMOD_SUCCESS;
 }
@@ -890,7 +897,8 @@ int amod_open(int device, amod_ctx **out) {
   int prio_least = 0, prio_greatest = 0;
   bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
             hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
-            hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+            hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
+                                        ctx->knobs.aux_priority ? prio_greatest : prio_least) == hipSuccess;
   for (auto &e : ctx->chunk_ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     amod_close(ctx);
@@ -1099,13 +1107,16 @@ int amod_kernel_stages(amod_ctx *ctx, double *ms, int32_t nslots, int64_t *n) {
   std::vector<unsigned long long> tlh;
   if (ctx->tl.p && !ctx->ev_used.empty()) {
     HIP_TRY(hipEventSynchronize(ctx->ev_used.back()[5]));
-    tlh.resize(4 * (size_t)kTlSlots);
+    tlh.resize((size_t)(ctx->tl_words * kTlSlots));
     HIP_TRY(hipMemcpy(tlh.data(), ctx->tl.p, sizeof(unsigned long long) * tlh.size(), hipMemcpyDeviceToHost));
     const size_t n = ctx->tl_of.size(), from = n > (size_t)kTlSlots ? n - kTlSlots : 0;
     for (size_t i = from; i < n; ++i) {
-      const int64_t sl = ctx->tl_of[i];
+      const int64_t sl = ctx->tl_of[i].first, nw = ctx->tl_of[i].second;
       if (sl < 0) continue;
-      const unsigned long long a_start = tlh[4 * sl], d_end = tlh[4 * sl + 1];
+      const unsigned long long *m = tlh.data() + ctx->tl_words * sl;
+      const unsigned long long a_start = m[0];
+      unsigned long long d_end = 0;
+      for (int64_t q = 0; q < nw; ++q) d_end = std::max(d_end, m[amod::kTlHead + q]);
       if (a_start == ~0ull || d_end == 0) continue; // list A took no frame / no k_demod wave ran
       ctx->ov_listed += 1;
       const double lead = ((double)(long long)(d_end - a_start)) / 100.0; // 100 MHz real-time clock
