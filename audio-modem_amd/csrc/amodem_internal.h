@@ -28,7 +28,9 @@ constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
 constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
 constexpr int kCrcMats = 512;
-constexpr int kTlHead = 4;     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+constexpr int kTlHead = 4;
+constexpr int kFbSet = 32;     // a decode's counter set: [0] list A, [1] list B, [2] replay list,
+constexpr int kFbDone = 3;     //   [3] list B's finished workgroups; lists follow at 64     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
 
 // Device-resident tables, built once per configuration by the runtime.
 struct DevTables {
@@ -133,9 +135,9 @@ struct DevWork {
   // exact kernel's waves (0: the whole grid)
   const int32_t *yield_count;
   int32_t yield_blocks;
-  // exact kernel, list B (the step's last launch): workgroup 0 zeroes fb_reset[0..31], the
-  // counter set the previous decode used (decodes alternate between two sets of 32), so
-  // the next decode needs no memset dispatch (null: no reset)
+  // exact kernel, list B (the step's last launch): its last workgroup to finish zeroes
+  // fb_reset[0 .. kFbSet), the decode's own counter set (kFbDone counts the finished
+  // workgroups), so neither the next decode nor a graph replay needs a memset (null: none)
   int32_t *fb_reset;
   // profiled decodes only (amod_aux_overlap): device real-time marks, [0] the first listed
   // frame list A's replica took (atomic min over the few workgroups that take one; k_detect

@@ -250,13 +250,12 @@ struct amod_ctx {
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
   int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0;
-  // fb[0..63] holds two counter sets of 32; a decode uses set fb_parity and its list-B
-  // launch zeroes the other (fb_reset). fb_zeroed: both sets are zero when this decode's
+  // fb[0 .. kFbSet) is the decode's counter set (lists from fb + 64); the decode's list-B
+  // launch zeroes it when it finishes (fb_reset). fb_zeroed: the set is zero when this decode's
   // launches run; a reallocation or an aborted launch sequence clears it (memset)
   bool fb_zeroed = false;
-  int fb_parity = 0;
-  bool fb_captured = false; // a decode was captured into a hipGraph: its replays memset and
-                            // dirty the counters unseen by the host, so every decode memsets
+  bool fb_captured = false; // a decode was captured into a hipGraph: a buffer that grows is
+                            // kept (not freed) until amod_close, for the graph's replays
   void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
   void (*ext_free[4])(void *) = {nullptr, nullptr, nullptr, nullptr};
   int64_t soft_stride = 0;
@@ -564,7 +563,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.samples = samples; w.off = offsets; w.len = lengths; w.nframes = nframes;
   w.res = results; w.payload = payload; w.stride = payload_stride; w.dbg = debug;
   int32_t *const fb_base = (int32_t *)ctx->fb.p;
-  int32_t *fb = fb_base + 32 * ctx->fb_parity; // this decode's counter set; lists from fb_base + 64
+  int32_t *fb = fb_base; // this decode's counter set; lists from fb_base + 64
   // exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod;
   // list C (fb[2]): frames whose detection the exact kernel replayed, for k_demod
   w.fb_count = fb; w.fb_list = fb_base + 64; w.fb_flags = fb_base + 64 + nframes;
@@ -604,7 +603,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(s, &cap));
   if (cap != hipStreamCaptureStatusNone) ctx->fb_captured = true;
-  if (!ctx->fb_zeroed || ctx->fb_captured) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // both counter sets
+  if (!ctx->fb_zeroed) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // after a reallocation or an aborted decode
   ctx->fb_zeroed = false; // until this decode's list-B launch is enqueued with its reset
   std::array<hipEvent_t, 6> ev{};
   if (ctx->profiling) {
@@ -738,10 +737,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(4));
-  wb.fb_reset = ctx->fb_captured ? nullptr : fb_base + 32 * (1 - ctx->fb_parity); // zeroed for the next decode
+  wb.fb_reset = fb; // zeroed by list B's last workgroup, for the next decode (or replay)
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
-  ctx->fb_zeroed = xslots > 0 && !ctx->fb_captured;
-  if (!ctx->fb_captured) ctx->fb_parity ^= 1;
+  ctx->fb_zeroed = xslots > 0;
   HIP_TRY(mark(5));
   if (ctx->profiling) {
     ctx->ev_used.push_back(ev);

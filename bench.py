@@ -772,7 +772,7 @@ def graph_leg(env: Env, wl: Workload, steps: int):
     amodem.h) and replayed `steps` times on the launch stream: the step time without the
     per-launch host work (the dependent kernels' GPU-side gaps remain). After the timed
     replays one replay's records are checked like the eager steps'. Runs last on the
-    workload: a captured context memsets its exact-list counters on every decode."""
+    workload (the capture stream is the graph's own)."""
     torch = env.torch
     try:
         g = torch.cuda.CUDAGraph()

@@ -1,8 +1,8 @@
 """amod_decode_device captured into a hipGraph (include/amodem.h: amod_reserve, then
 capture) and replayed: every replay, and an eager decode after the replays, returns the
 eager decode's records and payload. Frames are listed for the exact kernel (wide guard
-bands), so the exact-list counters — zeroed by a memset inside a captured decode, by
-the previous decode's list-B launch otherwise — are exercised across replays."""
+bands), so the exact-list counters — zeroed at the end of every decode, replayed or
+eager, by its own list-B launch's last workgroup — are exercised across replays."""
 
 import numpy as np
 import pytest

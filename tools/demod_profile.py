@@ -21,14 +21,12 @@ def main():
     conf = sys.argv[1] if len(sys.argv) > 1 else "c2"
     frames = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     env = bench.Env()
+    os.environ["AMOD_STAMPS"] = "1"  # (read when the workload's context opens)
     wl = bench.Workload(env, conf, frames, snr=10.0)
-    for _ in range(20):
-        wl.step()
-    os.environ["AMOD_STAMPS"] = "1"
-    for _ in range(3):
+    del os.environ["AMOD_STAMPS"]
+    for _ in range(23):
         wl.step()
     wl.dm.synchronize()
-    del os.environ["AMOD_STAMPS"]
     st = np.zeros(wl.F * 32, dtype=np.uint64)
     n = env.lib.amod_debug_stamps(wl.dm.ctx, st.ctypes.data, st.size)
     st = st[:n].reshape(-1, 32).astype(np.int64)
