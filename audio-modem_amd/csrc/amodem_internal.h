@@ -29,8 +29,7 @@ constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
 constexpr int kCrcMats = 512;
 constexpr int kTlHead = 4;
-constexpr int kFbSet = 32;     // a decode's counter set: [0] list A, [1] list B, [2] replay list,
-constexpr int kFbDone = 3;     //   [3] list B's finished workgroups; lists follow at 64     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
 
 // Device-resident tables, built once per configuration by the runtime.
 struct DevTables {
@@ -135,10 +134,13 @@ struct DevWork {
   // exact kernel's waves (0: the whole grid)
   const int32_t *yield_count;
   int32_t yield_blocks;
-  // exact kernel, list B (the step's last launch): its last workgroup to finish zeroes
-  // fb_reset[0 .. kFbSet), the decode's own counter set (kFbDone counts the finished
-  // workgroups), so neither the next decode nor a graph replay needs a memset (null: none)
+  // The decode's counters are zeroed by its own launches, so neither the next decode nor
+  // a graph replay needs a memset: list B's exact launch (the last) zeroes *fb_reset,
+  // list A's count, and k_detect / k_chunk_prep (the first) zero fb_zero[0 .. 1], the
+  // counts of list B and of the replay list, which only later launches append to
+  // (null: not this launch)
   int32_t *fb_reset;
+  int32_t *fb_zero;
   // profiled decodes only (amod_aux_overlap): device real-time marks, [0] the first listed
   // frame list A's replica took (atomic min over the few workgroups that take one; k_detect
   // / k_chunk_prep's workgroup 0 initialises it), [kTlHead + i] the end of k_demod's wave i
@@ -491,8 +493,10 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
   }
 }
 
-// a profiled decode's timeline slot (DevWork::tl), set by the first launch of the decode
+// the first launch of a decode: the counters later launches append to (DevWork::fb_zero),
+// and a profiled decode's timeline slot (DevWork::tl)
 __device__ inline void tl_init(const DevWork &w) {
+  if (w.fb_zero && blockIdx.x == 0 && threadIdx.x == 0) { w.fb_zero[0] = 0; w.fb_zero[1] = 0; }
   if (w.tl && blockIdx.x == 0 && threadIdx.x == 0) {
     w.tl[0] = ~0ull; w.tl[1] = 0ull; w.tl[2] = 0ull; w.tl[3] = 0ull;
   }

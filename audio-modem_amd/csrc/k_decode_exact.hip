@@ -193,6 +193,9 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
   // throughput-bound k_demod: their waves issue first on a shared SIMD
   __builtin_amdgcn_s_setprio(3);
   const int count = *w.fb_count;
+  // list B (the decode's last launch) zeroes list A's count for the next decode (or graph
+  // replay): every launch that appends to or reads it ran before this one
+  if (w.fb_reset && blockIdx.x == 0 && tid == 0) *w.fb_reset = 0;
   const int SYM = cfg.sym, CP = cfg.cp;
   for (int item = blockIdx.x; item < count; item += gridDim.x) {
     const int f = w.fb_list[item];
@@ -835,18 +838,6 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     }
     finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr, nv >> 3);
     __syncthreads();
-  }
-  // list B, the decode's last launch: its last workgroup zeroes the decode's counter set
-  // (every launch that reads or appends to a count ran before it, in stream order, and each
-  // workgroup of this one read its count before it arrives here), so the next decode, or
-  // the next replay of a captured one, starts from zero with no memset
-  if (w.fb_reset) {
-    __syncthreads();
-    if (tid == 0) {
-      __threadfence();
-      if (atomicAdd(w.fb_reset + kFbDone, 1) == (int)gridDim.x - 1)
-        for (int i = 0; i < kFbSet; ++i) __hip_atomic_store(w.fb_reset + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 

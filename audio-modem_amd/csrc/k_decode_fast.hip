@@ -1241,14 +1241,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) 
 }
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_WPE))) void k_detect_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
-  (void)w_arg;
+  tl_init(w_arg);
   detect<false, true>();
 }
 // stream pass + Schmidl-Cox only (diagnostics: AMOD_STOP_AFTER=1); launched with the same
 // dynamic LDS as k_detect, so the same number of workgroups share a CU
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_SCAN_WPE))) void k_corr_scan(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
-  (void)w_arg;
+  tl_init(w_arg);
   detect<true, false>();
 }
 

@@ -250,8 +250,8 @@ struct amod_ctx {
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
   int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0;
-  // fb[0 .. kFbSet) is the decode's counter set (lists from fb + 64); the decode's list-B
-  // launch zeroes it when it finishes (fb_reset). fb_zeroed: the set is zero when this decode's
+  // fb[0 .. 2] are the decode's counts (lists from fb + 64), zeroed by the decode's own first
+  // and last launches (DevWork::fb_zero, fb_reset). fb_zeroed: they are zero when this decode's
   // launches run; a reallocation or an aborted launch sequence clears it (memset)
   bool fb_zeroed = false;
   bool fb_captured = false; // a decode was captured into a hipGraph: a buffer that grows is
@@ -567,6 +567,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod;
   // list C (fb[2]): frames whose detection the exact kernel replayed, for k_demod
   w.fb_count = fb; w.fb_list = fb_base + 64; w.fb_flags = fb_base + 64 + nframes;
+  w.fb_zero = fb + 1; // (k_detect / k_chunk_prep: the counts of list B and the replay list)
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
@@ -652,6 +653,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   w.tl = tl;
   amod::DevWork wb = w; // every field as w, list B
   wb.tl = nullptr;
+  wb.fb_zero = nullptr;
   wb.fb_count = fb + 1; wb.fb_list = fb_base + 64 + 2 * nframes; wb.fb_flags = fb_base + 64 + 3 * nframes;
   // exact-kernel grid: persistent workgroups over the listed frames (usually none: the
   // launch then costs its dispatch, so two per CU, not one per slot)
@@ -721,6 +723,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   } else {
     for (int c = 0; c < nchunk; ++c) {
       w.f0 = wb.f0 = (int)((int64_t)nframes * c / nchunk);
+      w.fb_zero = c == 0 ? fb + 1 : nullptr; // (the first chunk only: k_demod of chunk c - 1 appends)
       w.f1 = wb.f1 = (int)((int64_t)nframes * (c + 1) / nchunk);
       HIP_TRY(amod_launch_detect(d, w, s));
       HIP_TRY(hipEventRecord(ctx->chunk_ev[c], s));
@@ -737,7 +740,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   }
   w.f0 = wb.f0 = 0; w.f1 = wb.f1 = nframes;
   HIP_TRY(mark(4));
-  wb.fb_reset = fb; // zeroed by list B's last workgroup, for the next decode (or replay)
+  wb.fb_reset = fb; // list A's count, zeroed for the next decode (or replay)
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
   ctx->fb_zeroed = xslots > 0;
   HIP_TRY(mark(5));

@@ -771,8 +771,8 @@ def graph_leg(env: Env, wl: Workload, steps: int):
     """The same decode captured once into a hipGraph (amod_reserve was called; include/
     amodem.h) and replayed `steps` times on the launch stream: the step time without the
     per-launch host work (the dependent kernels' GPU-side gaps remain). After the timed
-    replays one replay's records are checked like the eager steps'. Runs last on the
-    workload (the capture stream is the graph's own)."""
+    replays one replay's records are checked like the eager steps'. Runs right after the
+    eager steps, warmed up the same way (the capture stream is the graph's own)."""
     torch = env.torch
     try:
         g = torch.cuda.CUDAGraph()
@@ -789,8 +789,7 @@ def graph_leg(env: Env, wl: Workload, steps: int):
             finally:
                 wl.stream = stream0
         torch.cuda.synchronize(env.dev)
-        for _ in range(5):
-            g.replay()
+        warm_up(g.replay, lambda: torch.cuda.synchronize(env.dev), 5)  # (clocks, as for the eager steps)
         torch.cuda.synchronize(env.dev)
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -817,6 +816,8 @@ def run_leg(env: Env, conf: str, args, frames=0, snr=20.0, primary=False):
     if primary and conf != "c4":
         extra["scan_roofline"] = scan_phase(env, wl)
     out, rec = measure(env, wl, args.steps, args.warmup)
+    if primary and env.world == 1:  # right after the eager steps, while the clocks are up
+        out["graph"] = graph_leg(env, wl, args.steps)
     out["tx"] = tx_obj(wl)
     if conf == "c5" and args.soft and primary:
         out["soft_combine"] = soft_leg(env, wl, rec)
@@ -833,8 +834,6 @@ def run_leg(env: Env, conf: str, args, frames=0, snr=20.0, primary=False):
         progress(f"{conf}: CPU legs (C oracle over the whole batch, JS baseline on worker_threads)")
         js_frames = args.cpu_frames or (640 if conf != "c5" else 192)
         out["cpu_baseline"] = cpu_legs(wl, rec, js_frames, js_seconds=1.5 if primary else 1.0)
-    if primary and env.world == 1:
-        out["graph"] = graph_leg(env, wl, args.steps)
     out.update(extra)
     wl.close()
     return out
