@@ -162,6 +162,8 @@ struct Knobs {
   bool no_replay = false;   // AMOD_NO_REPLAY: listed frames demodulate in the replica too
   bool exact_serial = false;// AMOD_EXACT_SERIAL: list A after k_demod on the launch stream
   int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
+  int64_t mall_flush_mb = 0; // AMOD_MALL_FLUSH_MB: stream this many MB of a scratch buffer
+                            // between k_detect and k_demod (experiments: Infinity Cache probe)
   int aux_priority = 1;     // AMOD_AUX_PRIORITY: the second stream at the device's highest (1) or
                             // default (0) priority (experiments)
   // streaming receiver (stream.cpp)
@@ -521,6 +523,7 @@ void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_word
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s,
                              bool beside_demod = false); // list A runs beside k_demod
 hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hipStream_t s);
+hipError_t amod_launch_flush(const void *buf, size_t bytes, float *sink, hipStream_t s); // experiments
 int amod_fast_lds_bytes(int nb_cap, int fine_cap, int sym); // dynamic LDS of one k_detect workgroup
 // streaming receiver pieces (k_stream.hip)
 int64_t amod_ema_chunk();

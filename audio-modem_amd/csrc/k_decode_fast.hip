@@ -2022,6 +2022,24 @@ __host__ demod_fn demod_kernel(const DevCfg &cfg, bool dbg) {
 } // namespace
 } // namespace amod
 
+// experiments (AMOD_MALL_FLUSH_MB): stream a scratch buffer through L2 / the Infinity
+// Cache, so the next launch finds none of the previous launches' lines there
+namespace amod {
+__global__ __launch_bounds__(256) void k_flush(const float *__restrict__ p, size_t n, float *sink) {
+  float acc = 0.f;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n / 4; i += (size_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4 *>(p)[i];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 1.2345e-30f) *sink = acc; // (keeps the loads)
+}
+} // namespace amod
+
+extern "C" hipError_t amod_launch_flush(const void *buf, size_t bytes, float *sink, hipStream_t s) {
+  hipLaunchKernelGGL(amod::k_flush, dim3(4096), dim3(256), 0, s, (const float *)buf, bytes / 4, sink);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ launchers
 // dynamic LDS bytes of a k_detect workgroup with nb_cap moment blocks and fine_cap
 // fine-search positions

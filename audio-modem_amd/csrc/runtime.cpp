@@ -276,6 +276,7 @@ struct amod_ctx {
   std::vector<hipEvent_t> up_ev;
   std::mutex mu;
   DevBuf stamps;
+  DevBuf flush; // AMOD_MALL_FLUSH_MB scratch (experiments)
   DevBuf tx_pkt, tx_meta, tx_out; // amod_tx_host staging
   int64_t nstamps = 0;
   // kernel timing (amod_set_profiling)
@@ -314,6 +315,7 @@ void read_knobs(amod::Knobs &k) {
   k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
   if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
   k.aux_priority = env_int("AMOD_AUX_PRIORITY", 1);
+  k.mall_flush_mb = std::max(0, env_int("AMOD_MALL_FLUSH_MB", 0));
   k.stream_minseg = std::max(0, env_int("AMOD_STREAM_MINSEG", 0));
   k.stream_diag = getenv("AMOD_STREAM_DIAG") != nullptr;
   k.no_gap_scan = getenv("AMOD_NO_GAP_SCAN") != nullptr;
@@ -680,6 +682,11 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (nchunk == 1) {
     w.f0 = 0; w.f1 = nframes;
     HIP_TRY(amod_launch_detect(d, w, s));
+    if (ctx->knobs.mall_flush_mb > 0) { // (experiments: k_demod's window reads from a cold Infinity Cache)
+      const size_t fb_bytes = (size_t)ctx->knobs.mall_flush_mb << 20;
+      HIP_TRY(ctx->flush.ensure(fb_bytes + 256));
+      HIP_TRY(amod_launch_flush(ctx->flush.p, fb_bytes, (float *)((char *)ctx->flush.p + fb_bytes), s));
+    }
     HIP_TRY(mark(1));
     if (demod) {
       // list A is complete: the exact replica of the frames detection listed (long
