@@ -529,6 +529,11 @@ int amod_fast_lds_bytes(int nb_cap, int fine_cap, int sym); // dynamic LDS of on
 int64_t amod_ema_chunk();
 hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
                            int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s);
+int64_t amod_ema_wave_samples(); // the stream piece granule of amod_launch_ema_part
+hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
+                                const double *apow, int64_t s0, int64_t s1, hipStream_t s);
+hipError_t amod_launch_ema_fix(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end,
+                               int64_t *list, unsigned long long *fixed, hipStream_t s);
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
 hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,

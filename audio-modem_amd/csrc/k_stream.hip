@@ -55,9 +55,10 @@ __device__ __forceinline__ double ema_step(double m, float x) { return kAlpha * 
 // from a zero start (fp64, approximate: it only seeds the warm-up). One workgroup per
 // chunk, coalesced. apow[j] = a^j.
 __global__ __launch_bounds__(256) void k_ema_contrib(const float *__restrict__ x, int64_t nx,
-                                                     const double *__restrict__ apow, double *__restrict__ c) {
+                                                     const double *__restrict__ apow, double *__restrict__ c,
+                                                     int64_t kbase) {
   __shared__ double red[4];
-  const int64_t k = blockIdx.x;
+  const int64_t k = kbase + blockIdx.x;
   const int tid = threadIdx.x;
   double acc = 0.0;
 #pragma unroll
@@ -85,11 +86,13 @@ constexpr int kRow = kTile + 4; // row stride (floats): 16-byte rows for ds_read
 __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, int64_t nx, int64_t n,
                                                  const double *__restrict__ c,
                                                  double A, float *__restrict__ y, double *__restrict__ warm,
-                                                 double *__restrict__ end, int64_t nch, int kWarm, int per) {
+                                                 double *__restrict__ end, int64_t nch, int kWarm, int per,
+                                                 int64_t wave0, int64_t wave1) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kRow];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t k0 = ((int64_t)blockIdx.x * 4 + wv) * 64 * per; // the wave's first chunk
-  if (k0 >= nch) return;
+  const int64_t gw = wave0 + (int64_t)blockIdx.x * 4 + wv; // waves [wave0, wave1) of this launch
+  const int64_t k0 = gw * 64 * per; // the wave's first chunk
+  if (gw >= wave1 || k0 >= nch) return;
   const int64_t k = k0 + (int64_t)per * lane;                    // the lane's first output chunk
   const int64_t kw = k - kWarm > 0 ? k - kWarm : 0;           // first warm-up chunk
   double m = 0.0;                                             // zero start: the true one
@@ -754,28 +757,50 @@ extern "C" {
 int64_t amod_ema_chunk() { return amod::kL; }
 // DC removal of x[0, n) from a zero EMA state into y (x read for [0, nx), zero past it); warm / end / scr: nch = ceil(n / L)
 // doubles each; list: nch int64; apow: L doubles (a^j); fixed: 2 counters
-hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
-                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s) {
-  const int64_t nch = (n + amod::kL - 1) / amod::kL;
-  if (nch <= 0) return hipSuccess;
-  double A = 1.0;
-  for (int i = 0; i < amod::kL; ++i) A *= amod::kAlpha;
-  hipError_t e = hipMemsetAsync(fixed, 0, 2 * sizeof(unsigned long long), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)nch), dim3(256), 0, s, x, nx, apow, scr);
-  static const int warm_chunks = [] {
-    const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
-    return e ? std::max(0, atoi(e)) : amod::kWarmDefault;
-  }();
+namespace {
+int ema_per() {
   static const int per = [] {
     const char *e = getenv("AMOD_EMA_PER"); // experiments: output chunks per lane
     return e ? std::max(1, atoi(e)) : amod::kPerDefault;
   }();
-  hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((nch + 256 * per - 1) / (256 * per))), dim3(256), 0, s, x, nx, n,
-                     scr, A, y, warm, end, nch, warm_chunks, per);
-  // parallel fix rounds: each round checks every chunk's start state against its
-  // predecessor's end and recomputes the listed runs in parallel; after kEmaRounds rounds
-  // the serial fix settles anything left (normally nothing: runs are a chunk or two long)
+  return per;
+}
+} // namespace
+
+// samples per k_ema_out wave (64 lanes x per chunks): a piece of the stream that is a
+// multiple of this can be cleaned as soon as it and the samples before it have landed
+int64_t amod_ema_wave_samples() { return (int64_t)64 * ema_per() * amod::kL; }
+
+// stages (1) + (2) for the waves of samples [s0, s1) (s0 a multiple of
+// amod_ema_wave_samples(); s1 too, or the end n): their chunk contributions, then their
+// outputs; every sample before s1 must have landed (warm-up reads the chunks before s0)
+hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
+                                const double *apow, int64_t s0, int64_t s1, hipStream_t s) {
+  const int64_t nch = (n + amod::kL - 1) / amod::kL;
+  const int64_t c0 = s0 / amod::kL, c1 = std::min(nch, (s1 + amod::kL - 1) / amod::kL);
+  if (c1 <= c0) return hipSuccess;
+  double A = 1.0;
+  for (int i = 0; i < amod::kL; ++i) A *= amod::kAlpha;
+  hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)(c1 - c0)), dim3(256), 0, s, x, nx, apow, scr, c0);
+  static const int warm_chunks = [] {
+    const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
+    return e ? std::max(0, atoi(e)) : amod::kWarmDefault;
+  }();
+  const int per = ema_per();
+  const int64_t span = (int64_t)64 * per; // chunks per wave
+  const int64_t w0 = c0 / span, w1 = (c1 + span - 1) / span;
+  hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((w1 - w0 + 3) / 4)), dim3(256), 0, s, x, nx, n, scr, A, y, warm,
+                     end, nch, warm_chunks, per, w0, w1);
+  return hipGetLastError();
+}
+
+// (3) + (4) once every part is enqueued: the check rounds and the fixes
+hipError_t amod_launch_ema_fix(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end,
+                               int64_t *list, unsigned long long *fixed, hipStream_t s) {
+  const int64_t nch = (n + amod::kL - 1) / amod::kL;
+  if (nch <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(fixed, 0, 2 * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
   uint8_t *const lflag = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(list + nch) + 15) & ~uintptr_t(15));
   static const int rounds = [] {
     const char *e = getenv("AMOD_EMA_ROUNDS"); // experiments
@@ -796,6 +821,16 @@ hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, doub
   hipLaunchKernelGGL(amod::k_ema_fix, dim3(1), dim3(64), 0, s, x, nx, n, y, warm, end, nch, fixed + 1, lflag, fixed);
   return hipGetLastError();
 }
+
+hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
+                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s) {
+  const int64_t nch = (n + amod::kL - 1) / amod::kL;
+  if (nch <= 0) return hipSuccess;
+  hipError_t e = amod_launch_ema_part(x, nx, n, y, warm, end, scr, apow, 0, n, s);
+  if (e != hipSuccess) return e;
+  return amod_launch_ema_fix(x, nx, n, y, warm, end, list, fixed, s);
+}
+
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {
   const int64_t nblk = (n + 31) / 32;
   if (nblk <= 0) return hipSuccess;

@@ -23,6 +23,7 @@
 // Decisions are the reference's own arithmetic, so outcomes match it exactly; pinned
 // by tests/golden/stream.json (the reference receiver run on recipe streams).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -35,6 +36,7 @@
 #include <mutex>
 #include <condition_variable>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "amodem_internal.h"
@@ -116,6 +118,7 @@ struct CopyPool {
 constexpr int64_t kBlock = 4096;      // ScriptProcessor buffer (app.js:1103)
 const int64_t kEmaChunk = amod_ema_chunk(); // k_ema chunk (EMA end states are reported per chunk)
 constexpr int kBatch = 4096;          // frames decoded per GPU batch (after the metadata frame)
+constexpr int64_t kUpPieceSamples = int64_t(16) << 20; // host streams: samples per uploaded piece (64 MB)
 constexpr int kGranLog = 10, kGran = 1 << kGranLog; // sparse host copy granule (samples)
 constexpr int64_t kFirstPiece = int64_t(1) << 20;   // sparse mode: the first piece copied at once
 // blocks a GPU gap scan runs before it leaves the gap to the host (the kernel's time is its
@@ -159,9 +162,29 @@ struct RxState {
 struct FineTable {
   std::vector<int64_t> first, base, count;
   const double *metric = nullptr; // k_fine's metrics (pinned), NaN where the reference skips
+  // or, with the metrics kept on the device (k_gap_refine reads them there), the device
+  // array: a refinement the host runs itself (before the metadata frame, a stream without
+  // one, a window clamped to the ring) fetches its range's metrics once, on first use,
+  // instead of correlating every position on the host
+  const double *dmetric = nullptr;
+  mutable std::mutex fmu;
+  mutable std::unordered_map<size_t, std::vector<double>> fetched;
+  const double *range_metrics(size_t r) const {
+    if (metric) return metric + base[r];
+    if (!dmetric) return nullptr;
+    std::lock_guard<std::mutex> lk(fmu);
+    auto it = fetched.find(r);
+    if (it == fetched.end()) {
+      std::vector<double> v((size_t)count[r]);
+      if (hipMemcpy(v.data(), dmetric + base[r], sizeof(double) * v.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return nullptr;
+      it = fetched.emplace(r, std::move(v)).first;
+    }
+    return it->second.data();
+  }
   // refine walks consecutive positions: `last` (the caller's cursor) is tried first
   bool lookup(int64_t d, double &m, size_t &last) const {
-    if (!metric) return false; // (the metrics stayed on the device)
+    if (!metric && !dmetric) return false;
     size_t r = last;
     if (r >= first.size() || d < first[r] || d >= first[r] + count[r]) {
       auto it = std::upper_bound(first.begin(), first.end(), d);
@@ -170,14 +193,16 @@ struct FineTable {
       last = r;
     }
     if (d >= first[r] + count[r]) return false;
-    m = metric[base[r] + (d - first[r])];
+    const double *rm = range_metrics(r);
+    if (!rm) return false;
+    m = rm[d - first[r]];
     return true;
   }
   // the metrics of positions [d0, d1] when one range holds them all, else nullptr
   const double *span(int64_t d0, int64_t d1, size_t &last) const {
     double m;
     if (!lookup(d0, m, last) || d1 >= first[last] + count[last]) return nullptr;
-    return metric + base[last] + (d0 - first[last]);
+    return range_metrics(last) + (d0 - first[last]);
   }
 };
 
@@ -644,6 +669,27 @@ struct Pinned {
   template <typename T> T *as() const { return (T *)p; }
 };
 
+// Pageable host buffer (address space only until written: MAP_NORESERVE). The host copy of
+// the cleaned stream is touched sparsely (its first piece, the granules the state machine
+// reads); pinning all of it (hipHostMalloc of 3.6 GB for a 32k-chunk stream) cost ~150 ms
+// per first call of a size, more than the whole GPU prepass.
+struct PageBuf {
+  float *p = nullptr;
+  size_t cap = 0;
+  ~PageBuf() { if (p) munmap(p, cap); }
+  hipError_t alloc(size_t n) { // grow-only
+    n = std::max<size_t>(n, 16);
+    if (p && cap >= n) return hipSuccess;
+    if (p) { munmap(p, cap); p = nullptr; cap = 0; }
+    void *q = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (q == MAP_FAILED) return hipErrorOutOfMemory;
+    p = (float *)q;
+    cap = n;
+    return hipSuccess;
+  }
+  template <typename T> T *as() const { return (T *)p; }
+};
+
 // device and pinned buffers of the streaming receiver, kept per context (grow-only)
 struct StreamCache {
   DBuf d_x, d_y, d_warm, d_end, d_scr, d_list, d_apow, d_fixed, d_hot, d_ze;
@@ -657,7 +703,8 @@ struct StreamCache {
   DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
   DBuf d_barg, d_gaps;                      // k_fine's per-workgroup argmax, k_gap_scan's records
   Pinned gaps_h;
-  Pinned yh, yc, hot_h, metric_h;
+  PageBuf yh;
+  Pinned yc, hot_h, metric_h;
   Pinned w_res_h[kSets], w_pay_h[kSets];    // window decoder: results and payload rows (pinned D2H)
   // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
   std::vector<uint8_t> sp_need;
@@ -666,11 +713,15 @@ struct StreamCache {
   size_t sp_gcap = 0;
   bool apow_ready = false;
   hipStream_t s2 = nullptr;                 // the cleaned stream's device-to-host copy
+  hipStream_t s_up = nullptr;               // host samples: the upload, in pieces
+  std::vector<hipEvent_t> up_ev;            // one per uploaded piece (the EMA of a piece waits on it)
   static constexpr int kPieces = 16;
   hipEvent_t ema_done = nullptr, gathered = nullptr, piece[kPieces] = {}, cpiece[kPieces] = {};
   ~StreamCache() {
     if (s2) { (void)hipStreamSynchronize(s2); (void)hipStreamDestroy(s2); }
     if (s3) { (void)hipStreamSynchronize(s3); (void)hipStreamDestroy(s3); }
+    if (s_up) { (void)hipStreamSynchronize(s_up); (void)hipStreamDestroy(s_up); }
+    for (auto e : up_ev) (void)hipEventDestroy(e);
     for (auto e : w_kern)
       if (e) (void)hipEventDestroy(e);
     if (ema_done) (void)hipEventDestroy(ema_done);
@@ -972,18 +1023,42 @@ struct Prepass {
     }
     S_TRY(c->d_hot.alloc((size_t)(n / 32 + 1)));
     S_TRY(c->d_ze.alloc(sizeof(double2) * (size_t)(n / 32 + 1)));
-    if (device) {
-      x = samples;
-    } else {
-      x = c->d_x.as<float>();
-      if (nvalid) S_TRY(hipMemcpyAsync(c->d_x.p, samples, sizeof(float) * (size_t)nvalid, hipMemcpyHostToDevice, s));
-    }
     hipEvent_t ev[3];
     for (auto &e : ev) S_TRY(hipEventCreate(&e));
     S_TRY(hipEventRecord(ev[0], s));
-    S_TRY(amod_launch_ema(x, nvalid, n, c->d_y.as<float>(), c->d_warm.as<double>(), c->d_end.as<double>(),
-                          c->d_scr.as<double>(), c->d_list.as<int64_t>(), c->d_apow.as<double>(),
-                          c->d_fixed.as<unsigned long long>(), s));
+    float *const yd = c->d_y.as<float>();
+    double *const wd_ = c->d_warm.as<double>(), *const ed = c->d_end.as<double>(), *const sd = c->d_scr.as<double>();
+    if (device) {
+      x = samples;
+      S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), 0, n, s));
+    } else {
+      // the host samples go up in pieces on the upload stream (HIP's pageable copy runs at
+      // ~51 GB/s in 64 MB pieces, ~14 GB/s as one multi-GB copy), and each piece's EMA
+      // waves run on s as soon as it has landed (they read only it and the pieces before)
+      x = c->d_x.as<float>();
+      const int64_t wsz = amod_ema_wave_samples();
+      const int64_t P = std::max<int64_t>(1, kUpPieceSamples / wsz) * wsz;
+      const int64_t npc = (n + P - 1) / P;
+      if (!c->s_up) S_TRY(hipStreamCreateWithFlags(&c->s_up, hipStreamNonBlocking));
+      while ((int64_t)c->up_ev.size() < npc + 1) {
+        hipEvent_t e;
+        S_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->up_ev.push_back(e);
+      }
+      S_TRY(hipEventRecord(c->up_ev[npc], s)); // (the previous call's reads of d_x are done)
+      S_TRY(hipStreamWaitEvent(c->s_up, c->up_ev[npc], 0));
+      for (int64_t q = 0; q < npc; ++q) {
+        const int64_t a = q * P, b = std::min(n, a + P);
+        const int64_t va = std::min(a, nvalid), vb = std::min(b, nvalid);
+        if (vb > va)
+          S_TRY(hipMemcpyAsync(c->d_x.as<float>() + va, samples + va, sizeof(float) * (size_t)(vb - va),
+                               hipMemcpyHostToDevice, c->s_up));
+        S_TRY(hipEventRecord(c->up_ev[q], c->s_up));
+        S_TRY(hipStreamWaitEvent(s, c->up_ev[q], 0));
+        S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), a, b, s));
+      }
+    }
+    S_TRY(amod_launch_ema_fix(x, nvalid, n, yd, wd_, ed, c->d_list.as<int64_t>(), c->d_fixed.as<unsigned long long>(), s));
     S_TRY(hipEventRecord(ev[1], s));
     S_TRY(amod_launch_sc_screen(c->d_y.as<float>(), n, 0.25f, c->d_ze.as<double2>(), c->d_hot.as<uint8_t>(), s));
     // the fine ranges (every position within 448 samples of a hot block), built on the GPU
@@ -1039,6 +1114,8 @@ struct Prepass {
     // for the host's lookups (no copy queued behind the cleaned stream's transfer); with them
     // they stay on the device, and the few refinements left to the host correlate there
     ft.metric = nullptr;
+    ft.dmetric = nullptr;
+    ft.fetched.clear();
     if (!dev_metrics) {
       S_TRY(c->metric_h.alloc(sizeof(double) * (size_t)std::max<int64_t>(total, 1), true));
       ft.metric = c->metric_h.as<double>();
@@ -1049,7 +1126,10 @@ struct Prepass {
       double p1e = 0.0; // this.pre1Energy (app.js:744-745)
       for (float v : p1) p1e += (double)v * (double)v;
       nmetric = total;
-      if (dev_metrics) S_TRY(c->d_metric.alloc(sizeof(double) * (size_t)total));
+      if (dev_metrics) {
+        S_TRY(c->d_metric.alloc(sizeof(double) * (size_t)total));
+        ft.dmetric = c->d_metric.as<double>();
+      }
       std::vector<double> p1d(p1.begin(), p1.end()); // (exact: k_fine's fma operand)
       S_TRY(c->d_pre1.alloc(sizeof(double) * p1.size()));
       S_TRY(c->d_base.alloc(sizeof(int64_t) * nr));
@@ -1332,7 +1412,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   // decode frames[a, b) and dispatch them in order (_demodulateFrame, app.js:907-972);
   // `changed`: the first frame whose metadata result changed the window length of what
   // follows (its `after` updated), or -1
-  auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
+  auto dispatch_body = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
     changed = -1;
     // batch j + 1 decodes (buffer set (j + 1) % 3) while the host dispatches batch j and the
     // copy pool moves batch j - 1's chunks
@@ -1388,6 +1468,17 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     }
     copies.run();
     return AMOD_SUCCESS;
+  };
+  // every exit of a failed dispatch first lands the queued chunk copies (their bitmap bits
+  // are set) and drains the batches in flight (their D2H copies write the pinned rows the
+  // next call may reallocate)
+  auto decode_dispatch = [&](std::vector<FrameEv> &fr, size_t a, size_t b, int64_t &changed) -> int {
+    const int rc = dispatch_body(fr, a, b, changed);
+    if (rc != AMOD_SUCCESS) {
+      copies.run();
+      (void)wd.drain(ctx, pp);
+    }
+    return rc;
   };
 
   RxState st{};
