@@ -1058,6 +1058,20 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   }
   HIP_TRY(hipEventRecord(ctx->up_ev[0], s)); // the upload stream starts after the memset's stream order
   HIP_TRY(hipStreamWaitEvent(ctx->up, ctx->up_ev[0], 0));
+  // one workspace reservation and one fast-path capacity for the whole call (its longest
+  // frame): every piece's launch routes its frames as a one-piece call would, and no
+  // piece's reservation grows a buffer (hipFree would synchronise the upload pipeline)
+  int64_t call_max = 0;
+  for (int32_t i = 0; i < nframes; ++i) call_max = std::max<int64_t>(call_max, lengths[i]);
+  {
+    amod::DevCfg d;
+    int rc = get_tables(ctx, cfg, d);
+    if (rc == AMOD_SUCCESS) rc = reserve(ctx, cfg, nframes, call_max);
+    if (rc) {
+      (void)hipStreamSynchronize(ctx->up);
+      return rc;
+    }
+  }
   int32_t a = 0; // the first frame not yet enqueued
   for (int64_t p = 0; p <= npiece; ++p) {
     int64_t covered = nsamples;
@@ -1071,13 +1085,12 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
       if (!mono && p + 1 < npiece) continue;
     }
     int32_t b = a;
-    int64_t max_len = 0;
-    while (b < nframes && (p == npiece || offsets[b] + lengths[b] <= covered)) max_len = std::max<int64_t>(max_len, lengths[b++]);
+    while (b < nframes && (p == npiece || offsets[b] + lengths[b] <= covered)) ++b;
     if (b == a) continue;
     const int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p + a,
                                (const int32_t *)ctx->h_len.p + a, b - a, (amod_result *)ctx->h_res.p + a,
                                (uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride, payload_stride, options, s,
-                               nullptr, max_len);
+                               nullptr, call_max);
     if (rc) {
       (void)hipStreamSynchronize(ctx->up);
       return rc;

@@ -187,7 +187,9 @@ int amod_kernel_times(amod_ctx *ctx, double *fast_ms, int64_t *fast_launches, do
    accumulated over *n decodes; resets like amod_kernel_times */
 int amod_kernel_breakdown(amod_ctx *ctx, double *ms, int64_t *n);
 /* the stage slots of amod_kernel_stages (ms[AMOD_STAGE_*], milliseconds summed over *n
-   decodes; resets like amod_kernel_times) */
+   launch sequences; resets like amod_kernel_times). A device decode is one launch
+   sequence; amod_decode_host launches one per uploaded piece (64 MB) whose frames have
+   landed, so there *n counts pieces, not host calls. */
 enum {
   AMOD_STAGE_DETECT = 0,     /* k_detect / k_chunk_prep */
   AMOD_STAGE_DEMOD = 1,      /* k_demod alone (launch stream) */
