@@ -136,11 +136,16 @@ struct DevWork {
   int32_t yield_blocks;
   // The decode's counters are zeroed by its own launches, so neither the next decode nor
   // a graph replay needs a memset: list B's exact launch (the last) zeroes *fb_reset,
-  // list A's count, and k_detect / k_chunk_prep (the first) zero fb_zero[0 .. 1], the
-  // counts of list B and of the replay list, which only later launches append to
-  // (null: not this launch)
+  // list A's count, and k_detect / k_chunk_prep (the first) zero fb_zero[0 .. 2], the
+  // counts of list B and of the replay list and k_demod's claim counter, which only later
+  // launches use (null: not this launch)
   int32_t *fb_reset;
   int32_t *fb_zero;
+  // k_demod (main launch): with at least claim_min frames per wave, the frames past all but
+  // the last claim_rounds static rounds are claimed one at a time from this counter (null:
+  // every frame static)
+  int32_t *claim;
+  int32_t claim_rounds, claim_min;
   // profiled decodes only (amod_aux_overlap): device real-time marks, [0] the first listed
   // frame list A's replica took (atomic min over the few workgroups that take one; k_detect
   // / k_chunk_prep's workgroup 0 initialises it), [kTlHead + i] the end of k_demod's wave i
@@ -164,6 +169,9 @@ struct Knobs {
   int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
   int64_t mall_flush_mb = 0; // AMOD_MALL_FLUSH_MB: stream this many MB of a scratch buffer
                             // between k_detect and k_demod (experiments: Infinity Cache probe)
+  bool demod_static = false;// AMOD_DEMOD_STATIC: k_demod takes every frame by the static stride
+  int claim_rounds = 2;     // AMOD_CLAIM_ROUNDS: k_demod's claimed tail, in rounds of frames
+  int claim_min = 4;        // AMOD_CLAIM_MIN: frames per wave below which k_demod stays static
   int aux_priority = 1;     // AMOD_AUX_PRIORITY: the second stream at the device's highest (1) or
                             // default (0) priority (experiments)
   // streaming receiver (stream.cpp)
@@ -498,7 +506,7 @@ __device__ inline void finish_frame(const uint32_t *v, int nvoted, const DevCfg 
 // the first launch of a decode: the counters later launches append to (DevWork::fb_zero),
 // and a profiled decode's timeline slot (DevWork::tl)
 __device__ inline void tl_init(const DevWork &w) {
-  if (w.fb_zero && blockIdx.x == 0 && threadIdx.x == 0) { w.fb_zero[0] = 0; w.fb_zero[1] = 0; }
+  if (w.fb_zero && blockIdx.x == 0 && threadIdx.x == 0) { w.fb_zero[0] = 0; w.fb_zero[1] = 0; w.fb_zero[2] = 0; }
   if (w.tl && blockIdx.x == 0 && threadIdx.x == 0) {
     w.tl[0] = ~0ull; w.tl[1] = 0ull; w.tl[2] = 0ull; w.tl[3] = 0ull;
   }

@@ -1510,10 +1510,15 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(lane + 64 * rr < nband && cfg.t.known[lane + 64 * rr] < 0.f) << rr;
 
-  // next frame on the demodulation path at or after wave-iteration k (frames last-first).
-  // A static stride: the dispatcher places the grid's workgroups round-robin over the CUs,
-  // so every SIMD gets within one frame of the mean (a claim counter measured slower: its
-  // atomics' returns hold up the in-order vmcnt waits of the sample loads)
+  // Frames (last-first: frame f1 - 1 - k for the k-th) by a static stride for the first
+  // rounds, then one at a time from the claim counter (w.claim). Waves on one SIMD do not
+  // progress alike: VALU issue goes by priority, then age, so the youngest waves get the
+  // slots the older ones leave (MI355X_MICROARCH.md, issue arbitration) and under a purely
+  // static split they ran the kernel's tail alone (C4: the last-dispatched workgroups'
+  // waves lived 2.16 M cycles against 1.67 M for the rest). A wave claims the frame after
+  // its current one when it starts the current one, so the atomic's return is long back
+  // when it is read (a claim read at once holds up the in-order vmcnt waits of the sample
+  // loads: per-frame claims measured slower in round 2)
   int nblk = (int)gridDim.x;
   if (w.yield_blocks > 0 && w.yield_blocks < nblk && __builtin_amdgcn_readfirstlane(*w.yield_count) > 0)
     nblk = w.yield_blocks;
@@ -1522,16 +1527,31 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     return;
   }
   const int wstride = nblk * NWAVE;
+  // (at least claim_min frames per wave: a short batch's waves would all claim at once, and
+  // same-address device-scope atomics serialise at the memory side: C2, 2.44 frames per
+  // wave, lost 59 us that way)
+  const int rounds = nfr / wstride;
+  const bool dyn = w.claim != nullptr && !DBG && rounds >= w.claim_min;
+  const int kstat = dyn ? max(1, rounds - w.claim_rounds) * wstride : nfr; // k < kstat: static
+  auto claim = [&]() -> int { // lane 0: the next claimed k - kstat (not waited for here)
+    int v = 0;
+    if (lane == 0) v = atomicAdd(w.claim, 1);
+    return v;
+  };
+  int pend = 0; // (lane 0) the claim for the frame after the current one
+  // the first frame on the demodulation path from candidate k on
   auto next_frame = [&](int k, FrameS &F) -> int {
     FRESH_ARGS;
-    for (; k < nfr; k += wstride) {
+    while (k < nfr) {
       const int f = w.dm_list ? __builtin_amdgcn_readfirstlane(w.dm_list[k]) : w.f1 - 1 - k;
       const DetRec d = sload(w.det + f);
-      if (d.route != (w.dm_list ? ROUTE_REPLAY : ROUTE_DEMOD)) continue; // (the list launch: replayed frames)
-      F.f = f; F.T = d.T; F.M = d.M; F.start = d.start;
-      F.A = d.A; F.B = d.B;
-      F.X = w.samples + sload(w.off + f);
-      return k;
+      if (d.route == (w.dm_list ? ROUTE_REPLAY : ROUTE_DEMOD)) { // (the list launch: replayed frames)
+        F.f = f; F.T = d.T; F.M = d.M; F.start = d.start;
+        F.A = d.A; F.B = d.B;
+        F.X = w.samples + sload(w.off + f);
+        return k;
+      }
+      k = (!dyn || k + wstride < kstat) ? k + wstride : kstat + __builtin_amdgcn_readfirstlane(claim());
     }
     return nfr;
   };
@@ -1963,9 +1983,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   auto advance = [&](FrameS &F, int &k, int &j) -> bool {
     if (j + 1 < (F.f == live_f ? fnj : max(frame_jobs(F), 1))) { ++j; return true; }
     FrameS nf;
-    const int kn = next_frame(k + wstride, nf);
+    const int kc = (!dyn || k + wstride < kstat) ? k + wstride : kstat + __builtin_amdgcn_readfirstlane(pend);
+    const int kn = next_frame(kc, nf);
     if (kn >= nfr) return false;
     F = nf; k = kn; j = 0;
+    if (dyn && kn + wstride >= kstat) pend = claim(); // (for the frame after this one)
     return true;
   };
   // every load is unconditional (a frame without data symbols reads its CE window, the
@@ -1974,6 +1996,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // the sample registers are refilled with the next job as soon as the FFT input is formed
   FrameS fa, fb;
   int ka = next_frame((int)blockIdx.x * NWAVE + wave, fa), ja = 0, kb, jb;
+  if (dyn && ka < nfr && ka + wstride >= kstat) pend = claim();
   if (ka >= nfr) {
     if (w.tl && lane == 0) w.tl[kTlHead + (int)blockIdx.x * NWAVE + wave] = 0ull;
     return;

@@ -315,6 +315,9 @@ void read_knobs(amod::Knobs &k) {
   k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
   if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
   k.aux_priority = env_int("AMOD_AUX_PRIORITY", 1);
+  k.demod_static = getenv("AMOD_DEMOD_STATIC") != nullptr;
+  k.claim_rounds = std::max(1, env_int("AMOD_CLAIM_ROUNDS", 2));
+  k.claim_min = std::max(2, env_int("AMOD_CLAIM_MIN", 4));
   k.mall_flush_mb = std::max(0, env_int("AMOD_MALL_FLUSH_MB", 0));
   k.stream_minseg = std::max(0, env_int("AMOD_STREAM_MINSEG", 0));
   k.stream_diag = getenv("AMOD_STREAM_DIAG") != nullptr;
@@ -569,7 +572,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // exact-kernel work lists: A (fb[0]) filled by detection, B (fb[1]) by k_demod;
   // list C (fb[2]): frames whose detection the exact kernel replayed, for k_demod
   w.fb_count = fb; w.fb_list = fb_base + 64; w.fb_flags = fb_base + 64 + nframes;
-  w.fb_zero = fb + 1; // (k_detect / k_chunk_prep: the counts of list B and the replay list)
+  w.fb_zero = fb + 1; // (k_detect / k_chunk_prep: the counts of list B and the replay list, the claim counter)
   w.xs = (float *)ctx->xs.p; w.bits = (uint32_t *)ctx->bits.p;
   w.xs_stride = ctx->xs_stride; w.bits_stride = ctx->bits_stride;
   w.options = options;
@@ -712,6 +715,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
         // with frames listed, k_demod leaves one workgroup per CU free
         amod::DevWork wm = wb;
         wm.tl = tl;
+        wm.claim = ctx->knobs.demod_static ? nullptr : fb + 3; // the dynamic tail (zeroed by k_detect)
+        wm.claim_rounds = ctx->knobs.claim_rounds;
+        wm.claim_min = ctx->knobs.claim_min;
         const int nb = demod_blocks(nframes);
         if (per_cu >= 2 && nb >= (int)(ctx->cu_count * per_cu)) {
           wm.yield_count = fb;

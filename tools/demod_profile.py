@@ -51,6 +51,22 @@ def main():
         print(f"waves {ok.sum()}: lifetime median {np.median(b - a):.0f} p10 {np.percentile(b - a, 10):.0f} "
               f"p90 {np.percentile(b - a, 90):.0f}; start spread {a.max() - a.min()}, kernel span {b.max() - a.min()}; "
               f"frames per wave {wl.F / ok.sum():.2f}")
+        # per wave (its first frame f = F - 1 - w, frames last-first): lifetime by the number
+        # of frames it took and by XCD (blockIdx % 8) and SIMD (wave in the workgroup)
+        f_idx = np.nonzero(ok)[0]
+        w = wl.F - 1 - f_idx
+        nw = int(ok.sum())
+        life = (b - a).astype(np.float64)
+        nfw = (wl.F - 1 - w) // nw + 1  # frames w, w + nw, ... below F
+        for k in np.unique(nfw):
+            sel = nfw == k
+            print(f"  waves with {k} frames: {sel.sum()}  lifetime median {np.median(life[sel]):.0f}  "
+                  f"p90 {np.percentile(life[sel], 90):.0f}  per frame {np.median(life[sel]) / k:.0f}")
+        blk = w // 4
+        print("  lifetime median by XCD:", [int(np.median(life[(blk % 8) == x])) for x in range(8)])
+        print("  lifetime median by wave slot:", [int(np.median(life[(w % 4) == x])) for x in range(4)])
+        start = a - a.min()
+        print(f"  start offsets: median {np.median(start):.0f} p90 {np.percentile(start, 90):.0f} max {start.max()}")
     wl.close()
 
 
