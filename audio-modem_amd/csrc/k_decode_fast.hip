@@ -204,6 +204,7 @@ __device__ __forceinline__ void pk_dft8(f2v (&v)[8]) {
 // 72 q2 + l1 resp. 72 q2 + 9 p1 (q2 < 4 inside a group) are distinct mod 32.
 constexpr int XROW = 72;
 constexpr int XCH_F2 = 8 * XROW; // float2 per wave
+constexpr int kDecScratch = 2 * XCH_F2 - 64; // k_demod's decisions: per-lane scratch dwords (past any job's decisions)
 // spec_idx: bits 4-5 of n XOR-ed into bits 1-2. The pass-3 store of lane (p1, q2) writes
 // n = q2 + 8 p1 (+ 64 p2): in each 16-lane ds_write_b64 group (q2 in {2g, 2g + 1}) the
 // float2 slots mod 16 are then (q2 ^ 2 (p1 >> 1)) + 8 (p1 & 1), all distinct (the
@@ -1839,8 +1840,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           }
           db = live ? db : org_bits;
           unc_any |= !KO(0xFFFF) && dib >= 0 && live && margin <= tau;
-          const int pos = sbase + dib;
-          if (dib >= 0) dec[pos / BPS - g0] = db >> (pos & 31);
+          // a lane without a data subcarrier in this slot (pilot, past the band) stores into
+          // its own scratch dword at the buffer's end instead: no exec-mask block per store
+          const uint32_t pos = (uint32_t)(sbase + dib);
+          const uint32_t di = dib >= 0 ? pos / BPS - (uint32_t)g0 : (uint32_t)(kDecScratch + ln);
+          dec[di] = db >> (pos & 31);
         }
         if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
       }
@@ -1853,12 +1857,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       const int rot = (ln / (16 / NQ)) & (NQ - 1);
       for (int i = ln; i < (KO(2) ? 0 : (gend - g0) / DPW); i += 64) {
         const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
+        uint4 t[NQ]; // (every piece requested before the first is combined: one LDS wait)
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) t[k] = q[(k + rot) & (NQ - 1)];
         uint32_t word = 0u;
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) {
-          const uint4 t = q[(k + rot) & (NQ - 1)];
-          word |= (t.x | t.y) | (t.z | t.w);
-        }
+        for (int k = 0; k < NQ; ++k) word |= (t[k].x | t[k].y) | (t[k].z | t[k].w);
         atomicOr(bits + wfirst + i, word);
       }
       asm volatile("" ::: "memory"); // (the next FFT rewrites the buffer)
