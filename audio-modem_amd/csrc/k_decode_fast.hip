@@ -92,6 +92,10 @@ __host__ __device__ constexpr int fine_q(int fc, int sym) { return fine_yw(fc, s
 __host__ __device__ constexpr int fine_e(int fc, int sym) { return fine_q(fc, sym) + fc + 280; }
 __host__ __device__ constexpr int fine_floats(int fc, int sym) { return fine_e(fc, sym) + fc + fine_y(sym); }
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+// the LDS byte address of a pointer into __shared__ memory (the low half of its flat
+// address is the offset in the workgroup's LDS)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
 
 struct Smem {  // fixed part (static LDS)
   float rf[4 * NWAVE];
@@ -222,9 +226,24 @@ __device__ void fft512_wave(f2v (&v)[8], float2 *const X2f, const float2 *__rest
   int l = wave_lane();
   asm volatile("" : "+v"(l)); // keep lane-derived bases inside the job loop
   const int l1 = l & 7, q2 = l >> 3;
+  // each pass's twiddles are requested before its butterflies, so their LDS latency hides
+  // under the arithmetic (the compiler reads them after it, one exposed wait per read pair);
+  // the wait is explicit, with the twiddle registers as its operands
+  f4v t01, t23, t45;
+  f2v t6;
+  {
+    const uint32_t a = lds_addr(tw1 + 64 + l); // rows 1 .. 7, 512 B apart
+    asm volatile("ds_read2st64_b64 %0, %1 offset0:0 offset1:1" : "=v"(t01) : "v"(a));
+    asm volatile("ds_read2st64_b64 %0, %1 offset0:2 offset1:3" : "=v"(t23) : "v"(a));
+    asm volatile("ds_read2st64_b64 %0, %1 offset0:4 offset1:5" : "=v"(t45) : "v"(a));
+    asm volatile("ds_read_b64 %0, %1 offset:3072" : "=v"(t6) : "v"(a));
+  }
   pk_dft8(v);
-#pragma unroll
-  for (int q = 1; q < 8; ++q) v[q] = pk_cmul(v[q], tw1[q * 64 + l]);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t01), "+v"(t23), "+v"(t45), "+v"(t6));
+  v[1] = pk_cmul(v[1], t01.xy); v[2] = pk_cmul(v[2], t01.zw);
+  v[3] = pk_cmul(v[3], t23.xy); v[4] = pk_cmul(v[4], t23.zw);
+  v[5] = pk_cmul(v[5], t45.xy); v[6] = pk_cmul(v[6], t45.zw);
+  v[7] = pk_cmul(v[7], t6);
   // exchange 1: Y1[q][l] at row q, column l
   f2v *const w1 = X2 + l;
 #ifdef AMOD_KO
@@ -249,9 +268,21 @@ __device__ void fft512_wave(f2v (&v)[8], float2 *const X2f, const float2 *__rest
   f2v *const r1 = X2 + q2 * XROW + l1;
 #pragma unroll
   for (int l2 = 0; l2 < 8; ++l2) v[l2] = r1[8 * l2];
+  {
+    const uint32_t a = lds_addr(tw2 + l1); // p1 = 1 .. 7, 64 B apart
+    asm volatile("ds_read2_b64 %0, %1 offset0:8 offset1:16" : "=v"(t01) : "v"(a));
+    asm volatile("ds_read2_b64 %0, %1 offset0:24 offset1:32" : "=v"(t23) : "v"(a));
+    asm volatile("ds_read2_b64 %0, %1 offset0:40 offset1:48" : "=v"(t45) : "v"(a));
+    asm volatile("ds_read_b64 %0, %1 offset:448" : "=v"(t6) : "v"(a));
+  }
+  // (the row's samples above are compiler-issued reads: pk_dft8 waits for them itself; the
+  // twiddle reads behind them are only waited for below)
   pk_dft8(v);
-#pragma unroll
-  for (int p1 = 1; p1 < 8; ++p1) v[p1] = pk_cmul(v[p1], tw2[p1 * 8 + l1]);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t01), "+v"(t23), "+v"(t45), "+v"(t6));
+  v[1] = pk_cmul(v[1], t01.xy); v[2] = pk_cmul(v[2], t01.zw);
+  v[3] = pk_cmul(v[3], t23.xy); v[4] = pk_cmul(v[4], t23.zw);
+  v[5] = pk_cmul(v[5], t45.xy); v[6] = pk_cmul(v[6], t45.zw);
+  v[7] = pk_cmul(v[7], t6);
   __builtin_amdgcn_wave_barrier();
   // exchange 2: U[p1] of lane (l1, q2) at row q2, column 9 p1 + l1 (same base as r1)
 #pragma unroll
@@ -375,6 +406,25 @@ __device__ __forceinline__ float wsum_b(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
   return rlane(v, 63);
+}
+// four wsum_b reductions interleaved step by step: a DPP read of a value the previous VALU
+// instruction wrote needs two wait states, which the three other chains fill (one chain
+// alone pays an s_nop per step)
+__device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) {
+#define AMOD_W4(ctrl)                                                                   \
+  { const float ta = AMOD_DPP_F(a, ctrl), tb = AMOD_DPP_F(b, ctrl), tc = AMOD_DPP_F(c, ctrl), td = AMOD_DPP_F(d, ctrl); \
+    a += ta; b += tb; c += tc; d += td; }
+  AMOD_W4(0xB1) AMOD_W4(0x4E) AMOD_W4(0x141) AMOD_W4(0x140)
+#undef AMOD_W4
+#define AMOD_W4B(ctrl, rmask)                                                           \
+  { const float ta = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), ctrl, rmask, 0xF, false)); \
+    const float tb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(b), ctrl, rmask, 0xF, false)); \
+    const float tc = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c), ctrl, rmask, 0xF, false)); \
+    const float td = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), ctrl, rmask, 0xF, false)); \
+    a += ta; b += tb; c += tc; d += td; }
+  AMOD_W4B(0x142, 0xA) AMOD_W4B(0x143, 0xC)
+#undef AMOD_W4B
+  a = rlane(a, 63); b = rlane(b, 63); c = rlane(c, 63); d = rlane(d, 63);
 }
 __device__ __forceinline__ float wmax_b(float v) {
   v = fmaxf(v, AMOD_DPP_F(v, 0xB1)); v = fmaxf(v, AMOD_DPP_F(v, 0x4E));
@@ -1780,7 +1830,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) pilot(dib_of(rr) == -1, e1[rr], e2[rr]);
       }
-      if (!KO(4)) { ps1 = wsum_b(ps1); pe1 = wsum_b(pe1); ps2 = wsum_b(ps2); pe2 = wsum_b(pe2); }
+      if (!KO(4)) wsum_b4(ps1, pe1, ps2, pe2);
       else { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
       // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
       const bool ph_unc1 = __ballot(pflag1) != 0, ph_unc2 = __ballot(pflag2) != 0;
