@@ -66,6 +66,14 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 #else
 #define KO(b) 0
 #endif
+// k_demod's per-frame phase marks (AMOD_STAMPS, tools/demod_profile.py) exist only in a
+// diagnostic build (-DAMOD_DEMOD_STAMPS, tools/build_variants.sh): compiled in, their
+// pointer and address arithmetic held SGPRs the job loop then spilled to VGPR lanes
+#ifdef AMOD_DEMOD_STAMPS
+constexpr bool kDemodStamps = true;
+#else
+constexpr bool kDemodStamps = false;
+#endif
 #ifndef AMOD_DEMOD_WPE
 #define AMOD_DEMOD_WPE 4                     // k_demod: 104 registers, no VGPR spills; LDS (FFT exchange
                                              // rows, twiddles, bit streams) allows 4 workgroups per CU on C2 anyway
@@ -1669,10 +1677,14 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // c1 / c2: the job's samples; issue_next() refills them with the next job's once they
   // are folded into the FFT input, so those loads fly under this job's FFT, equalise, demap, finish
   auto run_job = [&](const FrameS &cur, const int jcur, f2v (&c)[8], auto &&issue_next) {
+#ifdef AMOD_DEMOD_STAMPS
 #define DSTAMP(k, cond)                                                                   \
   do {                                                                                  \
     if (w.stamps && (cond) && lane == 0) w.stamps[(int64_t)cur.f * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define DSTAMP(k, cond) do { } while (0)
+#endif
     const int f = cur.f;
     amod_debug *const D = DBG ? w.dbg + f : nullptr;
     if (jcur == 0) { // a new frame: clear its bit stream
@@ -2003,7 +2015,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
             // slice-by-4 lookups in the workgroup's LDS copy of the table
             r.actual_crc = KO(1) ? r.expected_crc : crc_len <= kCrcMats * kCrcChunk
                                ? wave_crc32(v, crc_len, cfg.t, crc_t4,
-                                            w.stamps ? w.stamps + (int64_t)f * 32 : nullptr)
+                                            kDemodStamps && w.stamps ? w.stamps + (int64_t)f * 32 : nullptr)
                                : wave_crc32_long(v, crc_len, cfg.t);
             r.crc_valid = r.expected_crc == r.actual_crc;
           }
@@ -2056,7 +2068,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     return;
   }
   const int f_first = fa.f; // diagnostics (AMOD_STAMPS): the wave's lifetime in its first frame's marks
-  if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
+  if (kDemodStamps && w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 28] = __builtin_amdgcn_s_memtime();
   f2v r[8];
   loads(fa, ja, r);
   for (;;) {
@@ -2066,7 +2078,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     if (!hb) break;
     fa = fb; ka = kb; ja = jb;
   }
-  if (w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
+  if (kDemodStamps && w.stamps && lane == 0) w.stamps[(int64_t)f_first * 32 + 29] = __builtin_amdgcn_s_memtime();
   if (w.tl && lane == 0) w.tl[kTlHead + (int)blockIdx.x * NWAVE + wave] = (unsigned long long)wall_clock64();
 }
 template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod(const DevCfg cfg_arg, const DevWork w_arg) {

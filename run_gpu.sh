@@ -12,7 +12,7 @@ for s in "$@"; do
     bench2g) run bench2g 600 env AMOD_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-frames -1 --stream-chunks 0 --no-e2e --legs c4,c5;;
     bench2fail) echo "== bench2fail"; timeout -k 10 300 python bench.py --gpus 2 > gpurun_out/bench2fail.log 2>&1; echo "rc=$? (2 expected)"; tail -2 gpurun_out/bench2fail.log;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --cpu-frames -1;;
-    demodprof) run demod_c2 300 python tools/demod_profile.py c2 && run demod_c4 300 python tools/demod_profile.py c4 && run demod_c5 300 python tools/demod_profile.py c5;;
+    demodprof) export AMODEM_LIB=audio-modem_amd/lib/variants/stamps/libamodem.so; run demod_c2 300 python tools/demod_profile.py c2 && run demod_c4 300 python tools/demod_profile.py c4 && run demod_c5 300 python tools/demod_profile.py c5;;
     streamdiag) run stream_diag 300 python tools/stream_diag.py ${NCHUNKS:-32000};;
     ab) run ab 600 python tools/ab_demod.py $(for v in ${VARIANTS}; do echo audio-modem_amd/lib/variants/$v/libamodem.so; done);;
   esac

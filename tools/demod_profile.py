@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Diagnostics: k_demod phase marks (AMOD_STAMPS=1, s_memtime per wave) on a bench workload.
 
-  python tools/demod_profile.py [c2|c4|c5] [frames]
+  bash tools/build_variants.sh stamps=-DAMOD_DEMOD_STAMPS
+  AMODEM_LIB=audio-modem_amd/lib/variants/stamps/libamodem.so python tools/demod_profile.py [c2|c4|c5] [frames]
+
+(the product build compiles k_demod's marks out: only the exact kernel's remain)
 
 Job 1 of each frame: 16 samples folded -> 17 FFT -> 18 band + equalise -> 19 guards + pilot
 reductions -> 20 demap + bit stream -> 21 end of job; frame end: 22 start -> 23 parse_need ->
