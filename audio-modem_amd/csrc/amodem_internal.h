@@ -141,6 +141,13 @@ struct DevWork {
   // launches use (null: not this launch)
   int32_t *fb_reset;
   int32_t *fb_zero;
+  // a captured decode (runtime.cpp): k_demod's first thread moves list A's count from
+  // snap_a[0] to snap_a[4] and zeroes snap_a[0]; list B's exact launch then takes list A's
+  // frames too, fb_count2 / fb_list2 / fb_flags2 after its own (null: not this launch)
+  int32_t *snap_a;
+  const int32_t *fb_count2;
+  const int32_t *fb_list2;
+  const int32_t *fb_flags2;
   // k_demod (main launch): with at least claim_min frames per wave, the frames past all but
   // the last claim_rounds static rounds are claimed one at a time from this counter (null:
   // every frame static)
@@ -180,7 +187,8 @@ struct Knobs {
   bool no_gap_scan = false; // AMOD_NO_GAP_SCAN
   int stream_threads = -1;  // AMOD_STREAM_THREADS (-1: unset)
   bool stream_fullcopy = false; // AMOD_STREAM_FULLCOPY
-  int ema_warm = 0, ema_per = 0, ema_rounds = 0; // AMOD_EMA_WARM / _PER / _ROUNDS (0: default)
+  // (AMOD_EMA_WARM / _PER / _ROUNDS, the EMA kernels' experiment shapes, are read once per
+  // process by k_stream.hip's launchers, which have no context)
 };
 
 // k_gap_scan -> streaming receiver: the scan that follows the frame of fine range r, run

@@ -583,17 +583,17 @@ void run_blocks(Receiver &rx, const RxState &start, int64_t stop, bool first_onl
 // the true run is carried across each boundary until it demodulates a window that the
 // speculative segment demodulated from the identical post-reset state, and adopts the
 // segment's trajectory from there (or covers the whole segment itself).
-Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, int nthreads, int64_t &fine_host) {
+Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, int nthreads, int64_t &fine_host,
+                  const amod::Knobs &kn) {
   const auto t_par0 = std::chrono::steady_clock::now();
   const int64_t span = nblocks - start.block;
-  const char *ms = getenv("AMOD_STREAM_MINSEG"); // tests: force short speculative segments
-  const int64_t minseg = ms ? std::max(1, atoi(ms)) : 64;
+  const int64_t minseg = kn.stream_minseg > 0 ? kn.stream_minseg : 64; // (tests force short segments)
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, span / minseg));
   std::vector<int64_t> bnd(T + 1);
   for (int k = 0; k <= T; ++k) bnd[k] = start.block + span * k / T;
   std::vector<Traj> seg(T);
   std::vector<Receiver> rxs(T, proto);
-  const bool diag = getenv("AMOD_STREAM_DIAG") != nullptr;
+  const bool diag = kn.stream_diag;
   for (auto &r : rxs) r.timed = diag;
   std::vector<double> th_ms(T, 0.0);
   std::vector<std::thread> th;
@@ -635,7 +635,7 @@ Traj run_parallel(const Receiver &proto, const RxState &start, int64_t nblocks, 
   }
   fine_host += rx.fine_host;
   for (auto &r : rxs) fine_host += r.fine_host;
-  if (getenv("AMOD_STREAM_DIAG")) {
+  if (diag) {
     int64_t sc = rx.scanned;
     double wmax = 0;
     for (auto &r : rxs) { sc += r.scanned; wmax = std::max(wmax, r.wait_ms); }
@@ -749,6 +749,7 @@ struct Prepass {
   FineTable ft;
   int64_t lo = 0, n = 0, fixed = 0;
   bool dev_metrics = false; // k_fine also keeps its metrics on the device (k_gap_refine reads them)
+  const amod::Knobs *kn = nullptr; // the context's knobs (read at amod_open)
   int64_t nmetric = 0;
   int64_t nhot = 0;            // 32-sample blocks screened (hot flags on the device)
   // the EMA state after local chunk k (its true end state, read from the device)
@@ -868,7 +869,7 @@ struct Prepass {
   int gap_scan_launch(const amod_cfg *cfg, const RxState &start, int64_t nblocks, int64_t cap) {
     gaps.clear();
     gap_launched = false;
-    if (nfr <= 0 || getenv("AMOD_NO_GAP_SCAN")) return AMOD_SUCCESS;
+    if (nfr <= 0 || kn->no_gap_scan) return AMOD_SUCCESS;
     const int32_t maxp = start.meta_received ? (start.chunk_size ? start.chunk_size : 4096) + 11 : 280;
     const int64_t F = amod_estimate_frame_samples(cfg, maxp);
     if (c->d_gaps.alloc(sizeof(amod::GapScan) * (size_t)nfr) != hipSuccess ||
@@ -1151,7 +1152,7 @@ struct Prepass {
     const auto tq2 = std::chrono::steady_clock::now();
     S_TRY(hipEventRecord(ev[2], s));
     S_TRY(hipStreamSynchronize(s));
-    if (getenv("AMOD_STREAM_DIAG"))
+    if (kn->stream_diag)
       fprintf(stderr, "[stream] prepass: wait for EMA+screen %.3f ms, fine ranges + launch %.3f ms (%zu ranges, %lld "
               "positions, longest %lld), k_fine wait %.3f ms\n",
               std::chrono::duration<double, std::milli>(tq1 - tq0).count(),
@@ -1316,9 +1317,9 @@ void apply_meta(const amod_result &r, RxState &after) {
   if (r.total_chunks > -8) after.meta_received = true;
 }
 
-int receiver_threads() {
-  const char *tenv = getenv("AMOD_STREAM_THREADS"); // tests: 1 = the plain sequential receiver
-  return tenv ? std::max(1, atoi(tenv)) : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+int receiver_threads(const amod::Knobs &kn) { // (AMOD_STREAM_THREADS=1 in tests: the plain sequential receiver)
+  return kn.stream_threads > 0 ? kn.stream_threads
+                               : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
 void to_state(const RxState &a, amod_stream_state &o) {
@@ -1382,8 +1383,10 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   const int64_t nblocks = (n + kBlock - 1) / kBlock, npad = nblocks * kBlock;
   amod_stream_stats stt{};
   Prepass pp;
-  pp.sparse = !getenv("AMOD_STREAM_FULLCOPY"); // (diagnostics: the whole cleaned stream to the host)
-  pp.dev_metrics = !getenv("AMOD_NO_GAP_SCAN");  // refinements of the gap scans' detections on the GPU
+  const amod::Knobs &kn = *amod_ctx_knobs(ctx);
+  pp.kn = &kn;
+  pp.sparse = !kn.stream_fullcopy; // (diagnostics: the whole cleaned stream to the host)
+  pp.dev_metrics = !kn.no_gap_scan; // refinements of the gap scans' detections on the GPU
   {
     const int rc = pp.run(ctx, cfg, samples, n, 0, npad, s, device);
     if (rc) return rc;
@@ -1401,7 +1404,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   }
   struct Guard { amod_assembler *a; ~Guard() { if (a) amod_asm_close(a); } } guard{own};
   Receiver proto = pp.receiver(cfg);
-  const int nthreads = receiver_threads();
+  const int nthreads = receiver_threads(kn);
   bool sparse_done = false;
   int64_t nfr = 0, frames_decoded = 0, frame_errors = 0, fine_host = 0;
   std::vector<int64_t> fails_out;
@@ -1508,7 +1511,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
         if (grc) return amod_ctx_fail(ctx, "gap scan", grc);
         if (!pp.gaps.empty()) proto.gaps = &pp.gaps;
         if (!pp.refs.empty()) proto.refs = &pp.refs;
-        if (getenv("AMOD_STREAM_DIAG")) {
+        if (kn.stream_diag) {
           int64_t smax = 0, ssum = 0;
           for (auto &g : pp.gaps) { smax = std::max(smax, g.scanned); ssum += g.scanned; }
           fprintf(stderr, "[stream] sparse setup %.3f ms (marks %.3f, index %.3f, pointers %.3f, copies %.3f), then gap scan: "
@@ -1521,13 +1524,13 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
           proto.gptr = pp.gptr; proto.present = &pp.present_fn; proto.copied = &pp.copied_fn;
         }
       }
-      tr = run_parallel(proto, st, nblocks, nthreads, fine_host);
+      tr = run_parallel(proto, st, nblocks, nthreads, fine_host, kn);
     }
     int64_t chg = -1;
     const auto t_dd = clk::now();
     const int rc = decode_dispatch(tr.frames, 0, tr.frames.size(), chg);
     if (rc) return rc;
-    if (getenv("AMOD_STREAM_DIAG"))
+    if (kn.stream_diag)
       fprintf(stderr, "[stream] decode_dispatch of %zu frames: %.3f ms (since prepass %.3f ms; window decoder %.3f ms (launches %.3f), "
               "per-frame loop %.3f ms, chunk copies %.3f ms so far)\n", tr.frames.size(),
               std::chrono::duration<double, std::milli>(clk::now() - t_dd).count(),
@@ -1558,7 +1561,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
     stt.final_state = final_state.state;
     stt.final_scan_pos = final_state.ac_pos;
     stt.fine_host_positions = fine_host;
-    if (getenv("AMOD_STREAM_DIAG"))
+    if (kn.stream_diag)
       fprintf(stderr, "[stream] sparse copy: %lld of %lld granules packed, %lld fetched on demand (%.3f ms), piece waits "
               "%.3f ms, full copy %d; fine positions on the host %lld\n",
               (long long)pp.npacked, (long long)pp.ng, (long long)pp.fallbacks.load(), pp.fetch_us.load() * 1e-3,
@@ -1599,6 +1602,8 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
   S_TRY(hipSetDevice(amod_ctx_device(ctx)));
   hipStream_t s = amod_ctx_stream(ctx);
   Prepass pp;
+  const amod::Knobs &kn = *amod_ctx_knobs(ctx);
+  pp.kn = &kn;
   {
     const int rc = pp.run(ctx, cfg, samples, hi - lo, lo, hi - lo, s);
     if (rc) return rc;
@@ -1651,7 +1656,7 @@ extern "C" int amod_stream_shard(amod_ctx *ctx, const amod_cfg *cfg, const float
       if (st.meta_received || st.block >= stop) break;
     }
   } else {
-    tr = run_parallel(pp.receiver(cfg), st, stop, receiver_threads(), fine_host);
+    tr = run_parallel(pp.receiver(cfg), st, stop, receiver_threads(kn), fine_host, kn);
   }
   *nevents = 0;
   size_t first = 0;
