@@ -45,6 +45,7 @@ struct DevTables {
   const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
   const uint32_t *crc_mat; // [kCrcMats][32] shift-by-(16*q) zero-byte operators as GF(2) matrices (column i = image of bit i)
   const uint32_t *crc_pre; // [16] register k zero bytes before the message start that becomes ~0 there
+  const uint32_t *crc_unpad; // [16][32] inverse k-zero-byte operators (same layout as crc_mat)
                            // (the inverse k-byte shift of ~0): chunk 0 left-padded to 16 bytes
   const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
   const double2 *tw_inv;   // [511] inverse-transform recurrence twiddles (fftIterative, ifft)
@@ -141,13 +142,6 @@ struct DevWork {
   // launches use (null: not this launch)
   int32_t *fb_reset;
   int32_t *fb_zero;
-  // a captured decode (runtime.cpp): k_demod's first thread moves list A's count from
-  // snap_a[0] to snap_a[4] and zeroes snap_a[0]; list B's exact launch then takes list A's
-  // frames too, fb_count2 / fb_list2 / fb_flags2 after its own (null: not this launch)
-  int32_t *snap_a;
-  const int32_t *fb_count2;
-  const int32_t *fb_list2;
-  const int32_t *fb_flags2;
   // k_demod (main launch): with at least claim_min frames per wave, the frames past all but
   // the last claim_rounds static rounds are claimed one at a time from this counter (null:
   // every frame static)

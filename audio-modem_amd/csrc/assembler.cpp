@@ -22,6 +22,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -37,10 +38,28 @@
 // claims a large file commits memory only for the chunks actually received (the reference
 // allocates the file only in assembleFile, app.js:668). release() stops the helper at its
 // next step instead of waiting for the whole window.
+// A released arena is kept for the next one (one mapping of at most kPoolMax bytes,
+// process-wide): a receiver serving recording after recording reuses the pages it has
+// already faulted in, and its helper thread does not hold the address-space lock (read,
+// 2 MB at a time) under the next receiver's host phase, whose own mappings (thread
+// stacks, vectors) queue behind it (2.4 ms of the 32k-chunk stream's sparse setup). Only
+// chunks a Loc records are ever read back, so the previous file's bytes stay unseen.
+struct ArenaPool {
+  static constexpr size_t kPoolMax = size_t(1) << 30;
+  std::mutex mu;
+  uint8_t *p = nullptr;
+  size_t n = 0, populated = 0;
+};
+static ArenaPool &arena_pool() {
+  static ArenaPool pool;
+  return pool;
+}
+
 struct FileArena {
   static constexpr size_t kPopulateMax = size_t(256) << 20;
   uint8_t *p = nullptr;
-  size_t n = 0;
+  size_t n = 0;                        // the mapping's length (>= the file span)
+  std::atomic<size_t> populated{0};    // bytes from the start the helper has faulted in
   std::thread filler;
   std::atomic<bool> stop{false};
   ~FileArena() { release(); }
@@ -48,31 +67,55 @@ struct FileArena {
     stop.store(true, std::memory_order_relaxed);
     if (filler.joinable()) filler.join();
     stop.store(false, std::memory_order_relaxed);
-    if (p) munmap(p, n);
+    if (p) {
+      ArenaPool &pool = arena_pool();
+      std::lock_guard<std::mutex> lk(pool.mu);
+      if (n <= ArenaPool::kPoolMax) {
+        if (pool.p) munmap(pool.p, pool.n);
+        pool.p = p; pool.n = n; pool.populated = populated.load(std::memory_order_relaxed);
+      } else {
+        munmap(p, n);
+      }
+    }
     p = nullptr;
     n = 0;
+    populated.store(0, std::memory_order_relaxed);
   }
   bool map(size_t bytes) {
     release();
     if (!bytes) return false;
-    void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (q == MAP_FAILED) return false;
-    p = (uint8_t *)q;
-    n = bytes;
+    size_t done = 0;
+    {
+      ArenaPool &pool = arena_pool();
+      std::lock_guard<std::mutex> lk(pool.mu);
+      if (pool.p && pool.n >= bytes && pool.n <= 2 * bytes + (size_t(64) << 20)) { // (not a far larger one)
+        p = pool.p; n = pool.n; done = pool.populated;
+        pool.p = nullptr; pool.n = pool.populated = 0;
+      }
+    }
+    if (!p) {
+      void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+      if (q == MAP_FAILED) return false;
+      p = (uint8_t *)q;
+      n = bytes;
 #ifdef MADV_HUGEPAGE
-    (void)madvise(p, n, MADV_HUGEPAGE);
+      (void)madvise(p, n, MADV_HUGEPAGE);
 #endif
-    if (getenv("AMOD_ASM_NO_POPULATE")) return true; // (experiments: first-touch faults in the copies)
-    filler = std::thread([q = p, len = std::min(n, kPopulateMax), halt = &stop] {
+    }
+    populated.store(done, std::memory_order_relaxed);
+    const size_t len = std::min(n, kPopulateMax);
+    if (getenv("AMOD_ASM_NO_POPULATE") || done >= len) return true; // (experiments: first-touch faults in the copies)
+    filler = std::thread([this, q = p, from = done, len] {
       constexpr int kPopulateWrite = 23; // MADV_POPULATE_WRITE (Linux 5.14)
       // one huge page per call: each call holds the address-space lock (read) while it
       // zeroes, and the receiver's own mappings (thread stacks, vectors) wait for it
       constexpr size_t kStep = size_t(2) << 20;
-      for (size_t o = 0; o < len && !halt->load(std::memory_order_relaxed); o += kStep) {
+      for (size_t o = from; o < len && !stop.load(std::memory_order_relaxed); o += kStep) {
         const size_t m = std::min(kStep, len - o);
         if (madvise(q + o, m, kPopulateWrite) != 0) { // older kernels: touch every page, value kept
           for (size_t b = o; b < o + m; b += 4096) __atomic_fetch_add(q + b, (uint8_t)0, __ATOMIC_RELAXED);
         }
+        populated.store(o + m, std::memory_order_relaxed);
       }
     });
     return true;

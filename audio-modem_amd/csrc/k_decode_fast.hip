@@ -1352,17 +1352,17 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
 // the exact kernel instead.
 
 // Wave-level CRC-32 (modem.js:443-457) of bytes [0, L) of stream v. The message is cut
-// into 16-byte chunks, right-aligned; chunk 0 is left-padded with zero bytes to a whole
-// chunk and starts from t.crc_pre[pad] (the register that the pad's zero bytes advance to
-// the reference's initial ~0), every other chunk from 0. Each chunk's register comes from
-// slice-by-4 lookups in the workgroup's copy of the table in LDS (t4l: 4 KB, staged once
-// at the kernel start; round 2 staged it per frame into the wave's exchange buffer: 2.6 K
-// cycles of global loads per frame), is moved to the message end by the GF(2) matrix of its
-// zero-byte shift and the images are XOR-combined (CRC linearity). Lane l takes chunks
-// whose distance to the end is l, l + 64, ..., CRC_ILP of them interleaved, so the
-// dependent lookups of different chunks overlap; the whole message is one pass (the
-// frame-end CRC was a chain of global-memory lookups: 13.5k cycles per C2 frame, 24.7k per
-// C4 window, tools/demod_profile.py).
+// into 16-byte chunks (wave_crc32: left-aligned, the last one zero-padded; wave_crc32_long:
+// right-aligned, the first one zero-padded and started from t.crc_pre[pad], the register
+// that the pad's zero bytes advance to the reference's initial ~0). Each chunk's register
+// comes from slice-by-4 lookups in the workgroup's copy of the table in LDS (t4l: 4 KB,
+// staged once at the kernel start; round 2 staged it per frame into the wave's exchange
+// buffer: 2.6 K cycles of global loads per frame), is moved to the message end by the
+// GF(2) matrix of its zero-byte shift and the images are XOR-combined (CRC linearity).
+// Lane l takes chunks l, l + 64, ..., CRC_ILP of them interleaved, so the dependent
+// lookups of different chunks overlap; the whole message is one pass (the frame-end CRC
+// was a chain of global-memory lookups: 13.5k cycles per C2 frame, 24.7k per C4 window,
+// tools/demod_profile.py).
 // bytes i .. i + 3 of an MSB-first stream as one little-endian word (CRC byte order);
 // bytes before the stream start (i >= -15) read as zero
 __device__ __forceinline__ uint32_t le_word_pad(const uint32_t *v, int i) {
@@ -1385,40 +1385,60 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   return r;
 }
 constexpr int CRC_ILP = 4;
+// chunks are LEFT-aligned here (chunk j = bytes [16 j, 16 j + 16), the last one zero-padded
+// to a whole chunk), so lane j reads its chunk as one ds_read_b128 (lanes 16 B apart: no
+// bank conflicts; the right-aligned chunks of round 3 took two unaligned ds_read_b32 per
+// word, lanes four words apart: 4-way). Chunk 0 starts from the reference's ~0; the
+// register of the padded message is moved back over the pad's zero bytes at the end by
+// crc_unpad[pad] (the inverse zero-byte operator, the workgroup's LDS copy of
+// t.crc_unpad: a global read there was one more dependent round trip per frame end).
 __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4l,
-                                               unsigned long long *stp = nullptr) {
+                                               const uint32_t *crc_unpad, unsigned long long *stp = nullptr) {
   const int lane = wave_lane();
   if (stp && lane == 0) stp[30] = __builtin_amdgcn_s_memtime(); // (diagnostics: table staged)
   const uint32_t *const t4 = t4l;
   const int nch = (L + kCrcChunk - 1) / kCrcChunk;
-  const uint32_t r0 = t.crc_pre[(kCrcChunk - (L & (kCrcChunk - 1))) & (kCrcChunk - 1)];
+  const int pad = kCrcChunk * nch - L;
   uint32_t acc = 0;
   for (int q0 = 0; q0 < nch; q0 += 64 * CRC_ILP) {
     uint32_t c[CRC_ILP];
-    int beg[CRC_ILP];
+    uint4 wd[CRC_ILP];
 #pragma unroll
     for (int k = 0; k < CRC_ILP; ++k) {
-      const int q = q0 + 64 * k + lane; // chunk distance to the end, in chunks
-      beg[k] = L - kCrcChunk * (q + 1);
-      c[k] = q == nch - 1 ? r0 : 0u;
+      const int j = q0 + 64 * k + lane; // chunk index from the message start
+      c[k] = j == 0 ? 0xFFFFFFFFu : 0u;
+      wd[k] = make_uint4(0, 0, 0, 0);
+      if (q0 + 64 * k < nch && j < nch) { // (wave-uniform first test)
+        wd[k] = reinterpret_cast<const uint4 *>(v)[j];
+        if (j == nch - 1 && pad) { // bytes past L read as zero (MSB-first words)
+          const int nv = kCrcChunk - pad; // valid bytes of this chunk, 1 .. 15
+          const auto keep = [&](int st) -> uint32_t {
+            const int b = nv - 4 * st;
+            return b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * b));
+          };
+          wd[k].x &= keep(0); wd[k].y &= keep(1); wd[k].z &= keep(2); wd[k].w &= keep(3);
+        }
+      }
     }
 #pragma unroll
     for (int st = 0; st < kCrcChunk / 4; ++st) {
 #pragma unroll
       for (int k = 0; k < CRC_ILP; ++k) {
         if (q0 + 64 * k >= nch) continue; // wave-uniform
-        uint32_t x = c[k] ^ le_word_pad(v, max(beg[k], -kCrcChunk) + 4 * st);
+        const uint32_t wv = st == 0 ? wd[k].x : st == 1 ? wd[k].y : st == 2 ? wd[k].z : wd[k].w;
+        const uint32_t x = c[k] ^ __builtin_bswap32(wv);
         c[k] = t4[768 + (x & 0xFF)] ^ t4[512 + ((x >> 8) & 0xFF)] ^ t4[256 + ((x >> 16) & 0xFF)] ^ t4[x >> 24];
       }
     }
     if (stp && lane == 0 && q0 == 0) stp[31] = __builtin_amdgcn_s_memtime(); // (chunk registers)
 #pragma unroll
     for (int k = 0; k < CRC_ILP; ++k) {
-      const int q = q0 + 64 * k + lane;
-      if (q0 + 64 * k < nch && q < nch) acc ^= crc_shift(t.crc_mat, q, c[k]);
+      const int j = q0 + 64 * k + lane;
+      if (q0 + 64 * k < nch && j < nch) acc ^= crc_shift(t.crc_mat, nch - 1 - j, c[k]);
     }
   }
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc)) ^ 0xFFFFFFFFu;
+  const uint32_t reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
+  return (pad ? crc_shift(crc_unpad, pad, reg) : reg) ^ 0xFFFFFFFFu;
 }
 
 // the same over messages longer than kCrcMats chunks (8 KB): kCrcMats-chunk blocks in
@@ -1522,6 +1542,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][XCH_F2];
   __shared__ float2 twl[512];   // tw1 rows 1-7 (row q at 64 (q - 1)), then tw2[64]
   __shared__ __attribute__((aligned(16))) uint32_t crc_t4[1024]; // CRC slice-by-4 table (frame ends)
+  __shared__ __attribute__((aligned(16))) uint32_t crc_up[16 * 32]; // inverse zero-byte operators
   FRESH_ARGS;
   const int tid = ltid();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1532,6 +1553,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     if (tid + WG < 7 * 64) twl[WG + tid] = t1b;
     if (tid < 64) twl[7 * 64 + tid] = t2;
     reinterpret_cast<uint4 *>(crc_t4)[tid] = c4;
+    if (tid < 128) reinterpret_cast<uint4 *>(crc_up)[tid] = reinterpret_cast<const uint4 *>(cfg.t.crc_unpad)[tid];
   }
   __syncthreads();
   const int lane = tid & 63;
@@ -2014,7 +2036,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           if (crc_len >= 0) {
             // slice-by-4 lookups in the workgroup's LDS copy of the table
             r.actual_crc = KO(1) ? r.expected_crc : crc_len <= kCrcMats * kCrcChunk
-                               ? wave_crc32(v, crc_len, cfg.t, crc_t4,
+                               ? wave_crc32(v, crc_len, cfg.t, crc_t4, crc_up,
                                             kDemodStamps && w.stamps ? w.stamps + (int64_t)f * 32 : nullptr)
                                : wave_crc32_long(v, crc_len, cfg.t);
             r.crc_valid = r.expected_crc == r.actual_crc;

@@ -4,15 +4,15 @@
 //                m_i = 0.999 m_(i-1) + (1 - 0.999) x_i in IEEE double, cleaned_i =
 //                f32(x_i - m_i), bit-exact. (1) each 1024-sample chunk's contribution
 //                to the state at its end, coalesced; (2) one lane per chunk runs the
-//                exact recurrence from an approximate state 16 chunks back (a short
+//                exact recurrence from an approximate state 4 chunks back (a short
 //                geometric sum of those contributions; the map
 //                contracts by 0.999 a step, so the chain meets the true one bit for bit)
-//                and through its own chunk, samples staged through per-wave LDS tiles
+//                and through its own 8 chunks, samples staged through per-wave LDS tiles
 //                (coalesced rows, one row per lane); (3) every chunk whose warm-up state
 //                differs from its predecessor's end state is listed, (4) and recomputed
 //                from the true state in order. Afterwards every cleaned sample equals the
 //                reference's.
-//   k_sc_blocks  fp64 32-sample block sums (coalesced, 32-lane reductions), then
+//   k_sc_blocks  fp32 32-sample block sums (coalesced, 8-lane DPP reductions), then
 //   k_sc_screen  hot-block screening for the fine precompute: the Schmidl-Cox metric
 //                at each block start from 8-block window sums; only a hint (the host
 //                recomputes anything the hint missed).
@@ -52,32 +52,44 @@ constexpr int kRPI = 64 / kLPR;                // tile rows per load instruction
 __device__ __forceinline__ double ema_step(double m, float x) { return kAlpha * m + kOneMinusAlpha * (double)x; }
 
 // (1) c_k = sum_i a^(L-1-i) (1-a) x_(kL+i): chunk k's contribution to the EMA at its end
-// from a zero start (fp64, approximate: it only seeds the warm-up). One workgroup per
-// chunk, coalesced. apow[j] = a^j.
+// from a zero start (fp64, approximate: it only seeds the warm-up). One WAVE per chunk,
+// chunks [kbase, kend): lane l takes samples 4 l + 256 u (u < 4) as float4 buffer loads
+// (1 KB per wave-instruction; dwords past nx read 0), apow[j] = a^j as double2 pairs. (One
+// 256-thread workgroup per chunk with dword loads ran at 4.2 TB/s: 888 K workgroups of
+// four loads a thread for a 32k-chunk stream.)
 __global__ __launch_bounds__(256) void k_ema_contrib(const float *__restrict__ x, int64_t nx,
                                                      const double *__restrict__ apow, double *__restrict__ c,
-                                                     int64_t kbase) {
-  __shared__ double red[4];
-  const int64_t k = kbase + blockIdx.x;
-  const int tid = threadIdx.x;
+                                                     int64_t kbase, int64_t kend) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = kbase + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= kend) return;
+  const int64_t a0 = k * kL, len = nx - a0 < kL ? (nx - a0 > 0 ? nx - a0 : 0) : kL;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(x + a0), (short)0, (int)(4 * len), 0x00020000);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  u4 v[kL / 256];
+#pragma unroll
+  for (int u = 0; u < kL / 256; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * lane + 1024 * u, 0, 0);
   double acc = 0.0;
 #pragma unroll
   for (int u = 0; u < kL / 256; ++u) {
-    const int i = tid + 256 * u;
-    const int64_t g = k * kL + i;
-    if (g < nx) acc += apow[kL - 1 - i] * (kOneMinusAlpha * (double)x[g]);
+    const int i = 4 * lane + 256 * u; // samples i .. i + 3 weigh a^(L-1-i) .. a^(L-4-i)
+    const double2 p01 = *reinterpret_cast<const double2 *>(apow + kL - 4 - i); // a^(L-4-i), a^(L-3-i)
+    const double2 p23 = *reinterpret_cast<const double2 *>(apow + kL - 2 - i); // a^(L-2-i), a^(L-1-i)
+    acc += p23.y * (kOneMinusAlpha * (double)__uint_as_float(v[u][0]));
+    acc += p23.x * (kOneMinusAlpha * (double)__uint_as_float(v[u][1]));
+    acc += p01.y * (kOneMinusAlpha * (double)__uint_as_float(v[u][2]));
+    acc += p01.x * (kOneMinusAlpha * (double)__uint_as_float(v[u][3]));
   }
   acc = wave_sum(acc);
-  if ((tid & 63) == 0) red[tid >> 6] = acc;
-  __syncthreads();
-  if (tid == 0) c[k] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (lane == 0) c[k] = acc;
 }
 
 // (2) the exact recurrence, one lane per chunk: from the approximate state at the end of
 // chunk k - kWarm - 1 (sum_j A^j c_(k - kWarm - 1 - j), A = a^L = 0.36: forty terms leave
 // a relative error below 1e-17), kWarm chunks of warm-up (the map contracts by 0.999 a step, so the
 // chain reaches the true one bit for bit), then chunk k with its outputs. The samples move
-// through a per-wave LDS tile (64 lanes x 64 samples): rows loaded coalesced one tile
+// through a per-wave LDS tile (64 lanes x 32 samples): rows loaded coalesced two tiles
 // ahead (registers), each lane walking its own row, output rows stored coalesced.
 // warm[k] = the state reached at chunk k's start. A lane outputs `per` consecutive chunks
 // after one warm-up (per = 1 read every sample kWarm + 1 times, from HBM: the re-reads are
@@ -113,8 +125,11 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
       (void *)(x + wb), (short)0, (int)(4 * (xlen < (1 << 28) ? xlen : (1 << 28))), 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)(y + yb), (short)0, (int)(4 * (ylen < (1 << 28) ? ylen : (1 << 28))), 0x00020000);
-  float4 pf[kLPR]; // the next tile's samples
-  auto load = [&](int j) {
+  // two tiles in flight (pfa: even steps, pfb: odd): with ~7 waves per CU for a C4-sized
+  // stream, one tile ahead (8 KB per wave) left each step waiting out most of a load's
+  // latency (k_ema_out 2.1 ms for a 3.6 GB stream, 4.3 TB/s of its 9.1 GB)
+  float4 pfa[kLPR], pfb[kLPR];
+  auto load = [&](int j, float4 (&pf)[kLPR]) {
 #pragma unroll
     for (int q = 0; q < kLPR; ++q) {
       const int64_t g = (k0 + (int64_t)per * (rr + kRPI * q) - kWarm) * kL + (int64_t)kTile * j + 4 * c4 - wb;
@@ -122,13 +137,12 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
       pf[q] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
   };
-  load(0);
-  for (int j = 0; j < steps; ++j) {
+  auto step = [&](int j, float4 (&pf)[kLPR]) {
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int q = 0; q < kLPR; ++q) *reinterpret_cast<float4 *>(T + (rr + kRPI * q) * kRow + 4 * c4) = pf[q];
     __builtin_amdgcn_wave_barrier();
-    if (j + 1 < steps) load(j + 1); // in flight under this tile's recurrence
+    if (j + 2 < steps) load(j + 2, pf); // in flight under this tile's and the next one's recurrence
     const int64_t row0 = (k - kWarm) * kL + (int64_t)kTile * j; // first sample of this lane's row
     const bool out = j >= wsteps;                                // chunks k .. k + per - 1
     if (out && (j - wsteps) % (kL / kTile) == 0) { // an output chunk starts
@@ -177,6 +191,12 @@ __global__ __launch_bounds__(256) void k_ema_out(const float *__restrict__ x, in
         __builtin_amdgcn_raw_buffer_store_b128(w, yrr, (int)(4 * g), 0, 0);
       }
     }
+  };
+  load(0, pfa);
+  if (steps > 1) load(1, pfb);
+  for (int j = 0; j < steps; j += 2) {
+    step(j, pfa);
+    if (j + 1 < steps) step(j + 1, pfb);
   }
   const int64_t kl = k + per - 1 < nch ? k + per - 1 : nch - 1; // the lane's last chunk
   if (kl >= k) end[kl] = m;
@@ -317,23 +337,41 @@ __global__ __launch_bounds__(64) void k_ema_fix(const float *__restrict__ x, int
   if (lane == 0 && nf) *fixed += nf;
 }
 
-// 32-sample block sums of the cleaned stream in fp64: z_b = sum y[k] y[k+256], e_b =
-// sum y[k]^2 over k in [32 b, 32 b + 32) (a screening hint: any order); four samples per
-// lane (float4, coalesced), 8-lane reductions. n is a multiple of 4.
+// 32-sample block sums of the cleaned stream: z_b = sum y[k] y[k+256], e_b = sum y[k]^2
+// over k in [32 b, 32 b + 32) (a screening hint, any order and precision: the host
+// recomputes anything it misses, and hot means a metric >= 0.25 against the reference's
+// 0.5). Four samples per lane (float4, coalesced) in fp32, the 8 lanes of a block combined
+// by DPP within the row (quad swaps, then the half-row mirror): no LDS. (fp64 sums with
+// 8-lane bpermute shuffles: 1.9 ms for a 32k-chunk stream, 1.9 TB/s.) n is a multiple of 4.
+__device__ __forceinline__ float dpp_add(float v, int ctrl) {
+  const int o = ctrl == 0xB1 ? __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)
+              : ctrl == 0x4E ? __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)
+                             : __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false);
+  return v + __int_as_float(o);
+}
 __global__ __launch_bounds__(256) void k_sc_blocks(const float *__restrict__ y, int64_t n, int64_t nblk,
                                                    double2 *__restrict__ ze) {
   const int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 a = k < n ? *reinterpret_cast<const float4 *>(y + k) : zero4;
-  const float4 c = k + 256 < n ? *reinterpret_cast<const float4 *>(y + k + 256) : zero4;
-  double z = (double)a.x * c.x, e = (double)a.x * a.x;
-  z = __builtin_fma((double)a.y, (double)c.y, z); e = __builtin_fma((double)a.y, (double)a.y, e);
-  z = __builtin_fma((double)a.z, (double)c.z, z); e = __builtin_fma((double)a.z, (double)a.z, e);
-  z = __builtin_fma((double)a.w, (double)c.w, z); e = __builtin_fma((double)a.w, (double)a.w, e);
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) { z += __shfl_xor(z, o, 8); e += __shfl_xor(e, o, 8); }
+  // raw buffer loads over this workgroup's 1024 + 256 samples (dwords past n read 0): plain
+  // float4 reads under the range tests compiled to four dword loads each
+  const int64_t base = (int64_t)blockIdx.x * 1024;
+  const int64_t len = n - base < 1024 + 256 ? (n - base > 0 ? n - base : 0) : 1024 + 256;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void *)(y + base), (short)0, (int)(4 * len),
+                                                                      0x00020000);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 av = __builtin_amdgcn_raw_buffer_load_b128(yr, 16 * (int)threadIdx.x, 0, 0);
+  const u4 cv = __builtin_amdgcn_raw_buffer_load_b128(yr, 16 * (int)threadIdx.x + 1024, 0, 0);
+  const float4 a = make_float4(__uint_as_float(av[0]), __uint_as_float(av[1]), __uint_as_float(av[2]), __uint_as_float(av[3]));
+  const float4 c = make_float4(__uint_as_float(cv[0]), __uint_as_float(cv[1]), __uint_as_float(cv[2]), __uint_as_float(cv[3]));
+  float z = a.x * c.x, e = a.x * a.x;
+  z = fmaf(a.y, c.y, z); e = fmaf(a.y, a.y, e);
+  z = fmaf(a.z, c.z, z); e = fmaf(a.z, a.z, e);
+  z = fmaf(a.w, c.w, z); e = fmaf(a.w, a.w, e);
+  z = dpp_add(z, 0xB1); e = dpp_add(e, 0xB1);   // lanes 0<->1, 2<->3
+  z = dpp_add(z, 0x4E); e = dpp_add(e, 0x4E);   // 0<->2, 1<->3: the quad's sum
+  z = dpp_add(z, 0x141); e = dpp_add(e, 0x141); // lane i <-> 7 - i: the other quad
   const int64_t b = k >> 5;
-  if ((threadIdx.x & 7) == 0 && b < nblk) ze[b] = make_double2(z, e);
+  if ((threadIdx.x & 7) == 0 && b < nblk) ze[b] = make_double2((double)z, (double)e);
 }
 
 // hot flag per block: the metric at position 32 b (window = 8 blocks) >= thresh
@@ -734,19 +772,63 @@ __global__ __launch_bounds__(256) void k_window(const float *__restrict__ y, int
                                                 const int32_t *__restrict__ len, const int64_t *__restrict__ woff,
                                                 float *__restrict__ out) {
   __shared__ float red[4];
+  __shared__ int red_nan[4];
   const int w = blockIdx.x, tid = threadIdx.x;
   const int64_t p = pos[w], o = woff[w];
   const int L = len[w];
+  // Math.max over |x| (app.js:920): a NaN sample makes mx NaN, and then `mx > 1e-6` is false
+  // (fmaxf would skip it): tracked beside the max
   float mx = 0.f;
-  for (int i = tid; i < L; i += 256) mx = fmaxf(mx, fabsf(sample_at(y, n, p + i)));
+  bool nan = false;
+  // a window inside the stream (every one the receiver cuts): float4 buffer loads over it,
+  // four in flight per thread (dwords past L read 0; the output offset o is a multiple of 4)
+  const bool inside = p >= 0 && p + L <= n;
+  const int nq = (L + 3) >> 2;
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(y + (inside ? p : 0)), (short)0, (int)(4 * (int64_t)L), 0x00020000);
+  auto ld = [&](int q) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(yr, 16 * q, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  };
+  if (inside) {
+    for (int q0 = tid; q0 < nq; q0 += 4 * 256) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld(q0 + 256 * u); // (past nq: past L, zeros)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+        nan |= (v[u].x != v[u].x) | (v[u].y != v[u].y) | (v[u].z != v[u].z) | (v[u].w != v[u].w);
+      }
+    }
+  } else {
+    for (int i = tid; i < L; i += 256) {
+      const float v = sample_at(y, n, p + i);
+      mx = fmaxf(mx, fabsf(v));
+      nan |= v != v;
+    }
+  }
   mx = wave_max(mx);
-  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  const bool wnan = __ballot(nan) != 0;
+  if ((tid & 63) == 0) { red[tid >> 6] = mx; red_nan[tid >> 6] = wnan; }
   __syncthreads();
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const bool norm = !(red_nan[0] | red_nan[1] | red_nan[2] | red_nan[3]) && (double)mx > 1e-6;
   const double dm = (double)mx;
-  for (int i = tid; i < L; i += 256) {
-    const float v = sample_at(y, n, p + i);
-    out[o + i] = dm > 1e-6 ? (float)((double)v / dm) : v;
+  if (inside) {
+    float4 *const o4 = reinterpret_cast<float4 *>(out + o);
+    for (int q = tid; q < nq; q += 256) {
+      const float4 v = ld(q);
+      o4[q] = norm ? make_float4((float)((double)v.x / dm), (float)((double)v.y / dm), (float)((double)v.z / dm),
+                                 (float)((double)v.w / dm))
+                   : v;
+    }
+  } else {
+    for (int i = tid; i < L; i += 256) {
+      const float v = sample_at(y, n, p + i);
+      out[o + i] = norm ? (float)((double)v / dm) : v;
+    }
   }
 }
 
@@ -781,7 +863,7 @@ hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y,
   if (c1 <= c0) return hipSuccess;
   double A = 1.0;
   for (int i = 0; i < amod::kL; ++i) A *= amod::kAlpha;
-  hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)(c1 - c0)), dim3(256), 0, s, x, nx, apow, scr, c0);
+  hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)((c1 - c0 + 3) / 4)), dim3(256), 0, s, x, nx, apow, scr, c0, c1);
   static const int warm_chunks = [] {
     const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
     return e ? std::max(0, atoi(e)) : amod::kWarmDefault;

@@ -32,10 +32,13 @@
 #define NAPI_VERSION 4
 #include <node_api.h>
 
+#include <execinfo.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "amodem.h"
 
@@ -158,12 +161,61 @@ static amod_group *get_group(napi_env env, int32_t ndev) {
   return g_group[ndev];
 }
 
+/* A resident batch holds GPU memory, so it is released explicitly (DeviceBatch.free() ->
+   residentFree), or at the environment's cleanup, and its JS handle is a plain number,
+   not a napi external: Node 12 gives every external a self-deleting weak reference, even
+   without a finalizer, and a GC at exit ran its second-pass phantom callback after the
+   environment was torn down (SIGSEGV inside libnode after the script's output,
+   tools/node_c4.py). busy counts decodes in flight: a free() during one takes effect
+   when the last completes. Main thread only. */
+typedef struct resident_box {
+  amod_resident *r;
+  int32_t nframes, max_len;
+  int32_t busy, free_pending;
+  int64_t id;
+  struct resident_box *next;
+} resident_box;
+static resident_box *g_boxes = NULL; /* the live boxes of this environment */
+static int64_t g_box_next = 1;
+
+static resident_box *resident_find(napi_env env, napi_value h) {
+  int64_t id = 0;
+  if (napi_get_value_int64(env, h, &id) != napi_ok) return NULL;
+  for (resident_box *b = g_boxes; b; b = b->next)
+    if (b->id == id) return b;
+  return NULL;
+}
+static void resident_release(resident_box *b) {
+  if (b->busy) {
+    b->free_pending = 1;
+    return;
+  }
+  amod_resident_free(b->r);
+  for (resident_box **pp = &g_boxes; *pp; pp = &(*pp)->next)
+    if (*pp == b) {
+      *pp = b->next;
+      break;
+    }
+  free(b);
+}
+static void resident_cleanup(void *arg) {
+  (void)arg;
+  while (g_boxes) {
+    resident_box *b = g_boxes;
+    g_boxes = b->next;
+    amod_resident_free(b->r);
+    free(b);
+  }
+}
+
+
 /* ------------------------------------------------------------------ decode */
 typedef struct {
   amod_ctx *ctx;
   amod_cfg cfg;
   amod_group *group; /* decodeBatch(..., {devices: n > 1}): the batch split across n GPUs */
   amod_resident *resident; /* residentDecodeAsync: a batch already resident on the GPUs */
+  struct resident_box *box; /* (its box: busy while this decode runs) */
   int32_t mode, nframes;
   uint32_t options;
   const float *samples;
@@ -341,6 +393,7 @@ static void async_complete(napi_env env, napi_status status, void *data) {
   napi_delete_reference(env, j->res_ref);
   napi_delete_reference(env, j->pay_ref);
   napi_delete_async_work(env, j->work);
+  if (j->box && --j->box->busy == 0 && j->box->free_pending) resident_release(j->box);
   free_job(j);
   free(j);
 }
@@ -371,19 +424,6 @@ static napi_value js_decode_async(napi_env env, napi_callback_info info) {
 }
 
 /* ------------------------------------------------------- resident batches */
-typedef struct {
-  amod_resident *r;
-  int32_t nframes, max_len;
-} resident_box;
-
-static void resident_finalize(napi_env env, void *data, void *hint) {
-  (void)env;
-  (void)hint;
-  resident_box *b = (resident_box *)data;
-  amod_resident_free(b->r);
-  free(b);
-}
-
 static napi_value js_resident_upload(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
@@ -426,11 +466,16 @@ static napi_value js_resident_upload(napi_env env, napi_callback_info info) {
   }
   b->nframes = (int32_t)no;
   b->max_len = max_len;
-  napi_value out, h, v, arr;
-  if (napi_create_external(env, b, resident_finalize, NULL, &h) != napi_ok) {
-    resident_finalize(env, b, NULL);
-    return throw_msg(env, "napi_create_external failed");
+  static int hooked = 0;
+  if (!hooked) {
+    napi_add_env_cleanup_hook(env, resident_cleanup, NULL);
+    hooked = 1;
   }
+  b->id = g_box_next++;
+  b->next = g_boxes;
+  g_boxes = b;
+  napi_value out, h, v, arr;
+  NAPI_TRY(env, napi_create_int64(env, b->id, &h));
   NAPI_TRY(env, napi_create_object(env, &out));
   NAPI_TRY(env, napi_set_named_property(env, out, "handle", h));
   NAPI_TRY(env, napi_create_int32(env, b->nframes, &v));
@@ -453,9 +498,8 @@ static napi_value js_resident_decode_async(napi_env env, napi_callback_info info
   napi_value argv[4];
   if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 4)
     return napi_throw_type_error(env, NULL, "residentDecodeAsync(handle, cfg, mode, options)"), NULL;
-  resident_box *b = NULL;
-  if (napi_get_value_external(env, argv[0], (void **)&b) != napi_ok || !b || !b->r)
-    return napi_throw_type_error(env, NULL, "handle must come from residentUpload"), NULL;
+  resident_box *b = resident_find(env, argv[0]);
+  if (!b || b->free_pending) return throw_msg(env, "the resident batch was freed (or never uploaded)");
   decode_job *j = (decode_job *)calloc(1, sizeof *j);
   if (!j) return throw_msg(env, "out of memory");
   if (!to_cfg(env, argv[1], &j->cfg)) {
@@ -468,6 +512,8 @@ static napi_value js_resident_decode_async(napi_env env, napi_callback_info info
   }
   if (napi_get_value_uint32(env, argv[3], &j->options) != napi_ok) j->options = 0;
   j->resident = b->r;
+  j->box = b;
+  ++b->busy;
   j->nframes = b->nframes;
   j->stride = amod_payload_stride(&j->cfg, b->max_len);
   if (napi_create_arraybuffer(env, (size_t)j->nframes * sizeof(amod_result), &j->results, &j->res_ab) != napi_ok ||
@@ -485,6 +531,17 @@ static napi_value js_resident_decode_async(napi_env env, napi_callback_info info
   NAPI_TRY(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
   NAPI_TRY(env, napi_queue_async_work(env, j->work));
   return promise;
+}
+
+/* residentFree(handle): the batch's GPU memory released now (after a decode in flight) */
+static napi_value js_resident_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 1)
+    return napi_throw_type_error(env, NULL, "residentFree(handle from residentUpload)"), NULL;
+  resident_box *b = resident_find(env, argv[0]);
+  if (b && !b->free_pending) resident_release(b); /* (a second free() is a no-op) */
+  return NULL;
 }
 
 /* loopback(samples: Float32Array, cfg, device?) -> { status, preambleIdx, fineMetric,
@@ -979,12 +1036,29 @@ static napi_value js_live_state(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* diagnostics (AMODEM_SEGV_TRACE=1): a crash prints the native stack (library + offset per
+   frame, for addr2line) before the default action */
+static void segv_trace(int sig) {
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  static const char msg[] = "[amodem.node] fatal signal, native stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static napi_value init(napi_env env, napi_value exports) {
+  if (getenv("AMODEM_SEGV_TRACE")) {
+    signal(SIGSEGV, segv_trace);
+    signal(SIGBUS, segv_trace);
+  }
   const napi_property_descriptor props[] = {
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decodeAsync", NULL, js_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"residentUpload", NULL, js_resident_upload, NULL, NULL, NULL, napi_enumerable, NULL},
       {"residentDecodeAsync", NULL, js_resident_decode_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"residentFree", NULL, js_resident_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"loopback", NULL, js_loopback, NULL, NULL, NULL, napi_enumerable, NULL},
       {"crc32", NULL, js_crc32, NULL, NULL, NULL, napi_enumerable, NULL},
       {"preamble1", NULL, js_preamble1, NULL, NULL, NULL, napi_enumerable, NULL},

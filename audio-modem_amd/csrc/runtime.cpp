@@ -347,9 +347,9 @@ int validate(const amod_cfg *c) {
 
 int build_crc(amod_ctx *ctx) {
   if (ctx->crc.p) return AMOD_SUCCESS;
-  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024 + amod::kCrcMats * 32 + 16);
+  std::vector<uint32_t> h(4 * 256 + 32 * 1024 + 32 * 1024 + 1024 + amod::kCrcMats * 32 + 16 + 16 * 32);
   uint32_t *s4 = h.data(), *m1 = s4 + 1024, *m2 = m1 + 32 * 1024, *mb = m2 + 32 * 1024, *mat = mb + 1024;
-  uint32_t *pre = mat + amod::kCrcMats * 32;
+  uint32_t *pre = mat + amod::kCrcMats * 32, *unpad = pre + 16;
   const uint32_t *t0 = crc_table();
   for (int i = 0; i < 256; ++i) s4[i] = t0[i];
   for (int k = 1; k < 4; ++k)
@@ -377,6 +377,16 @@ int build_crc(amod_ctx *ctx) {
       pre[k] = r;
       const uint32_t x = inv_top[r >> 24];
       r = ((r ^ crc_table()[x]) << 8) | x;
+    }
+    // unpad[k]: the inverse of k zero bytes as a GF(2) matrix (column b = the register that
+    // k zero bytes advance to 1 << b), for k_demod's left-aligned CRC chunks
+    for (int b = 0; b < 32; ++b) {
+      uint32_t u = 1u << b;
+      for (int k = 0; k < 16; ++k) {
+        unpad[32 * k + b] = u;
+        const uint32_t x = inv_top[u >> 24];
+        u = ((u ^ crc_table()[x]) << 8) | x;
+      }
     }
   }
   HIP_TRY(ctx->crc.ensure(h.size() * 4));
@@ -478,6 +488,7 @@ int get_tables(amod_ctx *ctx, const amod_cfg *c, amod::DevCfg &out) {
     d.t.crc_mb = crc + 1024 + 64 * 1024;
     d.t.crc_mat = crc + 1024 + 64 * 1024 + 1024;
     d.t.crc_pre = d.t.crc_mat + amod::kCrcMats * 32;
+    d.t.crc_unpad = d.t.crc_pre + 16;
     it = ctx->tables.emplace(key, std::move(ts)).first;
   }
   out = it->second->cfg;

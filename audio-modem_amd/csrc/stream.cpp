@@ -708,6 +708,7 @@ struct StreamCache {
   Pinned w_res_h[kSets], w_pay_h[kSets];    // window decoder: results and payload rows (pinned D2H)
   // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
   std::vector<uint8_t> sp_need;
+  std::vector<std::pair<int64_t, int64_t>> sp_reg; // (kept: its pages stay faulted in across calls)
   std::vector<int32_t> sp_cidx;
   std::unique_ptr<std::atomic<const float *>[]> sp_gptr;
   size_t sp_gcap = 0;
@@ -913,6 +914,8 @@ struct Prepass {
     first_g = p0_end >> kGranLog;
     std::vector<uint8_t> &need = c->sp_need;
     need.assign((size_t)ng, 0);
+    double tm_assign = 0, tm_reg = 0;
+    tick(tm_assign);
     // need[g]: 1 = read by the state machine, 2 = read first (a speculative segment's or the
     // true run's first scan: packed at the front, so each thread waits for one piece only)
     uint8_t mark_val = 1;
@@ -923,7 +926,10 @@ struct Prepass {
         need[(size_t)g] = std::max(need[(size_t)g], mark_val);
     };
     // hot regions (local), blocks less than 2 K samples apart merged
-    std::vector<std::pair<int64_t, int64_t>> reg;
+    // (a fresh 512 KB vector here took 2.4 ms of first-touch faults on the 32k-chunk stream
+    // while the runtime's copy threads fault in the host mirror)
+    std::vector<std::pair<int64_t, int64_t>> &reg = c->sp_reg;
+    reg.clear();
     reg.reserve(ft.first.size());
     if (gap_launched) { // (the fine ranges: hot blocks +- 448 samples, merged)
       for (size_t r = 0; r < ft.first.size(); ++r) reg.push_back({ft.first[r] - lo + 448, ft.first[r] - lo + ft.count[r] - 448});
@@ -940,6 +946,7 @@ struct Prepass {
         else reg.push_back({32 * b, 32 * b + 32});
       }
     }
+    tick(tm_reg);
     const int32_t maxp = start.meta_received ? (start.chunk_size ? start.chunk_size : 4096) + 11 : 280;
     const int64_t F = amod_estimate_frame_samples(cfg, maxp);
     const int64_t R = 3 * (int64_t)cfg->cp_len + cfg->symbol_len + 64; // refine radius + correlation
@@ -963,6 +970,10 @@ struct Prepass {
     const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, span / 64));
     for (int k = 1; k < T; ++k) scan_from((start.block + span * k / T) * kBlock - 511 - lo - 1024);
     tick(setup_ms[0]);
+    if (kn->stream_diag)
+      fprintf(stderr, "[stream] marks: assign %.3f ms, regions %.3f ms (%zu), marks %.3f ms\n", tm_assign, tm_reg,
+              reg.size(), setup_ms[0]);
+    setup_ms[0] += tm_assign + tm_reg;
     std::vector<int32_t> src;
     c->sp_cidx.assign((size_t)ng, -1);
     cidx = c->sp_cidx.data();

@@ -364,7 +364,7 @@ function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
 
 // A batch made resident on GPUs 0 .. devices-1 once (amod_group_upload: contiguous frame
 // ranges of about equal sample counts), for decodeBatch to decode from HBM as often as
-// needed (a Node host driving several GPUs without one upload per decode).
+// needed (a Node host driving several GPUs without one upload per decode); free() when done.
 class DeviceBatch {
   constructor(up, devices) {
     this.handle = up.handle;
@@ -372,6 +372,12 @@ class DeviceBatch {
     this.maxLen = up.maxLen;
     this.devices = devices;
     this.framesPerDevice = up.framesPerDevice;
+  }
+
+  // releases the batch's GPU memory (after a decode still in flight); otherwise it is
+  // released when the Node environment exits, not by the garbage collector
+  free() {
+    native.residentFree(this.handle);
   }
 }
 

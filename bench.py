@@ -568,7 +568,7 @@ def host_api_leg(env: Env, wl: Workload, reps=3):
                 nj["samples_per_s"] = wl.ndecoded / (nj["ms"] / 1e3)
                 out["node_decode_batch"] = nj
             else:
-                out["node_decode_batch"] = {"error": r.stderr[-400:]}
+                out["node_decode_batch"] = {"error": r.stderr[-3000:], "returncode": r.returncode}
     return out
 
 

@@ -60,8 +60,14 @@ async function main() {
           // uploadBatch once, decodeBatch(DeviceBatch) twice: both from HBM
           const b = M.uploadBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { devices: j.devices });
           const r1 = await M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode });
-          const r2 = await M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode });
-          r = { first: r1, second: r2, framesPerDevice: b.framesPerDevice, isDeviceBatch: b instanceof M.DeviceBatch };
+          // free() while a decode is in flight: that decode completes, later ones reject
+          const p2 = M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode });
+          b.free();
+          const r2 = await p2;
+          let afterFree = null;
+          try { M.decodeBatch(b, null, null, j.mod, j.rep, { mode: j.mode }); } catch (e) { afterFree = String(e.message || e); }
+          r = { first: r1, second: r2, framesPerDevice: b.framesPerDevice, isDeviceBatch: b instanceof M.DeviceBatch,
+            afterFree };
           break;
         }
         case 'asm': {

@@ -226,7 +226,8 @@ def test_resident_batch_through_js(tmp_path):
     got = ok(res, "r")
     want = [f["result"] for f in sel]
     assert got["isDeviceBatch"] and sum(got["framesPerDevice"]) == len(sel)
-    assert got["first"] == want and got["second"] == want
+    assert got["first"] == want and got["second"] == want  # (the second with free() called while in flight)
+    assert got["afterFree"] and "freed" in got["afterFree"]
 
 
 def _lb_num(v):

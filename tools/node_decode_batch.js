@@ -37,7 +37,9 @@ function readF32(file) {
 
 async function main() {
   const spec = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+  const say = (m) => process.stderr.write(`[node_decode_batch] ${m}\n`); // (progress: a crash names its step)
   const x = readF32(spec.samples);
+  say(`read ${x.length} samples`);
   const offs = Float64Array.from(spec.offsets), lens = Int32Array.from(spec.lengths);
   modem.setOFDMConfig(spec.preset);
   const opts = { device: spec.device | 0, devices: 1, mode: spec.chunk ? 'chunk' : 'received' };
@@ -45,6 +47,7 @@ async function main() {
   const med = (a) => a.slice().sort((p, q) => p - q)[a.length >> 1];
   const whole = [], nat = [];
   let res = null;
+  say('decodeBatch');
   for (let r = 0; r <= reps; r++) {
     const t0 = process.hrtime.bigint();
     res = await modem.decodeBatch(x, offs, lens, spec.mod, spec.rep, opts);
@@ -57,6 +60,7 @@ async function main() {
     sub_start: modem.OFDM.SUB_START, sub_end: modem.OFDM.SUB_END, pilots: modem.OFDM.PILOTS.slice(),
     modulation: { BPSK: 0, QPSK: 1, QAM16: 2 }[spec.mod], repetition: spec.rep,
   };
+  say('native.decodeAsync');
   for (let r = 0; r <= reps; r++) {
     const t0 = process.hrtime.bigint();
     await modem.native.decodeAsync(x, offs, lens, cfg, spec.chunk ? 1 : 0, 0, spec.device | 0, 1);
@@ -65,9 +69,11 @@ async function main() {
   }
   // the batch made resident once (uploadBatch), then decodeBatch(DeviceBatch) from HBM:
   // launches, the D2H of records + payload rows and the result objects, no upload
+  say('uploadBatch');
   const t0u = process.hrtime.bigint();
   const dbatch = modem.uploadBatch(x, offs, lens, spec.mod, spec.rep, { devices: 1 });
   const upload_ms = Number(process.hrtime.bigint() - t0u) / 1e6;
+  say('decodeBatch(DeviceBatch)');
   const resd = [];
   let rres = null;
   for (let r = 0; r <= reps; r++) {
@@ -76,6 +82,7 @@ async function main() {
     const t1 = process.hrtime.bigint();
     if (r) resd.push(Number(t1 - t0) / 1e6);
   }
+  dbatch.free();
   const ok = res.filter((r) => r.crcValid === true).length;
   process.stdout.write(JSON.stringify({
     what: `decodeBatch(${lens.length} frames) from node ${process.version}: host Float32Array -> N-API -> ` +
