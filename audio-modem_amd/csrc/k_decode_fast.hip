@@ -1569,13 +1569,19 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   uint32_t *const voted = bits + w.vote_off;
   float2 *const X2 = xch[wave];
   const float2 *const tw1 = twl - 64, *const tw2 = twl + 7 * 64;
-  // per-lane band facts for its 4 subcarriers b = lane + 64 rr: the bit offset of its
-  // decision in a symbol, di * BPS (-1 pilot, -2 none; di = data index)
+  // per-lane band facts for its 4 subcarriers b = bo + 64 rr, bo = (lane - sub_start) mod
+  // 64: the bin k = sub_start + b of slot 0 is congruent to the lane mod 64, so each 16-
+  // or 32-lane group of a band read covers whole aligned residue blocks of the spectrum
+  // (conflict-free under spec_idx; lane l on subcarrier l had every group 2-way, in both
+  // halves Z[k] and Z[512 - k]: 16 of k_demod's ~40 conflict cycles per job on C4); the
+  // mirrored half stays 2-way in one lane pair per group. The bit offset of its decision
+  // in a symbol, di * BPS (-1 pilot, -2 none; di = data index)
   // (two 16-bit fields per register: registers bound k_demod's occupancy)
+  const int bo0 = (lane - sub_start) & 63;
   uint32_t di_pk[2] = {0u, 0u};
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
-    const int di = lane + 64 * rr < nband ? (int)cfg.t.band_di[lane + 64 * rr] : -2;
+    const int di = bo0 + 64 * rr < nband ? (int)cfg.t.band_di[bo0 + 64 * rr] : -2;
     const int dib = di >= 0 ? di * BPS : di;
     di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
   }
@@ -1589,7 +1595,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   const bool pil_multi = __ballot(npl > 1) != 0;
   uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(lane + 64 * rr < nband && cfg.t.known[lane + 64 * rr] < 0.f) << rr;
+  for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(bo0 + 64 * rr < nband && cfg.t.known[bo0 + 64 * rr] < 0.f) << rr;
 
   // Frames (last-first: frame f1 - 1 - k for the k-th) by a static stride for the first
   // rounds, then one at a time from the claim counter (w.claim). Waves on one SIMD do not
@@ -1755,9 +1761,10 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       // per-job copies of the lane's slot facts: their comparisons are made where they are
       // used instead of held as lane masks across the loop (SGPR pairs that spill)
       asm volatile("" : "+v"(prr), "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg));
-      // the band: slot rr of lane ln is subcarrier b = ln + 64 rr, bins k = k0 + 64 rr and
+      // the band: slot rr of lane ln is subcarrier b = bo + 64 rr, bins k = k0 + 64 rr and
       // 512 - k (spec_idx(n +- 64) = spec_idx(n) +- 64: one base per side, immediate offsets)
-      const int k0 = sub_start + ln;
+      const int bo = (ln - sub_start) & 63; // (recomputed per job: no VGPR held across the loop)
+      const int k0 = sub_start + bo;
       const f2v *const zkp = reinterpret_cast<const f2v *>(X2 + spec_idx(k0));
       const f2v *const znp = reinterpret_cast<const f2v *>(X2 + spec_idx(kFft - 192 - k0));
       float zm = 0.f;
@@ -1777,7 +1784,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         if (rr == 0 && chunk_mode && !KO(8) && __ballot(!isfinite(zk.x + zk.y + zn.x + zn.y)))
           wflags |= AMOD_FLAG_NONFINITE;
         if (rr == NS - 1) { // the last slot may be partly filled
-          const bool in = ln + 64 * rr < nband;
+          const bool in = bo + 64 * rr < nband;
           a = in ? a : f2v{0.f, 0.f};
           c = in ? c : f2v{0.f, 0.f};
           zz = in ? zz : 0.f;
@@ -1792,7 +1799,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         int ch = 0;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int b = ln + 64 * rr;
+          const int b = bo + 64 * rr;
           const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
           const float2 h = const1 ? make_float2(0.f, 0.f) : make_float2(x1[rr].x * kn, x1[rr].y * kn);
           const float m2 = h.x * h.x + h.y * h.y;
@@ -1818,7 +1825,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         e1[rr] = pk_cmul(x1[rr], g);
         e2[rr] = pk_cmul(x2[rr], g);
         em = fmaxf(em, fmaxf(fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y)));
-        const int b = ln + 64 * rr;
+        const int b = bo + 64 * rr;
         if (DBG && b < nband && (s1 == 0 || s2 == 0)) {
           const bool one = s1 == 0;
           const f2v xx = one ? x1[rr] : x2[rr], ee = one ? e1[rr] : e2[rr];
