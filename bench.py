@@ -272,11 +272,33 @@ class Workload:
                               self.F, self.d_res.data_ptr(), self.d_pay.data_ptr(), self.stride, stream=self.stream,
                               options=options)
 
+    def enable_pipeline(self):
+        """Consecutive batches over two contexts (each its own workspace, result buffers and
+        stream): batch i + 1's k_detect runs while batch i's k_demod finishes, so the two
+        kernels' tails and the dependent-launch gaps overlap (tools/pipeline_ab.py: C2
+        0.455 -> 0.425 ms per step, C5 1.60 -> 1.47; C4, one k_demod launch, no gain)."""
+        torch, amodem = self.env.torch, self.env.amodem
+        self.dm2 = amodem.Demodulator(self.env.local)
+        self.dm2.reserve(self.cfg, self.F, int(self.dlens.max()))
+        self.d_res2 = torch.zeros_like(self.d_res)
+        self.d_pay2 = torch.zeros_like(self.d_pay)
+        self.pstreams = [torch.cuda.Stream(self.env.dev), torch.cuda.Stream(self.env.dev)]
+        self.pi = 0
+
+    def step_pipelined(self):
+        k, self.pi = self.pi, self.pi ^ 1
+        dm, res, pay = (self.dm, self.d_res, self.d_pay) if k == 0 else (self.dm2, self.d_res2, self.d_pay2)
+        dm.decode_device(self.cfg, self.mode, self.xs.data_ptr(), self.d_doff.data_ptr(), self.d_dlen.data_ptr(),
+                         self.F, res.data_ptr(), pay.data_ptr(), self.stride, stream=self.pstreams[k].cuda_stream)
+
     def records(self):
         return np.frombuffer(self.d_res.cpu().numpy().tobytes(), self.env.amodem.RESULT_DTYPE)
 
     def close(self):
         self.dm.close()
+        if getattr(self, "dm2", None) is not None:
+            self.dm2.close()
+            self.dm2 = self.d_res2 = self.d_pay2 = None
         self.xs = self.d_res = self.d_pay = self.d_doff = self.d_dlen = None
         self.env.torch.cuda.empty_cache()
 
@@ -299,19 +321,43 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     Returns the leg's measurement dict (rank 0) and the last step's records."""
     torch, lib = env.torch, env.lib
     dev = env.dev
-    warm = warm_up(wl.step, lambda: torch.cuda.synchronize(dev), warmup)
-    lib.amod_set_profiling(wl.dm.ctx, 1)
+    # received mode: consecutive batches pipelined over two contexts (Workload.enable_pipeline);
+    # chunk mode (one k_demod launch a step) and AMOD_BENCH_PIPELINE=0: one context
+    pipe = not wl.chunk and os.environ.get("AMOD_BENCH_PIPELINE", "1") != "0"
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    serial = None
+    if pipe:
+        # first the per-kernel times (rooflines, chain) from K steps on one context alone, so
+        # no launch shares the GPU with the next batch's (its wall time is reported too),
+        # then the timed K steps pipelined over two contexts
+        wl.enable_pipeline()
+        warm_up(wl.step, sync, warmup)
+        lib.amod_set_profiling(wl.dm.ctx, 1)
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            wl.step()
+        sync()
+        serial = env.max_over_ranks(time.perf_counter() - t1)
+        lib.amod_set_profiling(wl.dm.ctx, 0)
+    step = wl.step_pipelined if pipe else wl.step
+    warm = warm_up(step, sync, warmup, min_s=0.3 if pipe else 0.5)
+    if not pipe:
+        lib.amod_set_profiling(wl.dm.ctx, 1)
     env.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        wl.step()
-    torch.cuda.synchronize(dev)
+        step()
+    sync()
     env.barrier()
     elapsed = time.perf_counter() - t0
+    if pipe:  # both contexts decoded the same batch: the same records and payload bytes
+        assert wl.d_res2.cpu().numpy().tobytes() == wl.d_res.cpu().numpy().tobytes() and \
+            np.array_equal(wl.d_pay2.cpu().numpy(), wl.d_pay.cpu().numpy()), "pipelined contexts disagree"
     L = env.L
     kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
-    lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))
+    lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))  # (the profiled steps)
     lib.amod_set_profiling(wl.dm.ctx, 0)
     ov_l, ov_b, ov_lead = C.c_int64(), C.c_int64(), C.c_double()
     lib.amod_aux_overlap(wl.dm.ctx, C.byref(ov_l), C.byref(ov_b), C.byref(ov_lead))
@@ -363,6 +409,12 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     out = {
         "value": value, "unit": "samples/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "warmup_run": warm, "ms_per_step": elapsed / steps * 1e3,
+        "pipeline": {"contexts": 2 if pipe else 1,
+                     "what": "consecutive batches alternate between two contexts (own workspace, results and "
+                             "stream): batch i+1's k_detect overlaps batch i's k_demod; rooflines and chain from "
+                             "the same K steps on one context alone" if pipe else "one context, one stream",
+                     "one_context_ms_per_step": (serial / steps * 1e3) if serial else elapsed / steps * 1e3,
+                     "one_context_samples_per_s": wl.ndecoded * world * steps / (serial if serial else elapsed)},
         "payload_MB_per_s": wl.payload_bytes * wl.F * world * steps / elapsed / 1e6,
         "config": {"workload": wl.workload_text(), "frames_per_gpu": wl.F, "samples_per_frame": int(wl.dlens[0]),
                    "fft": 512, "modulation": wl.mod, "payload_bytes": wl.payload_bytes,
@@ -401,7 +453,7 @@ def traffic_for(wl, kernel):
             tj = json.load(f)
         for entry in tj if isinstance(tj, list) else [tj]:
             kt = entry.get("kernels", {}).get(kernel)
-            if entry.get("frames") == wl.F and entry.get("samples_per_frame") == wl.spf and kt:
+            if entry.get("frames") == wl.F and entry.get("samples_per_frame") == int(wl.dlens[0]) and kt:
                 return (kt["read_bytes"] + kt["write_bytes"]) / kt.get("dispatches_per_step", 1.0)
     return None
 
