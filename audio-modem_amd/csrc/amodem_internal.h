@@ -27,9 +27,8 @@ constexpr int kMaxBand = 256;  // sub_end < fft/2
 constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
 constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
-constexpr int kCrcMats = 512;
-constexpr int kTlHead = 4;
-     // DevWork::tl: marks before the per-wave k_demod end stamps  // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+constexpr int kCrcMats = 512; // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+constexpr int kTlHead = 4;    // DevWork::tl: marks before the per-wave k_demod end stamps
 
 // Device-resident tables, built once per configuration by the runtime.
 struct DevTables {
@@ -45,8 +44,8 @@ struct DevTables {
   const uint32_t *crc_mb;  // [4][256] shift-by-4096 operator (pass to pass)
   const uint32_t *crc_mat; // [kCrcMats][32] shift-by-(16*q) zero-byte operators as GF(2) matrices (column i = image of bit i)
   const uint32_t *crc_pre; // [16] register k zero bytes before the message start that becomes ~0 there
-  const uint32_t *crc_unpad; // [16][32] inverse k-zero-byte operators (same layout as crc_mat)
                            // (the inverse k-byte shift of ~0): chunk 0 left-padded to 16 bytes
+  const uint32_t *crc_unpad; // [16][32] inverse k-zero-byte operators (same layout as crc_mat)
   const double2 *points;   // [16] constellation points of cfg.mod (initConstellation)
   const double2 *tw_inv;   // [511] inverse-transform recurrence twiddles (fftIterative, ifft)
   const float *tmpl;       // [3][symbol_len] pre1, pre2, CE symbols (f32, before normalisation)

@@ -1567,7 +1567,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // the wave's bit stream (and voted stream) in dynamic LDS
   uint32_t *const bits = LDS_U + wave * w.stream_words;
   uint32_t *const voted = bits + w.vote_off;
-  float2 *const X2 = xch[wave];
+  // the wave's exchange buffer, its base held in a VGPR: as a scalar it was one of the
+  // values the full SGPR file spilled to a VGPR lane and read back (v_readlane, VALU) five
+  // times a job
+  int xoff = wave * XCH_F2;
+  asm volatile("" : "+v"(xoff));
+  float2 *const X2 = &xch[0][0] + xoff;
   const float2 *const tw1 = twl - 64, *const tw2 = twl + 7 * 64;
   // per-lane band facts for its 4 subcarriers b = bo + 64 rr, bo = (lane - sub_start) mod
   // 64: the bin k = sub_start + b of slot 0 is congruent to the lane mod 64, so each 16-

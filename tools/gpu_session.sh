@@ -1,7 +1,4 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-for c in ${CONFS:-c2 c4}; do
-  extra=""; [ "$c" = c5 ] && extra="--snr 10"
-  echo "== profile $c"; bash tools/profile_round.sh gpurun_out/r04/$c $c $extra || exit $?
-  ls gpurun_out/r04/$c
-done
+AB_ROUNDS=16 AB_CONFS=${CONFS:-c2,c4,c5} timeout -k 10 170 python -u tools/aux_ab.py d: bal:AMOD_DEMOD_BALANCE=1 > gpurun_out/bal.log 2>&1 || exit $?
+grep "^c" gpurun_out/bal.log
