@@ -285,11 +285,15 @@ class Workload:
         self.pstreams = [torch.cuda.Stream(self.env.dev), torch.cuda.Stream(self.env.dev)]
         self.pi = 0
 
-    def step_pipelined(self):
-        k, self.pi = self.pi, self.pi ^ 1
+    def step_ctx(self, k, stream):
+        """one decode on context k (0: dm, 1: dm2) into its own result buffers, on `stream`"""
         dm, res, pay = (self.dm, self.d_res, self.d_pay) if k == 0 else (self.dm2, self.d_res2, self.d_pay2)
         dm.decode_device(self.cfg, self.mode, self.xs.data_ptr(), self.d_doff.data_ptr(), self.d_dlen.data_ptr(),
-                         self.F, res.data_ptr(), pay.data_ptr(), self.stride, stream=self.pstreams[k].cuda_stream)
+                         self.F, res.data_ptr(), pay.data_ptr(), self.stride, stream=stream)
+
+    def step_pipelined(self):
+        k, self.pi = self.pi, self.pi ^ 1
+        self.step_ctx(k, self.pstreams[k].cuda_stream)
 
     def records(self):
         return np.frombuffer(self.d_res.cpu().numpy().tobytes(), self.env.amodem.RESULT_DTYPE)
@@ -824,41 +828,54 @@ def cpu_legs(wl: Workload, rec, js_frames, js_seconds=1.5):
 # --------------------------------------------------------------------- main --
 def graph_leg(env: Env, wl: Workload, steps: int):
     """The same decode captured once into a hipGraph (amod_reserve was called; include/
-    amodem.h) and replayed `steps` times on the launch stream: the step time without the
-    per-launch host work (the dependent kernels' GPU-side gaps remain). After the timed
-    replays one replay's records are checked like the eager steps'. Runs right after the
-    eager steps, warmed up the same way (the capture stream is the graph's own)."""
+    amodem.h) and replayed `steps` times: the step time without the per-launch host work
+    (the dependent kernels' GPU-side gaps remain), on one context: compare it with
+    pipeline.one_context_ms_per_step. (AMOD_BENCH_GRAPH_PIPE=1 captures each context's
+    decode into its own graph and alternates the replays over the two streams, as the
+    eager steps do: 0.456 ms per C2 step against 0.441 on one context and 0.425 eager
+    pipelined. This runtime ran the two graphs' replays one after the other.) After the
+    timed replays one replay's records are checked like the eager steps'."""
     torch = env.torch
     try:
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(env.dev)
+        nctx = 2 if getattr(wl, "dm2", None) is not None and os.environ.get("AMOD_BENCH_GRAPH_PIPE") == "1" else 1
+        graphs, streams = [], []
         torch.cuda.synchronize(env.dev)
-        with torch.cuda.stream(s):
-            stream0 = wl.stream
-            wl.stream = s.cuda_stream
-            try:
-                wl.step()  # (one eager decode on the capture stream first)
+        for k in range(nctx):
+            g, s = torch.cuda.CUDAGraph(), torch.cuda.Stream(env.dev)
+            with torch.cuda.stream(s):
+                wl.step_ctx(k, s.cuda_stream)  # (one eager decode on the capture stream first)
                 s.synchronize()
                 with torch.cuda.graph(g, stream=s):
-                    wl.step()
-            finally:
-                wl.stream = stream0
+                    wl.step_ctx(k, s.cuda_stream)
+            graphs.append(g)
+            streams.append(s)
         torch.cuda.synchronize(env.dev)
-        warm_up(g.replay, lambda: torch.cuda.synchronize(env.dev), 5)  # (clocks, as for the eager steps)
+        it = [0]
+
+        def replay():
+            k = it[0] % nctx
+            it[0] += 1
+            with torch.cuda.stream(streams[k]):
+                graphs[k].replay()
+
+        warm_up(replay, lambda: torch.cuda.synchronize(env.dev), 5)  # (clocks, as for the eager steps)
         torch.cuda.synchronize(env.dev)
         t0 = time.perf_counter()
         for _ in range(steps):
-            g.replay()
+            replay()
         torch.cuda.synchronize(env.dev)
         dt = (time.perf_counter() - t0) / steps
         wl.d_res.zero_()
-        g.replay()
+        with torch.cuda.stream(streams[0]):
+            graphs[0].replay()
         torch.cuda.synchronize(env.dev)
         rec = wl.records()
         ok = int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum())
-        return {"what": "the primary decode captured into a hipGraph, replayed (host launch work removed; "
-                        "the kernels' GPU-side dependency gaps remain)",
-                "ms_per_step": dt * 1e3, "samples_per_s": wl.ndecoded / dt, "frames_ok": ok, "steps": steps}
+        return {"what": "the decode captured into a hipGraph per context (%d), replays alternating over the "
+                        "contexts' streams as the eager steps do (host launch work removed; the kernels' GPU-side "
+                        "dependency gaps remain)" % nctx,
+                "ms_per_step": dt * 1e3, "samples_per_s": wl.ndecoded / dt, "frames_ok": ok, "steps": steps,
+                "contexts": nctx}
     except Exception as e:  # (reported, never fatal: the eager line above is the metric)
         return {"error": repr(e)[:300]}
 
