@@ -755,18 +755,115 @@ static napi_value js_abi(napi_env env, napi_callback_info info) {
 
 
 /* ----------------------------------------------- chunk assembler / stream receive */
-static void asm_finalize(napi_env env, void *data, void *hint) {
-  (void)env; (void)hint;
-  amod_asm_close((amod_assembler *)data);
+/* Assemblers and live receivers get numeric handles for the reason resident batches do
+   (no napi externals: their weak references crash Node 12 at exit). Each is released by
+   close() or at the environment's cleanup, live receivers before assemblers. A live
+   receiver uses its assembler: closing the assembler first takes effect when the last
+   receiver on it closes. Main thread only. */
+enum { OBJ_ASM = 1, OBJ_LIVE = 2 };
+typedef struct obj_box {
+  int32_t kind;
+  int32_t users;        /* OBJ_ASM: live receivers open on it */
+  int32_t close_pending;
+  int64_t id;
+  void *p;
+  struct obj_box *dep;  /* OBJ_LIVE: its assembler's box */
+  struct obj_box *next;
+} obj_box;
+static obj_box *g_objs = NULL;
+static int64_t g_obj_next = 1;
+
+static void obj_unlink_free(obj_box *b) {
+  for (obj_box **pp = &g_objs; *pp; pp = &(*pp)->next)
+    if (*pp == b) {
+      *pp = b->next;
+      break;
+    }
+  free(b);
+}
+static void obj_release(obj_box *b) {
+  if (b->kind == OBJ_ASM) {
+    if (b->users) {
+      b->close_pending = 1;
+      return;
+    }
+    amod_asm_close((amod_assembler *)b->p);
+    obj_unlink_free(b);
+    return;
+  }
+  amod_live_close((amod_live *)b->p);
+  obj_box *a = b->dep;
+  obj_unlink_free(b);
+  if (a && --a->users == 0 && a->close_pending) obj_release(a);
+}
+static void obj_cleanup(void *arg) {
+  (void)arg;
+  for (int kind = OBJ_LIVE; kind >= OBJ_ASM; --kind) {
+    obj_box **pp = &g_objs;
+    while (*pp) {
+      obj_box *b = *pp;
+      if (b->kind != kind) {
+        pp = &b->next;
+        continue;
+      }
+      *pp = b->next;
+      if (kind == OBJ_LIVE) amod_live_close((amod_live *)b->p);
+      else amod_asm_close((amod_assembler *)b->p);
+      free(b);
+    }
+  }
+}
+static obj_box *obj_find(napi_env env, napi_value h, int32_t kind) {
+  int64_t id = 0;
+  if (napi_get_value_int64(env, h, &id) != napi_ok) return NULL;
+  for (obj_box *b = g_objs; b; b = b->next)
+    if (b->id == id && b->kind == kind && !b->close_pending) return b;
+  return NULL;
+}
+static napi_value obj_new(napi_env env, int32_t kind, void *p, obj_box *dep) {
+  napi_value out;
+  obj_box *b = (obj_box *)calloc(1, sizeof *b);
+  if (!b) return throw_msg(env, "out of memory");
+  if (napi_create_int64(env, g_obj_next, &out) != napi_ok) {
+    free(b);
+    return throw_msg(env, "handle");
+  }
+  static int hooked = 0;
+  if (!hooked) {
+    napi_add_env_cleanup_hook(env, obj_cleanup, NULL);
+    hooked = 1;
+  }
+  b->kind = kind;
+  b->p = p;
+  b->dep = dep;
+  if (dep) ++dep->users;
+  b->id = g_obj_next++;
+  b->next = g_objs;
+  g_objs = b;
+  return out;
 }
 
+static obj_box *get_asm_box(napi_env env, napi_value v) {
+  obj_box *b = obj_find(env, v, OBJ_ASM);
+  if (!b) napi_throw_type_error(env, NULL, "expected an open assembler handle");
+  return b;
+}
 static amod_assembler *get_asm(napi_env env, napi_value v) {
-  void *p = NULL;
-  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
-    napi_throw_type_error(env, NULL, "expected an assembler handle");
-    return NULL;
-  }
-  return (amod_assembler *)p;
+  obj_box *b = get_asm_box(env, v);
+  return b ? (amod_assembler *)b->p : NULL;
+}
+
+/* asmClose(h) / liveClose(h): released now (an assembler: once its receivers close); a
+   second close is a no-op */
+static napi_value js_obj_close(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  void *data = NULL;
+  size_t argc = 1;
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, &data) != napi_ok || argc < 1)
+    return napi_throw_type_error(env, NULL, "close(handle)"), NULL;
+  obj_box *b = obj_find(env, argv[0], (int32_t)(intptr_t)data);
+  if (b) obj_release(b);
+  return NULL;
 }
 
 static napi_value make_i32(napi_env env, int32_t v) {
@@ -775,7 +872,7 @@ static napi_value make_i32(napi_env env, int32_t v) {
   return out;
 }
 
-/* asmOpen(dir | null) -> handle (closed when collected) */
+/* asmOpen(dir | null) -> handle (asmClose(handle), or closed at exit) */
 static napi_value js_asm_open(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return NULL;
@@ -786,8 +883,8 @@ static napi_value js_asm_open(napi_env env, napi_callback_info info) {
   }
   amod_assembler *a;
   if (amod_asm_open(dir[0] ? dir : NULL, &a) != AMOD_SUCCESS) return throw_msg(env, "assembler");
-  napi_value out;
-  NAPI_TRY(env, napi_create_external(env, a, asm_finalize, NULL, &out));
+  napi_value out = obj_new(env, OBJ_ASM, a, NULL);
+  if (!out) amod_asm_close(a);
   return out;
 }
 
@@ -952,35 +1049,31 @@ static napi_value js_receive_stream(napi_env env, napi_callback_info info) {
 }
 
 /* ------------------------------------------------- live receiver (processAudioBlock) */
-static void live_finalize(napi_env env, void *data, void *hint) {
-  (void)env; (void)hint;
-  amod_live_close((amod_live *)data);
-}
-
 static amod_live *get_live(napi_env env, napi_value v) {
-  void *p = NULL;
-  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
-    napi_throw_type_error(env, NULL, "expected a live receiver handle");
+  obj_box *b = obj_find(env, v, OBJ_LIVE);
+  if (!b) {
+    napi_throw_type_error(env, NULL, "expected an open live receiver handle");
     return NULL;
   }
-  return (amod_live *)p;
+  return (amod_live *)b->p;
 }
 
-/* liveOpen(cfg, assemblerHandle, device) -> handle (closed when collected) */
+/* liveOpen(cfg, assemblerHandle, device) -> handle (liveClose(handle), or closed at exit) */
 static napi_value js_live_open(napi_env env, napi_callback_info info) {
   napi_value argv[3], out;
   if (!get_args(env, info, 3, argv)) return NULL;
   amod_cfg c;
   if (!to_cfg(env, argv[0], &c)) return NULL;
-  amod_assembler *a = get_asm(env, argv[1]);
-  if (!a) return NULL;
+  obj_box *ab = get_asm_box(env, argv[1]);
+  if (!ab) return NULL;
   int32_t dev = 0;
   napi_get_value_int32(env, argv[2], &dev);
   amod_ctx *ctx = get_ctx(env, dev);
   if (!ctx) return NULL;
   amod_live *lv;
-  if (amod_live_open(ctx, &c, a, &lv) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(ctx));
-  NAPI_TRY(env, napi_create_external(env, lv, live_finalize, NULL, &out));
+  if (amod_live_open(ctx, &c, (amod_assembler *)ab->p, &lv) != AMOD_SUCCESS) return throw_msg(env, amod_last_error(ctx));
+  out = obj_new(env, OBJ_LIVE, lv, ab);
+  if (!out) amod_live_close(lv);
   return out;
 }
 
@@ -1076,10 +1169,12 @@ static napi_value init(napi_env env, napi_value exports) {
       {"asmState", NULL, js_asm_state, NULL, NULL, NULL, napi_enumerable, NULL},
       {"asmMissing", NULL, js_asm_missing, NULL, NULL, NULL, napi_enumerable, NULL},
       {"asmFile", NULL, js_asm_file, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"asmClose", NULL, js_obj_close, NULL, NULL, NULL, napi_enumerable, (void *)(intptr_t)OBJ_ASM},
       {"receiveStream", NULL, js_receive_stream, NULL, NULL, NULL, napi_enumerable, NULL},
       {"liveOpen", NULL, js_live_open, NULL, NULL, NULL, napi_enumerable, NULL},
       {"liveProcess", NULL, js_live_process, NULL, NULL, NULL, napi_enumerable, NULL},
       {"liveState", NULL, js_live_state, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"liveClose", NULL, js_obj_close, NULL, NULL, NULL, napi_enumerable, (void *)(intptr_t)OBJ_LIVE},
   };
   if (napi_define_properties(env, exports, sizeof props / sizeof props[0], props) != napi_ok) return NULL;
   return exports;

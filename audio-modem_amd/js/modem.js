@@ -489,6 +489,10 @@ class ChunkAssembler {
     return r;
   }
   cleanup() {}
+  // releases the native assembler (its chunks and maps) now, or when the last
+  // StreamingReceiver on it closes; otherwise at exit (not by the garbage collector).
+  // Additive: the reference's store lives as long as the page.
+  close() { native.asmClose(this._h); }
 }
 
 const E_STREAM_LOST = 101;
@@ -570,6 +574,9 @@ class StreamingReceiver {
   get frameErrors() { return this._st().frameErrors; }
   get totalWritten() { return this._st().totalWritten; }
   cleanup() { this.assembler.cleanup(); }
+  // releases the native receiver (its ring buffer and GPU workspace) now; the assembler
+  // stays open for the caller (assembler.close()). Additive, like ChunkAssembler.close().
+  close() { native.liveClose(this._h); }
 }
 
 const api = {

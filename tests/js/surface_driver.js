@@ -120,6 +120,33 @@ async function main() {
               fileName: a.fileName, receivedCount: a.receivedCount, crcErrors: a.crcErrors, complete: a.isComplete() },
             file: a.totalChunks > 0 ? sha(await a.assembleFile()) : null,
           };
+          // close() order: the assembler first (its handle is dead at once, its native
+          // object lives until the receiver on it closes), then the receiver
+          a.close();
+          const thrown = (f) => { try { f(); return null; } catch (e) { return e.constructor.name; } };
+          r.afterAsmClose = { asm: thrown(() => a.receivedCount), rxState: rx.state,
+            rxBlock: thrown(() => rx.processAudioBlock(new Float32Array(4096))) };
+          rx.close();
+          r.afterRxClose = { rx: thrown(() => rx.state), again: thrown(() => { rx.close(); a.close(); }) };
+          break;
+        }
+        case 'asm_close': {
+          // handles: close() frees, later use throws TypeError, a second close is a no-op;
+          // open/close cycles; assemblers left open are closed at exit (clean exit code)
+          const thrown = (f) => { try { f(); return null; } catch (e) { return e.constructor.name; } };
+          const a = new M.ChunkAssembler();
+          await a.handleMetadataFrame({ totalChunks: 2, totalFileSize: 10, chunkSize: 5, fileName: 'x' });
+          const before = a.totalChunks;
+          a.close();
+          r = { before, after: thrown(() => a.totalChunks), chunk: thrown(() => M.native.asmChunk(a._h, 0, new Uint8Array(5), true)),
+            again: thrown(() => a.close()) };
+          for (let i = 0; i < j.cycles; i++) {
+            const b = new M.ChunkAssembler();
+            await b.handleDataChunk(0, new Uint8Array(5), true);
+            b.close();
+          }
+          for (let i = 0; i < j.leftOpen; i++) new M.ChunkAssembler();
+          r.cycles = j.cycles;
           break;
         }
         default: throw new Error('unknown op ' + j.op);

@@ -310,6 +310,15 @@ def test_chunk_assembler_through_js(store, tmp_path):
                 assert g["received"] == [i not in miss for i in range(w["totalChunks"])], name
 
 
+def test_chunk_assembler_close(tmp_path):
+    """ChunkAssembler handles are numbers released by close() (or at exit), not napi
+    externals: a closed handle throws TypeError, a second close is a no-op, 3000
+    open/close cycles run, and assemblers left open do not crash the exit (Node 12's
+    weak references on externals did)."""
+    r = ok(run([{"op": "asm_close", "id": "c", "cycles": 3000, "leftOpen": 50}], tmp_path), "c")
+    assert r == {"before": 2, "after": "TypeError", "chunk": "TypeError", "again": None, "cycles": 3000}
+
+
 @pytest.mark.gpu
 def test_receive_stream_through_js(tmp_path):
     """receiveStream (StreamingReceiver over a recorded stream) from JS on the golden
@@ -372,6 +381,9 @@ def test_live_receiver_through_js(tmp_path):
         assert (g["framesDecoded"], g["frameErrors"]) == (sp["framesDecoded"], sp["frameErrors"]), name
         assert (g["state"], g["acScanPos"]) == (sp["final"]["state"], sp["final"]["acScanPos"]), name
         assert g["totalWritten"] == sp["n"], name
+        # assembler closed first: its handle throws, the receiver on it keeps working
+        assert g["afterAsmClose"] == {"asm": "TypeError", "rxState": g["state"], "rxBlock": None}, name
+        assert g["afterRxClose"] == {"rx": "TypeError", "again": None}, name
         a = sp["assembler"]
         assert [g["asm"][k] for k in ("totalChunks", "totalFileSize", "chunkSize", "receivedCount", "crcErrors",
                                       "complete", "fileName")] == [a[k] for k in ("totalChunks", "totalFileSize",
