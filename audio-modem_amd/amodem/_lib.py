@@ -123,6 +123,13 @@ SIGNATURES = {
     "amod_decode_host": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P, _P,
                                    C.c_int64, C.c_uint32]),
     "amod_synchronize": (C.c_int, [_P]),
+    "amod_pipe_open": (C.c_int, [_P, _P, C.POINTER(_P)]),
+    "amod_pipe_close": (C.c_int, [_P]),
+    "amod_pipe_next_stream": (_P, [_P]),
+    "amod_pipe_decode_device": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, _P, _P, C.c_int32, _P, _P,
+                                          C.c_int64, C.c_uint32, _P]),
+    "amod_pipe_flush": (C.c_int, [_P, _P]),
+    "amod_pipe_synchronize": (C.c_int, [_P]),
     "amod_set_profiling": (C.c_int, [_P, C.c_int]),
     "amod_kernel_breakdown": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "amod_kernel_stages": (C.c_int, [_P, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int64)]),

@@ -210,6 +210,10 @@ class Demodulator:
     def synchronize(self):
         L.check(self._L.amod_synchronize(self.ctx), self.ctx)
 
+    def pipeline(self, other: "Demodulator") -> "Pipeline":
+        """A depth-2 pipeline of device decodes over this context and `other` (amod_pipe_*)."""
+        return Pipeline(self, other)
+
     # ------------------------------------------------------------ streaming
     def stream_receive(self, cfg: L.Cfg, samples: np.ndarray, assembler: "ChunkAssembler | None" = None,
                        max_frames: int = 1 << 20):
@@ -312,6 +316,50 @@ class Demodulator:
             L.check(0 if self._L.amod_tx_host(*args, out.ctypes.data, offs.ctypes.data) == total else -1, self.ctx)
         lens = np.diff(np.append(offs, total)).astype(np.int32)
         return out[:total], offs, lens
+
+
+class Pipeline:
+    """amod_pipe_*: consecutive device decodes alternate between two Demodulators, on the
+    pipe's two streams, so batch i + 1's detection overlaps batch i's demodulation.
+    Fastest: enqueue a batch's inputs on next_stream(), decode with stream=0, and read its
+    results on that stream (e.g. torch.cuda.ExternalStream(next_stream())). With another
+    `stream`, decode i's results are ordered on it once decode i + 1 is enqueued, or after
+    flush(stream). synchronize() waits on the host. The Demodulators stay the caller's."""
+
+    def next_stream(self) -> int:
+        """the hipStream_t (int) the next decode runs on"""
+        return int(self._L.amod_pipe_next_stream(self._h) or 0)
+
+    def __init__(self, a: Demodulator, b: Demodulator):
+        self._L = a._L
+        self._dms = (a, b) # (kept alive while the pipe uses their contexts)
+        h = C.c_void_p()
+        L.check(self._L.amod_pipe_open(a.ctx, b.ctx, C.byref(h)), a.ctx)
+        self._h = h
+
+    def decode_device(self, cfg: L.Cfg, mode: int, samples_ptr: int, offsets_ptr: int, lengths_ptr: int,
+                      nframes: int, results_ptr: int, payload_ptr: int, stride: int, stream: int = 0,
+                      options: int = 0):
+        L.check(self._L.amod_pipe_decode_device(self._h, C.byref(cfg), mode, samples_ptr, offsets_ptr, lengths_ptr,
+                                                nframes, results_ptr, payload_ptr, stride, options, stream or None),
+                self._dms[0].ctx)
+
+    def flush(self, stream: int = 0):
+        L.check(self._L.amod_pipe_flush(self._h, stream or None), self._dms[0].ctx)
+
+    def synchronize(self):
+        L.check(self._L.amod_pipe_synchronize(self._h), self._dms[0].ctx)
+
+    def close(self):
+        if self._h:
+            self._L.amod_pipe_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ------------------------------------------------------------ host utilities --

@@ -273,16 +273,18 @@ class Workload:
                               options=options)
 
     def enable_pipeline(self):
-        """Consecutive batches over two contexts (each its own workspace, result buffers and
-        stream): batch i + 1's k_detect runs while batch i's k_demod finishes, so the two
-        kernels' tails and the dependent-launch gaps overlap (tools/pipeline_ab.py: C2
-        0.455 -> 0.425 ms per step, C5 1.60 -> 1.47; C4, one k_demod launch, no gain)."""
+        """Consecutive batches through the library's depth-2 pipe (amod_pipe_*, Python
+        `Pipeline`) over two contexts, each decoding on its own stream: batch i + 1's
+        k_detect runs while batch i's k_demod finishes, so the two kernels' tails and the
+        dependent-launch gaps overlap (tools/pipeline_ab.py: C2 0.455 -> 0.425 ms per step,
+        C5 1.60 -> 1.47; C4, one k_demod launch, no gain). Result buffers alternate, so
+        batch i's rows are intact until batch i + 2."""
         torch, amodem = self.env.torch, self.env.amodem
         self.dm2 = amodem.Demodulator(self.env.local)
         self.dm2.reserve(self.cfg, self.F, int(self.dlens.max()))
         self.d_res2 = torch.zeros_like(self.d_res)
         self.d_pay2 = torch.zeros_like(self.d_pay)
-        self.pstreams = [torch.cuda.Stream(self.env.dev), torch.cuda.Stream(self.env.dev)]
+        self.pipe = self.dm.pipeline(self.dm2)
         self.pi = 0
 
     def step_ctx(self, k, stream):
@@ -293,12 +295,20 @@ class Workload:
 
     def step_pipelined(self):
         k, self.pi = self.pi, self.pi ^ 1
-        self.step_ctx(k, self.pstreams[k].cuda_stream)
+        res, pay = (self.d_res, self.d_pay) if k == 0 else (self.d_res2, self.d_pay2)
+        self.pipe.decode_device(self.cfg, self.mode, self.xs.data_ptr(), self.d_doff.data_ptr(),
+                                self.d_dlen.data_ptr(), self.F, res.data_ptr(), pay.data_ptr(), self.stride)
+
+    def pipeline_flush(self):
+        self.pipe.synchronize()
 
     def records(self):
         return np.frombuffer(self.d_res.cpu().numpy().tobytes(), self.env.amodem.RESULT_DTYPE)
 
     def close(self):
+        if getattr(self, "pipe", None) is not None:
+            self.pipe.close()
+            self.pipe = None
         self.dm.close()
         if getattr(self, "dm2", None) is not None:
             self.dm2.close()
@@ -353,6 +363,8 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if pipe:
+        wl.pipeline_flush()  # (the decodes ran on the pipe's slot streams)
     sync()
     env.barrier()
     elapsed = time.perf_counter() - t0
@@ -414,9 +426,10 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
         "value": value, "unit": "samples/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "warmup_run": warm, "ms_per_step": elapsed / steps * 1e3,
         "pipeline": {"contexts": 2 if pipe else 1,
-                     "what": "consecutive batches alternate between two contexts (own workspace, results and "
-                             "stream): batch i+1's k_detect overlaps batch i's k_demod; rooflines and chain from "
-                             "the same K steps on one context alone" if pipe else "one context, one stream",
+                     "what": "the library's depth-2 pipe (amod_pipe_decode_device): consecutive batches alternate "
+                             "between two contexts (own workspace and stream), batch i+1's k_detect overlaps batch "
+                             "i's k_demod; rooflines and chain from the same K steps on one context alone"
+                             if pipe else "one context, one stream",
                      "one_context_ms_per_step": (serial / steps * 1e3) if serial else elapsed / steps * 1e3,
                      "one_context_samples_per_s": wl.ndecoded * world * steps / (serial if serial else elapsed)},
         "payload_MB_per_s": wl.payload_bytes * wl.F * world * steps / elapsed / 1e6,

@@ -174,6 +174,28 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
                      amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options);
 int amod_synchronize(amod_ctx *ctx);
 
+/* ---- a depth-2 pipeline of device decodes (additive; no reference counterpart) ----
+ * Consecutive batches alternate between two caller-owned contexts of one device, each
+ * decoding on one of the pipe's two streams, so batch i + 1's detection overlaps batch i's
+ * demodulation. Fastest use (stream = NULL or the slot's stream): enqueue each batch's
+ * inputs on amod_pipe_next_stream(p) (hipStream_t), decode, and read its results on that
+ * same stream: plain stream order. With another `stream`, a decode starts once that
+ * stream reaches the call, and decode i's results are ordered on it when decode i + 1 has
+ * been enqueued, or after amod_pipe_flush(stream) (two cross-queue signals per batch: less
+ * overlap). amod_pipe_synchronize waits on the host. One host thread per pipe; the
+ * contexts must outlive it and take no other work while it runs. */
+typedef struct amod_pipe amod_pipe;
+int amod_pipe_open(amod_ctx *a, amod_ctx *b, amod_pipe **out);
+int amod_pipe_close(amod_pipe *p); /* waits for its decodes and destroys its two streams;
+                                      the contexts stay open */
+void *amod_pipe_next_stream(const amod_pipe *p);
+int amod_pipe_decode_device(amod_pipe *p, const amod_cfg *cfg, int32_t mode, const float *samples,
+                            const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                            amod_result *results, uint8_t *payload, int64_t payload_stride,
+                            uint32_t options, void *stream);
+int amod_pipe_flush(amod_pipe *p, void *stream);
+int amod_pipe_synchronize(amod_pipe *p);
+
 /* kernel timing: when enabled, every decode brackets each launch of the fast path
    (k_detect, k_demod) and k_decode_exact with hipEvents on the launch
    stream; amod_kernel_times waits for them, returns the accumulated milliseconds of
