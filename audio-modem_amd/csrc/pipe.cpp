@@ -4,7 +4,9 @@
 // alternate between the two contexts, each decoding on a stream of the pipe's own, so
 // batch i + 1's k_detect (the HBM-bound stream pass) starts while batch i's k_demod and
 // frame ends are still running: the two kernels' tails and the dependent-launch gaps
-// between them overlap (C2: 0.444 -> 0.419 ms per batch, tools/pipeline_ab.py).
+// between them overlap (C2: 0.445 -> 0.42-0.43 ms per batch, C5 10 dB 1.60 -> 1.48-1.53,
+// tools/pipeline_ab.py; the contexts' own streams or high-priority slot streams measured
+// the same within the run-to-run spread).
 //
 // The caller works on the slot's stream (amod_pipe_next_stream: the stream the next decode
 // runs on): it enqueues that batch's inputs there before the call and reads the results
