@@ -216,7 +216,6 @@ __device__ __forceinline__ void pk_dft8(f2v (&v)[8]) {
 // 72 q2 + l1 resp. 72 q2 + 9 p1 (q2 < 4 inside a group) are distinct mod 32.
 constexpr int XROW = 72;
 constexpr int XCH_F2 = 8 * XROW; // float2 per wave
-constexpr int kDecScratch = 2 * XCH_F2 - 64; // k_demod's decisions: per-lane scratch dwords (past any job's decisions)
 // spec_idx: bits 4-5 of n XOR-ed into bits 1-2. The pass-3 store of lane (p1, q2) writes
 // n = q2 + 8 p1 (+ 64 p2): in each 16-lane ds_write_b64 group (q2 in {2g, 2g + 1}) the
 // float2 slots mod 16 are then (q2 ^ 2 (p1 >> 1)) + 8 (p1 & 1), all distinct (the
@@ -1580,23 +1579,27 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   // (conflict-free under spec_idx; lane l on subcarrier l had every group 2-way, in both
   // halves Z[k] and Z[512 - k]: 16 of k_demod's ~40 conflict cycles per job on C4); the
   // mirrored half stays 2-way in one lane pair per group. The bit offset of its decision
-  // in a symbol, di * BPS (-1 pilot, -2 none; di = data index)
+  // in a symbol, di * BPS (di = data index). A slot without a data subcarrier holds
+  // BPS * (jk + lane) (a pilot) or BPS * (jk + 64 + lane) (none): its decision store then
+  // lands in a junk dword past any job's decision run (jk: two symbols' decisions plus
+  // two stream words) by the same address arithmetic as a data slot's, so a store is one
+  // add and one shift-add (it was five VALU with the select of a scratch dword)
   // (two 16-bit fields per register: registers bound k_demod's occupancy)
   const int bo0 = (lane - sub_start) & 63;
+  const int jk = 2 * ndata + 64;
   uint32_t di_pk[2] = {0u, 0u};
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int di = bo0 + 64 * rr < nband ? (int)cfg.t.band_di[bo0 + 64 * rr] : -2;
-    const int dib = di >= 0 ? di * BPS : di;
-    di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
-  }
-  auto dib_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
   // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
   // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
   int prr = -1, npl = 0;
 #pragma unroll
-  for (int rr = 3; rr >= 0; --rr)
-    if (dib_of(rr) == -1) { prr = rr; ++npl; }
+  for (int rr = 3; rr >= 0; --rr) {
+    const int di = bo0 + 64 * rr < nband ? (int)cfg.t.band_di[bo0 + 64 * rr] : -2;
+    const int dib = di >= 0 ? di * BPS : BPS * (jk + lane + (di == -2 ? 64 : 0));
+    di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
+    if (di == -1) { prr = rr; ++npl; }
+  }
+  auto dib_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
+  auto pilot_slot = [&](int rr) { const int b = dib_of(rr); return b >= BPS * jk && b < BPS * (jk + 64); };
   const bool pil_multi = __ballot(npl > 1) != 0;
   uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
 #pragma unroll
@@ -1874,7 +1877,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         pilot(prr >= 0, p1, p2);
       } else {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) pilot(dib_of(rr) == -1, e1[rr], e2[rr]);
+        for (int rr = 0; rr < 4; ++rr) pilot(pilot_slot(rr), e1[rr], e2[rr]);
       }
       if (!KO(4)) wsum_b4(ps1, pe1, ps2, pe2);
       else { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
@@ -1911,6 +1914,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         if (ge + ln < gend) dec[ge - g0 + ln] = 0u;
       }
       const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
+      char *const decg = reinterpret_cast<char *>(dec) - 4 * g0; // (byte base of decision index 0)
       int dflag1 = 0, dflag2 = 0;
 #pragma unroll
       for (int which = 0; which < 2; ++which) {
@@ -1935,12 +1939,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
             db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
           }
           db = live ? db : org_bits;
-          unc_any |= !KO(0xFFFF) && dib >= 0 && live && margin <= tau;
-          // a lane without a data subcarrier in this slot (pilot, past the band) stores into
-          // its own scratch dword at the buffer's end instead: no exec-mask block per store
+          unc_any |= !KO(0xFFFF) && dib < BPS * jk && live && margin <= tau;
+          // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
+          // stores into its junk dword: no exec-mask block per store); pos is a multiple of
+          // BPS, so the byte offset is pos * (4 / BPS): one shift-add from the job's base
           const uint32_t pos = (uint32_t)(sbase + dib);
-          const uint32_t di = dib >= 0 ? pos / BPS - (uint32_t)g0 : (uint32_t)(kDecScratch + ln);
-          dec[di] = db >> (pos & 31);
+          *reinterpret_cast<uint32_t *>(decg + pos * (4 / BPS)) = db >> (pos & 31);
         }
         if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
       }

@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../audio-modem_amd/csrc"
 HIPCC=/opt/rocm/bin/hipcc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -I."
-OBJS="../lib/k_decode_exact.o ../lib/k_tx.o ../lib/k_stream.o ../lib/stream.o ../lib/runtime.o ../lib/assembler.o ../lib/group.o"
+OBJS="../lib/k_decode_exact.o ../lib/k_tx.o ../lib/k_stream.o ../lib/stream.o ../lib/runtime.o ../lib/assembler.o ../lib/group.o ../lib/pipe.o"
 for v in "$@"; do
   name=${v%%=*}; extra=${v#*=}
   out=../lib/variants/$name; mkdir -p $out

@@ -1,6 +1,4 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-for v in own ctx hi; do
-  AMOD_PIPE_STREAMS=$v AB_CONFS=c2,c5,c3 AB_ROUNDS=6 timeout -k 10 300 python -u tools/pipeline_ab.py > gpurun_out/pab_$v.log 2>&1 || exit $?
-  echo "== $v"; grep -v Warn gpurun_out/pab_$v.log | grep ms/step
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+AB_CONFS=c2,c4,c5 timeout -k 10 600 python -u tools/ab_demod.py audio-modem_amd/lib/variants/base/libamodem.so audio-modem_amd/lib/variants/junk/libamodem.so > gpurun_out/junk_ab.log 2>&1; rc=$?; grep -v Warn gpurun_out/junk_ab.log | tail -8; exit $rc
