@@ -1931,15 +1931,21 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           const int dib = dib_of(rr);
           const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
           uint32_t db;
-          float margin;
+          bool near; // the decision margin is inside the guard band
           if (MOD == AMOD_QPSK) {
             db = qpsk_bits(c.x, c.y);
-            margin = fminf(fabsf(c.x), fabsf(c.y));
+            // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
+            // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
+            float margin;
+            asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(margin) : "v"(c.x), "v"(c.y));
+            near = margin <= tau;
           } else {
+            float margin;
             db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
+            near = margin <= tau;
           }
           db = live ? db : org_bits;
-          unc_any |= !KO(0xFFFF) && dib < BPS * jk && live && margin <= tau;
+          unc_any |= !KO(0xFFFF) && dib < BPS * jk && live && near;
           // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
           // stores into its junk dword: no exec-mask block per store); pos is a multiple of
           // BPS, so the byte offset is pos * (4 / BPS): one shift-add from the job's base
