@@ -1923,6 +1923,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         const bool live = which == 0 ? live1 : live2;
         const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
         const float tau = which == 0 ? tau1 : tau2;
+        const uint32_t lm31 = live ? 0x80000000u : 0u, lm30 = live ? 0x40000000u : 0u; // (QPSK)
         const int sbase = sidx * per_sym;
         int unc_any = 0;
 #pragma unroll
@@ -1933,7 +1934,12 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           uint32_t db;
           bool near; // the decision margin is inside the guard band
           if (MOD == AMOD_QPSK) {
-            db = qpsk_bits(c.x, c.y);
+            // the sign-bit decision with the symbol's liveness folded into its two masks:
+            // QPSK's origin decision is index 0 (four equidistant points, the first kept:
+            // runtime.cpp demap_exact(QPSK, 0, 0)), so a dead symbol's bits are 0 and no
+            // per-slot select is needed
+            const uint32_t a = __float_as_uint(c.x), b = __float_as_uint(c.y);
+            db = (b & lm31) | (((a ^ b) >> 1) & lm30);
             // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
             // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
             float margin;
@@ -1944,7 +1950,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
             db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
             near = margin <= tau;
           }
-          db = live ? db : org_bits;
+          if (MOD != AMOD_QPSK) db = live ? db : org_bits;
           unc_any |= !KO(0xFFFF) && dib < BPS * jk && live && near;
           // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
           // stores into its junk dword: no exec-mask block per store); pos is a multiple of
