@@ -91,3 +91,19 @@ def test_payload_stride():
     cfg = amodem.preset("standard", "QPSK", 1)
     s = amodem.payload_stride(cfg, 35874)
     assert s % 16 == 0 and s >= (35874 // 576) * 410 // 8
+
+
+def test_pipe_rejects_bad_arguments_without_a_gpu():
+    """amod_pipe_*: argument errors come back as AMOD_ERR_ARG before any HIP call (NULL
+    contexts, a NULL pipe); a NULL pipe has no next stream and closes as a no-op (the same
+    context twice: tests/test_gpu_pipe.py, it needs a real context)."""
+    lib = L.load()
+    h = C.c_void_p()
+    assert lib.amod_pipe_open(None, None, C.byref(h)) == -1
+    assert not h.value
+    cfg = amodem.make_cfg("QPSK", 1)
+    assert lib.amod_pipe_decode_device(None, C.byref(cfg), 0, None, None, None, 0, None, None, 16, 0, None) == -1
+    assert lib.amod_pipe_flush(None, None) == -1
+    assert lib.amod_pipe_synchronize(None) == -1
+    assert not lib.amod_pipe_next_stream(None)
+    assert lib.amod_pipe_close(None) == 0
