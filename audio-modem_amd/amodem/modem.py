@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
+import weakref
 
 import numpy as np
 
@@ -146,6 +147,10 @@ class Demodulator:
 
     def close(self):
         if self.ctx:
+            # a Pipeline over this context finishes its decodes and closes first (its slot
+            # streams may still run kernels on this context's workspace)
+            for p in list(getattr(self, "_pipes", ())):
+                p.close()
             self._L.amod_close(self.ctx)
             self.ctx = None
 
@@ -333,9 +338,14 @@ class Pipeline:
     def __init__(self, a: Demodulator, b: Demodulator):
         self._L = a._L
         self._dms = (a, b) # (kept alive while the pipe uses their contexts)
+        self._h = None
         h = C.c_void_p()
         L.check(self._L.amod_pipe_open(a.ctx, b.ctx, C.byref(h)), a.ctx)
         self._h = h
+        for dm in (a, b):
+            if not hasattr(dm, "_pipes"):
+                dm._pipes = weakref.WeakSet()
+            dm._pipes.add(self)
 
     def decode_device(self, cfg: L.Cfg, mode: int, samples_ptr: int, offsets_ptr: int, lengths_ptr: int,
                       nframes: int, results_ptr: int, payload_ptr: int, stride: int, stream: int = 0,

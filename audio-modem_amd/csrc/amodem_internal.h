@@ -180,8 +180,10 @@ struct Knobs {
   bool no_gap_scan = false; // AMOD_NO_GAP_SCAN
   int stream_threads = -1;  // AMOD_STREAM_THREADS (-1: unset)
   bool stream_fullcopy = false; // AMOD_STREAM_FULLCOPY
-  // (AMOD_EMA_WARM / _PER / _ROUNDS, the EMA kernels' experiment shapes, are read once per
-  // process by k_stream.hip's launchers, which have no context)
+  // the EMA kernels' experiment shapes (k_stream.hip; < 0: the kernel defaults)
+  int ema_per = -1;         // AMOD_EMA_PER: output chunks per k_ema_out lane
+  int ema_warm = -1;        // AMOD_EMA_WARM: warm-up chunks per output chunk
+  int ema_rounds = -1;      // AMOD_EMA_ROUNDS: parallel fix rounds before the serial safety net
 };
 
 // k_gap_scan -> streaming receiver: the scan that follows the frame of fine range r, run
@@ -535,14 +537,16 @@ hipError_t amod_launch_tx(const amod::DevCfg &cfg, const amod::DevTxWork &w, hip
 hipError_t amod_launch_flush(const void *buf, size_t bytes, float *sink, hipStream_t s); // experiments
 int amod_fast_lds_bytes(int nb_cap, int fine_cap, int sym); // dynamic LDS of one k_detect workgroup
 // streaming receiver pieces (k_stream.hip)
+// (kn: the calling context's knobs, for the EMA's experiment shapes; null: the defaults)
 int64_t amod_ema_chunk();
 hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
-                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s);
-int64_t amod_ema_wave_samples(); // the stream piece granule of amod_launch_ema_part
+                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s,
+                           const amod::Knobs *kn);
+int64_t amod_ema_wave_samples(const amod::Knobs *kn); // the stream piece granule of amod_launch_ema_part
 hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
-                                const double *apow, int64_t s0, int64_t s1, hipStream_t s);
+                                const double *apow, int64_t s0, int64_t s1, hipStream_t s, const amod::Knobs *kn);
 hipError_t amod_launch_ema_fix(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end,
-                               int64_t *list, unsigned long long *fixed, hipStream_t s);
+                               int64_t *list, unsigned long long *fixed, hipStream_t s, const amod::Knobs *kn);
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s);
 hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int sym, double pre1_energy,
                             const int64_t *first, const int64_t *base, const int64_t *count, int nranges,

@@ -62,6 +62,9 @@ struct FileArena {
   std::atomic<size_t> populated{0};    // bytes from the start the helper has faulted in
   std::thread filler;
   std::atomic<bool> stop{false};
+  // experiments (AMOD_ASM_NO_POPULATE): no background population, so the copies take the
+  // first-touch faults; read once per assembler, when it is created
+  const bool no_populate = getenv("AMOD_ASM_NO_POPULATE") != nullptr;
   ~FileArena() { release(); }
   void release() {
     stop.store(true, std::memory_order_relaxed);
@@ -104,7 +107,7 @@ struct FileArena {
     }
     populated.store(done, std::memory_order_relaxed);
     const size_t len = std::min(n, kPopulateMax);
-    if (getenv("AMOD_ASM_NO_POPULATE") || done >= len) return true; // (experiments: first-touch faults in the copies)
+    if (no_populate || done >= len) return true;
     filler = std::thread([this, q = p, from = done, len] {
       constexpr int kPopulateWrite = 23; // MADV_POPULATE_WRITE (Linux 5.14)
       // one huge page per call: each call holds the address-space lock (read) while it

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -146,6 +147,10 @@ struct ResidentShard {
 };
 
 struct amod_resident {
+  // one decode at a time: every decode of the batch shares its shards' device result and
+  // payload buffers (and may reallocate the payload), and the Node addon runs decodes on
+  // the libuv pool, so two outstanding decodeBatch(DeviceBatch) calls would race
+  std::mutex mu;
   amod_group *g = nullptr;
   int32_t nframes = 0;
   int32_t max_len = 0;
@@ -236,6 +241,7 @@ extern "C" int amod_resident_decode(amod_resident *r, const amod_cfg *cfg, int32
                                     amod_result *results, uint8_t *payload, int64_t payload_stride) {
   if (!r || !cfg || (r->nframes && (!results || !payload)) || payload_stride < 16 || payload_stride % 16)
     return amod_ctx_fail(nullptr, "invalid argument", AMOD_ERR_ARG);
+  std::lock_guard<std::mutex> lock(r->mu); // the memsets, the decode and the copies back, as one
   amod_group *g = r->g;
   std::vector<amod_shard> shards(r->sh.size());
   for (size_t k = 0; k < r->sh.size(); ++k) {

@@ -58,7 +58,8 @@ constexpr int SB = AMOD_SB;                  // stream pass: chunks per load bat
 // no frame is listed for the exact kernel and every job of every frame runs (the time of
 // the same work); bit 1 skips the frame-end CRC, 2 the demap and bit-stream packing, 4 the
 // pilot reductions, 8 the window checks, 16 the FFT, 128 only the FFT's LDS exchanges
-// (arithmetic kept). The results are
+// (arithmetic kept), 0x200 the whole frame end (vote, parse, CRC, stores), 0x400 the
+// header evaluation after each job. The results are
 // wrong; only the kernel time matters (0x100 alone: the policy change only, the
 // baseline of the others). Undefined in every product build.
 #ifdef AMOD_KO
@@ -423,14 +424,21 @@ __device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) 
     a += ta; b += tb; c += tc; d += td; }
   AMOD_W4(0xB1) AMOD_W4(0x4E) AMOD_W4(0x141) AMOD_W4(0x140)
 #undef AMOD_W4
-#define AMOD_W4B(ctrl, rmask)                                                           \
-  { const float ta = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), ctrl, rmask, 0xF, false)); \
-    const float tb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(b), ctrl, rmask, 0xF, false)); \
-    const float tc = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c), ctrl, rmask, 0xF, false)); \
-    const float td = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), ctrl, rmask, 0xF, false)); \
-    a += ta; b += tb; c += tc; d += td; }
-  AMOD_W4B(0x142, 0xA) AMOD_W4B(0x143, 0xC)
-#undef AMOD_W4B
+  // the two row broadcasts as DPP adds into the value itself: the rows a broadcast does
+  // not enable keep their sums (the builtin form moved a zero and the broadcast into a
+  // scratch register first, then added: three VALU per step instead of one). The s_nop
+  // covers the DPP read of a value the compiler's last VALU may have just written;
+  // inside the block each chain's previous write is three instructions back
+  asm volatile("s_nop 1\n"
+               "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "v_add_f32_dpp %3, %3, %3 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "v_add_f32_dpp %3, %3, %3 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
   a = rlane(a, 63); b = rlane(b, 63); c = rlane(c, 63); d = rlane(d, 63);
 }
 __device__ __forceinline__ float wmax_b(float v) {
@@ -448,8 +456,12 @@ __device__ __forceinline__ float wmax_nn(float x) {
   int v = __float_as_int(x);
   v = max(v, AMOD_DPP_I(v, 0xB1)); v = max(v, AMOD_DPP_I(v, 0x4E));
   v = max(v, AMOD_DPP_I(v, 0x141)); v = max(v, AMOD_DPP_I(v, 0x140));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));
+  // the row broadcasts as DPP maxima into v itself (see wsum_b4)
+  asm volatile("s_nop 1\n"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "s_nop 1\n"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               : "+v"(v));
   return __int_as_float(__builtin_amdgcn_readlane(v, 63));
 }
 
@@ -1761,6 +1773,13 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       }
       DSTAMP(16, jcur == 1);
       DSTAMP(27, jcur == 2); // (job 2 samples ready: minus mark 21 = the wait for its loads)
+#ifdef AMOD_LOAD_FENCE
+      // (experiment) the FFT input formed before the next job's loads are issued: the
+      // compiler otherwise issues the loads first and copies the samples out of their
+      // target registers
+      asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                   "+v"(v[7])::"memory");
+#endif
       issue_next(); // the samples are in v: the next job's loads fly under this FFT too
       if (!KO(16)) fft512_wave(v, X2, tw1, tw2);
       DSTAMP(17, jcur == 1);
@@ -1994,7 +2013,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       DSTAMP(21, jcur == 1);
       // once the header is decoded the parse's byte range is known: the frame takes only
       // the jobs that demodulate it (trailing silence or noise is never transformed)
-      if (!DBG && fneed < 0 && !wflags) { // (parity-debug launches demodulate every symbol)
+      if (!DBG && fneed < 0 && !wflags && !KO(0x400)) { // (parity-debug launches demodulate every symbol)
         const int dsym = jcur == 0 ? 1 : min(2 * jcur + 1, cur.T);
         // (the job count only ever shrinks, once the answer is final: the next job was
         // chosen before this one ran, so a frame whose count grew would lose jobs)
@@ -2017,7 +2036,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       }
     }
     // ---------------------------------------------------------------- frame end
-    if (jcur + 1 >= fnj) {
+    if (jcur + 1 >= fnj && !KO(0x200)) {
       FRESH_ARGS; // the finish's tables and outputs: scalar loads here, not held across the loop
       DSTAMP(22, true);
       const int nbits = cur.M * per_sym;

@@ -840,35 +840,29 @@ int64_t amod_ema_chunk() { return amod::kL; }
 // DC removal of x[0, n) from a zero EMA state into y (x read for [0, nx), zero past it); warm / end / scr: nch = ceil(n / L)
 // doubles each; list: nch int64; apow: L doubles (a^j); fixed: 2 counters
 namespace {
-int ema_per() {
-  static const int per = [] {
-    const char *e = getenv("AMOD_EMA_PER"); // experiments: output chunks per lane
-    return e ? std::max(1, atoi(e)) : amod::kPerDefault;
-  }();
-  return per;
-}
+// the EMA's experiment shapes come from the context's knobs (read at amod_open)
+int ema_per(const amod::Knobs *kn) { return kn && kn->ema_per > 0 ? kn->ema_per : amod::kPerDefault; }
+int ema_warm(const amod::Knobs *kn) { return kn && kn->ema_warm >= 0 ? kn->ema_warm : amod::kWarmDefault; }
+int ema_rounds(const amod::Knobs *kn) { return kn && kn->ema_rounds >= 0 ? kn->ema_rounds : amod::kEmaRounds; }
 } // namespace
 
 // samples per k_ema_out wave (64 lanes x per chunks): a piece of the stream that is a
 // multiple of this can be cleaned as soon as it and the samples before it have landed
-int64_t amod_ema_wave_samples() { return (int64_t)64 * ema_per() * amod::kL; }
+int64_t amod_ema_wave_samples(const amod::Knobs *kn) { return (int64_t)64 * ema_per(kn) * amod::kL; }
 
 // stages (1) + (2) for the waves of samples [s0, s1) (s0 a multiple of
 // amod_ema_wave_samples(); s1 too, or the end n): their chunk contributions, then their
 // outputs; every sample before s1 must have landed (warm-up reads the chunks before s0)
 hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
-                                const double *apow, int64_t s0, int64_t s1, hipStream_t s) {
+                                const double *apow, int64_t s0, int64_t s1, hipStream_t s, const amod::Knobs *kn) {
   const int64_t nch = (n + amod::kL - 1) / amod::kL;
   const int64_t c0 = s0 / amod::kL, c1 = std::min(nch, (s1 + amod::kL - 1) / amod::kL);
   if (c1 <= c0) return hipSuccess;
   double A = 1.0;
   for (int i = 0; i < amod::kL; ++i) A *= amod::kAlpha;
   hipLaunchKernelGGL(amod::k_ema_contrib, dim3((unsigned)((c1 - c0 + 3) / 4)), dim3(256), 0, s, x, nx, apow, scr, c0, c1);
-  static const int warm_chunks = [] {
-    const char *e = getenv("AMOD_EMA_WARM"); // experiments: warm-up chunks per output chunk
-    return e ? std::max(0, atoi(e)) : amod::kWarmDefault;
-  }();
-  const int per = ema_per();
+  const int warm_chunks = ema_warm(kn);
+  const int per = ema_per(kn);
   const int64_t span = (int64_t)64 * per; // chunks per wave
   const int64_t w0 = c0 / span, w1 = (c1 + span - 1) / span;
   hipLaunchKernelGGL(amod::k_ema_out, dim3((unsigned)((w1 - w0 + 3) / 4)), dim3(256), 0, s, x, nx, n, scr, A, y, warm,
@@ -878,16 +872,13 @@ hipError_t amod_launch_ema_part(const float *x, int64_t nx, int64_t n, float *y,
 
 // (3) + (4) once every part is enqueued: the check rounds and the fixes
 hipError_t amod_launch_ema_fix(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end,
-                               int64_t *list, unsigned long long *fixed, hipStream_t s) {
+                               int64_t *list, unsigned long long *fixed, hipStream_t s, const amod::Knobs *kn) {
   const int64_t nch = (n + amod::kL - 1) / amod::kL;
   if (nch <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(fixed, 0, 2 * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   uint8_t *const lflag = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(list + nch) + 15) & ~uintptr_t(15));
-  static const int rounds = [] {
-    const char *e = getenv("AMOD_EMA_ROUNDS"); // experiments
-    return e ? std::max(0, atoi(e)) : amod::kEmaRounds;
-  }();
+  const int rounds = ema_rounds(kn);
   for (int r = 0; r < rounds; ++r) {
     e = hipMemsetAsync(fixed + 1, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
@@ -905,12 +896,13 @@ hipError_t amod_launch_ema_fix(const float *x, int64_t nx, int64_t n, float *y, 
 }
 
 hipError_t amod_launch_ema(const float *x, int64_t nx, int64_t n, float *y, double *warm, double *end, double *scr,
-                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s) {
+                           int64_t *list, const double *apow, unsigned long long *fixed, hipStream_t s,
+                           const amod::Knobs *kn) {
   const int64_t nch = (n + amod::kL - 1) / amod::kL;
   if (nch <= 0) return hipSuccess;
-  hipError_t e = amod_launch_ema_part(x, nx, n, y, warm, end, scr, apow, 0, n, s);
+  hipError_t e = amod_launch_ema_part(x, nx, n, y, warm, end, scr, apow, 0, n, s, kn);
   if (e != hipSuccess) return e;
-  return amod_launch_ema_fix(x, nx, n, y, warm, end, list, fixed, s);
+  return amod_launch_ema_fix(x, nx, n, y, warm, end, list, fixed, s, kn);
 }
 
 hipError_t amod_launch_sc_screen(const float *y, int64_t n, float thresh, double2 *ze, uint8_t *hot, hipStream_t s) {

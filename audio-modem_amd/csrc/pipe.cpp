@@ -27,8 +27,10 @@ struct amod_pipe {
   hipStream_t slot[2] = {nullptr, nullptr}; // the streams the decodes run on
   hipEvent_t ev_in = nullptr;               // a caller's stream reached the call
   hipEvent_t ev_done[2] = {nullptr, nullptr};
-  bool pending[2] = {false, false}; // decode on slot k not yet joined onto a caller stream
+  bool pending[2] = {false, false}; // decode on slot k not yet joined onto its caller's stream
+  hipStream_t caller[2] = {nullptr, nullptr}; // the caller stream that issued slot k's pending decode
   int next = 0;
+  int device = 0; // (close never touches the contexts: they may be closed already)
 };
 
 namespace {
@@ -52,7 +54,8 @@ extern "C" int amod_pipe_open(amod_ctx *a, amod_ctx *b, amod_pipe **out) {
   auto *p = new amod_pipe;
   p->ctx[0] = a;
   p->ctx[1] = b;
-  hipError_t e = hipSetDevice(amod_ctx_device(a));
+  p->device = amod_ctx_device(a);
+  hipError_t e = hipSetDevice(p->device);
   for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&p->slot[k], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming);
   for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&p->ev_done[k], hipEventDisableTiming);
@@ -67,7 +70,7 @@ extern "C" int amod_pipe_open(amod_ctx *a, amod_ctx *b, amod_pipe **out) {
 
 extern "C" int amod_pipe_close(amod_pipe *p) {
   if (!p) return AMOD_SUCCESS;
-  (void)hipSetDevice(amod_ctx_device(p->ctx[0]));
+  (void)hipSetDevice(p->device);
   for (hipStream_t s : p->slot)
     if (s) {
       (void)hipStreamSynchronize(s);
@@ -87,7 +90,7 @@ extern "C" int amod_pipe_decode_device(amod_pipe *p, const amod_cfg *cfg, int32_
                                        amod_result *results, uint8_t *payload, int64_t payload_stride,
                                        uint32_t options, void *stream) {
   if (!p) return amod_ctx_fail(nullptr, "null pipe", AMOD_ERR_ARG);
-  PIPE_TRY(p, hipSetDevice(amod_ctx_device(p->ctx[0])));
+  PIPE_TRY(p, hipSetDevice(p->device));
   const int k = p->next;
   amod_ctx *c = p->ctx[k];
   hipStream_t w = p->slot[k];
@@ -107,22 +110,33 @@ extern "C" int amod_pipe_decode_device(amod_pipe *p, const amod_cfg *cfg, int32_
   if (s) {
     PIPE_TRY(p, hipEventRecord(p->ev_done[k], w));
     p->pending[k] = true;
-    // the previous decode (the other slot) is joined now, after this one's start was recorded
-    if (p->pending[k ^ 1]) {
-      PIPE_TRY(p, hipStreamWaitEvent(s, p->ev_done[k ^ 1], 0));
-      p->pending[k ^ 1] = false;
-    }
+    p->caller[k] = s;
+  }
+  // the previous decode (the other slot) is joined now, after this one's start was
+  // recorded, onto the stream that issued it (whatever this call passed)
+  if (p->pending[k ^ 1]) {
+    PIPE_TRY(p, hipStreamWaitEvent(p->caller[k ^ 1], p->ev_done[k ^ 1], 0));
+    p->pending[k ^ 1] = false;
   }
   return AMOD_SUCCESS;
 }
 
 extern "C" int amod_pipe_flush(amod_pipe *p, void *stream) {
   if (!p) return amod_ctx_fail(nullptr, "null pipe", AMOD_ERR_ARG);
-  if (!stream) return AMOD_SUCCESS; // (slot-stream callers: their results are in stream order)
-  PIPE_TRY(p, hipSetDevice(amod_ctx_device(p->ctx[0])));
+  PIPE_TRY(p, hipSetDevice(p->device));
+  if (!stream) { // slot-stream callers: their results are in stream order; a pending
+                 // caller-stream decode is joined onto the stream that issued it
+    for (int k = 0; k < 2; ++k)
+      if (p->pending[k]) {
+        PIPE_TRY(p, hipStreamWaitEvent(p->caller[k], p->ev_done[k], 0));
+        p->pending[k] = false;
+      }
+    return AMOD_SUCCESS;
+  }
   for (int k = 0; k < 2; ++k)
-    if (p->pending[k]) {
-      PIPE_TRY(p, hipStreamWaitEvent((hipStream_t)stream, p->ev_done[k], 0));
+    if (p->pending[k]) { // onto the stream that issued it, and onto the one flushed
+      PIPE_TRY(p, hipStreamWaitEvent(p->caller[k], p->ev_done[k], 0));
+      if (p->caller[k] != (hipStream_t)stream) PIPE_TRY(p, hipStreamWaitEvent((hipStream_t)stream, p->ev_done[k], 0));
       p->pending[k] = false;
     }
   return AMOD_SUCCESS;
@@ -130,7 +144,7 @@ extern "C" int amod_pipe_flush(amod_pipe *p, void *stream) {
 
 extern "C" int amod_pipe_synchronize(amod_pipe *p) {
   if (!p) return amod_ctx_fail(nullptr, "null pipe", AMOD_ERR_ARG);
-  PIPE_TRY(p, hipSetDevice(amod_ctx_device(p->ctx[0])));
+  PIPE_TRY(p, hipSetDevice(p->device));
   for (hipStream_t s : p->slot) PIPE_TRY(p, hipStreamSynchronize(s));
   p->pending[0] = p->pending[1] = false;
   return AMOD_SUCCESS;

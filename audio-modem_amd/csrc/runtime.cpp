@@ -324,6 +324,9 @@ void read_knobs(amod::Knobs &k) {
   k.no_gap_scan = getenv("AMOD_NO_GAP_SCAN") != nullptr;
   k.stream_threads = env_int("AMOD_STREAM_THREADS", -1);
   k.stream_fullcopy = getenv("AMOD_STREAM_FULLCOPY") != nullptr;
+  k.ema_per = env_int("AMOD_EMA_PER", -1);
+  k.ema_warm = env_int("AMOD_EMA_WARM", -1);
+  k.ema_rounds = env_int("AMOD_EMA_ROUNDS", -1);
 }
 
 int fail(amod_ctx *ctx, const std::string &msg, int code) {
@@ -766,7 +769,9 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   HIP_TRY(mark(4));
   wb.fb_reset = fb; // list A's count, zeroed for the next decode (or replay)
   HIP_TRY(amod_launch_exact(d, wb, xslots, s)); // list B: frames k_demod listed
-  ctx->fb_zeroed = xslots > 0;
+  // a captured decode does not run here: its launches (the reset included) exist only in
+  // the graph, so the next eager decode must zero the counters itself
+  ctx->fb_zeroed = xslots > 0 && cap == hipStreamCaptureStatusNone;
   HIP_TRY(mark(5));
   if (ctx->profiling) {
     ctx->ev_used.push_back(ev);

@@ -1042,13 +1042,13 @@ struct Prepass {
     double *const wd_ = c->d_warm.as<double>(), *const ed = c->d_end.as<double>(), *const sd = c->d_scr.as<double>();
     if (device) {
       x = samples;
-      S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), 0, n, s));
+      S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), 0, n, s, kn));
     } else {
       // the host samples go up in pieces on the upload stream (HIP's pageable copy runs at
       // ~51 GB/s in 64 MB pieces, ~14 GB/s as one multi-GB copy), and each piece's EMA
       // waves run on s as soon as it has landed (they read only it and the pieces before)
       x = c->d_x.as<float>();
-      const int64_t wsz = amod_ema_wave_samples();
+      const int64_t wsz = amod_ema_wave_samples(kn);
       const int64_t P = std::max<int64_t>(1, kUpPieceSamples / wsz) * wsz;
       const int64_t npc = (n + P - 1) / P;
       if (!c->s_up) S_TRY(hipStreamCreateWithFlags(&c->s_up, hipStreamNonBlocking));
@@ -1067,10 +1067,10 @@ struct Prepass {
                                hipMemcpyHostToDevice, c->s_up));
         S_TRY(hipEventRecord(c->up_ev[q], c->s_up));
         S_TRY(hipStreamWaitEvent(s, c->up_ev[q], 0));
-        S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), a, b, s));
+        S_TRY(amod_launch_ema_part(x, nvalid, n, yd, wd_, ed, sd, c->d_apow.as<double>(), a, b, s, kn));
       }
     }
-    S_TRY(amod_launch_ema_fix(x, nvalid, n, yd, wd_, ed, c->d_list.as<int64_t>(), c->d_fixed.as<unsigned long long>(), s));
+    S_TRY(amod_launch_ema_fix(x, nvalid, n, yd, wd_, ed, c->d_list.as<int64_t>(), c->d_fixed.as<unsigned long long>(), s, kn));
     S_TRY(hipEventRecord(ev[1], s));
     S_TRY(amod_launch_sc_screen(c->d_y.as<float>(), n, 0.25f, c->d_ze.as<double2>(), c->d_hot.as<uint8_t>(), s));
     // the fine ranges (every position within 448 samples of a hot block), built on the GPU
@@ -1369,7 +1369,7 @@ extern "C" int amod_dc_remove_device(amod_ctx *ctx, const float *x, int64_t n, f
   for (auto &v : ap) { v = a; a *= 0.999; }
   S_TRY(hipMemcpyAsync(apow.p, ap.data(), sizeof(double) * ap.size(), hipMemcpyHostToDevice, s));
   S_TRY(amod_launch_ema(x, n, n, y, warm.as<double>(), end.as<double>(), scr.as<double>(), list.as<int64_t>(),
-                        apow.as<double>(), fixed.as<unsigned long long>(), s));
+                        apow.as<double>(), fixed.as<unsigned long long>(), s, amod_ctx_knobs(ctx)));
   double e = 0.0;
   unsigned long long fx = 0;
   S_TRY(hipMemcpyAsync(&e, end.as<double>() + nch - 1, sizeof(double), hipMemcpyDeviceToHost, s));

@@ -43,7 +43,40 @@ SAMPLES_PER_FRAME_C3 = 30114  # C3: 16-QAM 1 KB legacy frame
 PAYLOAD = 1024
 PAYLOAD_C5 = 256
 CHUNK = 2048                  # C4: data bytes per chunk frame
-HOST_THREADS = 16             # the GPU box's CPU share (os.cpu_count() shows the whole machine)
+
+
+def host_threads():
+    """(threads, where the number came from): the CPUs this process may run on
+    (sched_getaffinity), capped by the cgroup CPU quota (cgroup v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us) and by OMP_NUM_THREADS, which the GPU box sets to its
+    CPU share (os.cpu_count() shows the whole machine there)."""
+    import math
+    n = len(os.sched_getaffinity(0))
+    src = [f"sched_getaffinity {n}"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        src.append(f"cgroup quota {quota:g}")
+        n = min(n, max(1, math.ceil(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        src.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, int(omp))
+    return max(1, n), ", ".join(src)
+
+
+HOST_THREADS, HOST_THREADS_SOURCE = host_threads()
 FLAG_NAMES = {0: "FORCED", 1: "NONFINITE", 2: "BIG", 3: "COARSE", 4: "FINE", 5: "CHANNEL", 6: "PHASE", 7: "DEMAP",
               8: "THRESH", 9: "SPAN", 10: "SOFT", 11: "REPLAY"}
 
@@ -781,7 +814,8 @@ def js_baseline(wl: Workload, x, nframes, seconds=1.5, single_frames=60, single_
     if r.returncode != 0:
         return {"error": r.stderr[-400:]}
     j = json.loads(r.stdout)
-    out = {"value": j["all_cores"], "unit": "samples/s", "cores": j["threads"], "kind": "port",
+    out = {"value": j["all_cores"], "unit": "samples/s", "cores": j["threads"], "cores_source": HOST_THREADS_SOURCE,
+           "kind": "port",
            "sample": f"{nframes} {wl.name()} frames dealt round-robin to {j['threads']} worker_threads, each repeating "
                      f"its share for {seconds} s ({j['all_cores_samples']} samples in {j['all_cores_seconds']:.2f} s); "
                      f"{j['single_core_frames']} frames on 1 thread; oracle/rx_cpu.js (JS restatement of modem.js, "

@@ -181,9 +181,12 @@ int amod_synchronize(amod_ctx *ctx);
  * inputs on amod_pipe_next_stream(p) (hipStream_t), decode, and read its results on that
  * same stream: plain stream order. With another `stream`, a decode starts once that
  * stream reaches the call, and decode i's results are ordered on it when decode i + 1 has
- * been enqueued, or after amod_pipe_flush(stream) (two cross-queue signals per batch: less
+ * been enqueued (whatever stream that call passes: the join goes to the stream that issued
+ * decode i), or after amod_pipe_flush(stream) (two cross-queue signals per batch: less
  * overlap). amod_pipe_synchronize waits on the host. One host thread per pipe; the
- * contexts must outlive it and take no other work while it runs. */
+ * contexts must take no other work while it runs, and a context closed before the pipe
+ * must have its pipe decodes finished first (amod_pipe_synchronize / amod_pipe_close;
+ * the Python Demodulator closes its pipes itself). */
 typedef struct amod_pipe amod_pipe;
 int amod_pipe_open(amod_ctx *a, amod_ctx *b, amod_pipe **out);
 int amod_pipe_close(amod_pipe *p); /* waits for its decodes and destroys its two streams;

@@ -70,6 +70,21 @@ async function main() {
             afterFree };
           break;
         }
+        case 'decode_resident_concurrent': {
+          // two decodes of ONE DeviceBatch in flight at once, with different modulations (the
+          // payload stride differs): each must equal the same decode run alone
+          const b = M.uploadBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { devices: j.devices });
+          const alone = [];
+          for (const m of j.mods) alone.push(await M.decodeBatch(b, null, null, m, j.rep, { mode: j.mode }));
+          let same = true;
+          for (let it = 0; it < 4; ++it) {
+            const got = await Promise.all(j.mods.map((m) => M.decodeBatch(b, null, null, m, j.rep, { mode: j.mode })));
+            same = same && JSON.stringify(enc(got)) === JSON.stringify(enc(alone));
+          }
+          b.free();
+          r = { same, first: alone[0] };
+          break;
+        }
         case 'asm': {
           // one ChunkAssembler scenario (tests/golden/assembler.json ops); state after each op
           const a = new M.ChunkAssembler(j.directory ? { directory: j.directory } : undefined);

@@ -118,3 +118,58 @@ def test_replay_after_workspace_growth():
         assert np.array_equal(pay.cpu().numpy(), ref_pay), k
     del g
     dm.close()
+
+
+def test_eager_decode_after_capture_before_replay():
+    """amod_reserve, then capture, then an EAGER decode before the first replay,
+    then replays. The captured decode's counter reset exists only in the graph, so the
+    eager decode must zero the exact-list counters itself; frames are listed (wide guard
+    bands) so a stale list count would put list writes out of place."""
+    import torch
+    cfg = amodem.preset("acoustic", "BPSK", 3)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, 24, payload_len=64, threads=8)
+    sp = float(np.mean(x[x != 0] ** 2))
+    rng = np.random.default_rng(11)
+    x = (x + rng.standard_normal(len(x)).astype(np.float32) * np.float32(np.sqrt(sp / 10 ** 0.6))).astype(np.float32)
+    F, N = len(offs), int(lens.max())
+    dev = torch.device("cuda", 0)
+    xs = torch.zeros(len(x) + 16, dtype=torch.float32, device=dev)
+    xs[:len(x)].copy_(torch.from_numpy(x))
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    stride = amodem.payload_stride(cfg, N)
+    res = torch.zeros(F * 96, dtype=torch.uint8, device=dev)
+    pay = torch.zeros(F * stride, dtype=torch.uint8, device=dev)
+    dm = open_with_env(0, AMOD_GUARD_SCALE=50)
+    dm.reserve(cfg, F, N)
+    s = torch.cuda.Stream()
+
+    def decode():
+        dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
+                         res.data_ptr(), pay.data_ptr(), stride, stream=torch.cuda.current_stream().cuda_stream)
+
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):  # the context's first decode is the captured one
+        decode()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        decode()  # eager, before any replay
+    torch.cuda.synchronize()
+    ref_res, ref_pay = res.cpu().numpy().copy(), pay.cpu().numpy().copy()
+    rec = np.frombuffer(ref_res.tobytes(), amodem.RESULT_DTYPE)
+    assert ((rec["flags"] & (L.FLAG_EXACT | L.FLAG_REPLAY)) != 0).sum() > 0, np.unique(rec["flags"])
+    r2, p2 = dm.decode_batch(x, offs, lens, cfg=cfg, stride=stride)  # host path: a third decode
+    assert np.array_equal(r2.tobytes(), ref_res.tobytes())
+    for k in range(3):
+        res.zero_()
+        pay.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(res.cpu().numpy(), ref_res), k
+        assert np.array_equal(pay.cpu().numpy(), ref_pay), k
+        with torch.cuda.stream(s):
+            decode()  # eager between replays
+        torch.cuda.synchronize()
+        assert np.array_equal(res.cpu().numpy(), ref_res), k
+    del g
+    dm.close()

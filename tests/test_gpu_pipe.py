@@ -142,3 +142,47 @@ def test_pipeline_arguments():
     with pytest.raises(RuntimeError):
         a.pipeline(a)  # two distinct contexts
     a.close()
+
+
+def test_pipeline_stream_switch_and_close_order():
+    """a decode issued with a caller stream is joined onto THAT stream when the
+    next decode is enqueued, even if the next call passes no stream (slot mode), and a
+    Demodulator closed before its Pipeline finishes and closes the pipe first."""
+    import torch
+    bs = _batches()[:3]
+    F = max(len(b[3]) for b in bs)
+    N = max(int(b[4].max()) for b in bs)
+    cfg = bs[0][0]
+    stride = amodem.payload_stride(cfg, N)
+    dev = torch.device("cuda", 0)
+    ins = [_dev(torch, b) for b in bs]
+    a, b2 = amodem.Demodulator(0), amodem.Demodulator(0)
+    for dm in (a, b2):
+        dm.reserve(cfg, F, N)
+    pipe = a.pipeline(b2)
+    s = torch.cuda.Stream(dev)
+    bufs = [(torch.zeros(F * 96, dtype=torch.uint8, device=dev), torch.zeros(F * stride, dtype=torch.uint8, device=dev))
+            for _ in range(3)]
+    # decode 0 on the caller stream s, decode 1 in slot mode (no stream): decode 0 must be
+    # ordered on s after the second call
+    b, (xs, do, dl) = bs[0], ins[0]
+    with torch.cuda.stream(s):
+        pipe.decode_device(cfg, b[1], xs.data_ptr(), do.data_ptr(), dl.data_ptr(), len(b[3]), bufs[0][0].data_ptr(),
+                           bufs[0][1].data_ptr(), stride, stream=s.cuda_stream)
+    b, (xs, do, dl) = bs[1], ins[1]
+    pipe.decode_device(cfg, b[1], xs.data_ptr(), do.data_ptr(), dl.data_ptr(), len(b[3]), bufs[1][0].data_ptr(),
+                       bufs[1][1].data_ptr(), stride)
+    with torch.cuda.stream(s):
+        r0 = bufs[0][0][:len(bs[0][3]) * 96].cpu().numpy()
+    rec = np.frombuffer(r0.tobytes(), amodem.RESULT_DTYPE)
+    assert ((rec["status"] == 0) & (rec["crc_valid"] == 1)).all()
+    # a third decode in flight, then the Demodulator closed under it: the pipe goes first
+    b, (xs, do, dl) = bs[2], ins[2]
+    pipe.decode_device(cfg, b[1], xs.data_ptr(), do.data_ptr(), dl.data_ptr(), len(b[3]), bufs[2][0].data_ptr(),
+                       bufs[2][1].data_ptr(), stride)
+    a.close()
+    assert pipe._h is None
+    torch.cuda.synchronize()
+    rec = np.frombuffer(bufs[2][0][:len(bs[2][3]) * 96].cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
+    assert ((rec["status"] == 0) & (rec["crc_valid"] == 1)).all()
+    b2.close()

@@ -230,6 +230,27 @@ def test_resident_batch_through_js(tmp_path):
     assert got["afterFree"] and "freed" in got["afterFree"]
 
 
+@pytest.mark.gpu
+def test_resident_batch_concurrent_decodes(tmp_path):
+    """two decodeBatch(DeviceBatch) promises in flight on one resident batch,
+    with different modulations (different payload strides; the batch was reserved for
+    QPSK, so the other is the narrower BPSK), run on the libuv pool at
+    once; amod_resident_decode serialises them, so each equals the same decode alone."""
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["mod"] == "QPSK"
+           and f["rep"] == 1]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    res = run([{"op": "decode_resident_concurrent", "config": "standard", "file": str(fn), "offsets": offs,
+                "lengths": [len(x) for x in xs], "mod": "QPSK", "mods": ["QPSK", "BPSK", "QPSK"], "rep": 1,
+                "devices": 2, "id": "c"}], tmp_path, env={"AMODEM_GROUP_DEVICES": "0,0"})
+    got = ok(res, "c")
+    assert got["same"]
+    assert got["first"] == [f["result"] for f in sel]
+
+
 def _lb_num(v):
     return float(v["num"]) if isinstance(v, dict) else float(v)
 
