@@ -29,6 +29,7 @@
 #include "amodem_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace amod {
 namespace {
@@ -440,6 +441,16 @@ __device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) 
                "v_add_f32_dpp %3, %3, %3 row_bcast:31 row_mask:0xc bank_mask:0xf"
                : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
   a = rlane(a, 63); b = rlane(b, 63); c = rlane(c, 63); d = rlane(d, 63);
+}
+// the same four sums over row 0 only (lanes 0 .. 15; the pilot lanes of every built-in
+// preset): the row reductions alone, then lane 0
+__device__ __forceinline__ void wsum16_4(float &a, float &b, float &c, float &d) {
+#define AMOD_W4(ctrl)                                                                   \
+  { const float ta = AMOD_DPP_F(a, ctrl), tb = AMOD_DPP_F(b, ctrl), tc = AMOD_DPP_F(c, ctrl), td = AMOD_DPP_F(d, ctrl); \
+    a += ta; b += tb; c += tc; d += td; }
+  AMOD_W4(0xB1) AMOD_W4(0x4E) AMOD_W4(0x141) AMOD_W4(0x140)
+#undef AMOD_W4
+  a = rlane(a, 0); b = rlane(b, 0); c = rlane(c, 0); d = rlane(d, 0);
 }
 __device__ __forceinline__ float wmax_b(float v) {
   v = fmaxf(v, AMOD_DPP_F(v, 0xB1)); v = fmaxf(v, AMOD_DPP_F(v, 0x4E));
@@ -1395,14 +1406,28 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
   }
   return r;
 }
-constexpr int CRC_ILP = 4;
-// chunks are LEFT-aligned here (chunk j = bytes [16 j, 16 j + 16), the last one zero-padded
-// to a whole chunk), so lane j reads its chunk as one ds_read_b128 (lanes 16 B apart: no
-// bank conflicts; the right-aligned chunks of round 3 took two unaligned ds_read_b32 per
-// word, lanes four words apart: 4-way). Chunk 0 starts from the reference's ~0; the
-// register of the padded message is moved back over the pad's zero bytes at the end by
-// crc_unpad[pad] (the inverse zero-byte operator, the workgroup's LDS copy of
-// t.crc_unpad: a global read there was one more dependent round trip per frame end).
+// XOR over the wave to a wave-uniform value: DPP row reductions, then the two row
+// broadcasts as DPP xors into v itself (the rows a broadcast does not enable keep theirs)
+__device__ __forceinline__ uint32_t wave_xor_dpp(uint32_t x) {
+  int v = (int)x;
+  v ^= AMOD_DPP_I(v, 0xB1); v ^= AMOD_DPP_I(v, 0x4E); v ^= AMOD_DPP_I(v, 0x141); v ^= AMOD_DPP_I(v, 0x140);
+  asm volatile("s_nop 1\n"
+               "v_xor_b32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+               "s_nop 1\n"
+               "v_xor_b32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               : "+v"(v));
+  return (uint32_t)__builtin_amdgcn_readlane(v, 63);
+}
+// chunks are LEFT-aligned (chunk j = bytes [16 j, 16 j + 16), the last one zero-padded to a
+// whole chunk), read as one ds_read_b128 each. Lane l hashes the CONTIGUOUS chunks
+// [n l, n l + n) (n = ceil(nch / 64)) in sequence, the register carried from chunk to chunk,
+// so each lane moves its register to the message end once, by the GF(2) zero-shift matrix
+// of the chunks after its range (round 4 gave lane l the chunks l, l + 64, ... and shifted
+// each: three matrix products per lane on C4, each behind eight global reads of its
+// matrix; the frame-end CRC was 15.7 k of a frame's 201 k wave cycles there). Chunk 0 starts
+// from the reference's ~0; the register of the padded message is moved back over the pad's
+// zero bytes at the end by crc_unpad[pad] (the inverse zero-byte operator, the workgroup's
+// LDS copy of t.crc_unpad).
 __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const DevTables &t, const uint32_t *t4l,
                                                const uint32_t *crc_unpad, unsigned long long *stp = nullptr) {
   const int lane = wave_lane();
@@ -1410,45 +1435,32 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const D
   const uint32_t *const t4 = t4l;
   const int nch = (L + kCrcChunk - 1) / kCrcChunk;
   const int pad = kCrcChunk * nch - L;
-  uint32_t acc = 0;
-  for (int q0 = 0; q0 < nch; q0 += 64 * CRC_ILP) {
-    uint32_t c[CRC_ILP];
-    uint4 wd[CRC_ILP];
-#pragma unroll
-    for (int k = 0; k < CRC_ILP; ++k) {
-      const int j = q0 + 64 * k + lane; // chunk index from the message start
-      c[k] = j == 0 ? 0xFFFFFFFFu : 0u;
-      wd[k] = make_uint4(0, 0, 0, 0);
-      if (q0 + 64 * k < nch && j < nch) { // (wave-uniform first test)
-        wd[k] = reinterpret_cast<const uint4 *>(v)[j];
-        if (j == nch - 1 && pad) { // bytes past L read as zero (MSB-first words)
-          const int nv = kCrcChunk - pad; // valid bytes of this chunk, 1 .. 15
-          const auto keep = [&](int st) -> uint32_t {
-            const int b = nv - 4 * st;
-            return b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * b));
-          };
-          wd[k].x &= keep(0); wd[k].y &= keep(1); wd[k].z &= keep(2); wd[k].w &= keep(3);
-        }
+  const int n = (nch + 63) >> 6; // chunks per lane (wave-uniform)
+  const int j0 = n * lane, j1 = min(j0 + n, nch);
+  uint32_t c = lane == 0 ? 0xFFFFFFFFu : 0u;
+  for (int q = 0; q < n; ++q) { // (wave-uniform trip count; a lane past its range idles)
+    const int j = j0 + q;
+    if (j < nch) {
+      uint4 wd = reinterpret_cast<const uint4 *>(v)[j];
+      if (j == nch - 1 && pad) { // bytes past L read as zero (MSB-first words)
+        const int nv = kCrcChunk - pad; // valid bytes of this chunk, 1 .. 15
+        const auto keep = [&](int st) -> uint32_t {
+          const int b = nv - 4 * st;
+          return b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * b));
+        };
+        wd.x &= keep(0); wd.y &= keep(1); wd.z &= keep(2); wd.w &= keep(3);
       }
-    }
 #pragma unroll
-    for (int st = 0; st < kCrcChunk / 4; ++st) {
-#pragma unroll
-      for (int k = 0; k < CRC_ILP; ++k) {
-        if (q0 + 64 * k >= nch) continue; // wave-uniform
-        const uint32_t wv = st == 0 ? wd[k].x : st == 1 ? wd[k].y : st == 2 ? wd[k].z : wd[k].w;
-        const uint32_t x = c[k] ^ __builtin_bswap32(wv);
-        c[k] = t4[768 + (x & 0xFF)] ^ t4[512 + ((x >> 8) & 0xFF)] ^ t4[256 + ((x >> 16) & 0xFF)] ^ t4[x >> 24];
+      for (int st = 0; st < kCrcChunk / 4; ++st) {
+        const uint32_t wv = st == 0 ? wd.x : st == 1 ? wd.y : st == 2 ? wd.z : wd.w;
+        const uint32_t x = c ^ __builtin_bswap32(wv);
+        c = t4[768 + (x & 0xFF)] ^ t4[512 + ((x >> 8) & 0xFF)] ^ t4[256 + ((x >> 16) & 0xFF)] ^ t4[x >> 24];
       }
-    }
-    if (stp && lane == 0 && q0 == 0) stp[31] = __builtin_amdgcn_s_memtime(); // (chunk registers)
-#pragma unroll
-    for (int k = 0; k < CRC_ILP; ++k) {
-      const int j = q0 + 64 * k + lane;
-      if (q0 + 64 * k < nch && j < nch) acc ^= crc_shift(t.crc_mat, nch - 1 - j, c[k]);
     }
   }
-  const uint32_t reg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_xor(acc));
+  if (stp && lane == 0) stp[31] = __builtin_amdgcn_s_memtime(); // (chunk registers)
+  const uint32_t acc = j0 < nch ? crc_shift(t.crc_mat, nch - j1, c) : 0u;
+  const uint32_t reg = wave_xor_dpp(acc);
   return (pad ? crc_shift(crc_unpad, pad, reg) : reg) ^ 0xFFFFFFFFu;
 }
 
@@ -1535,6 +1547,67 @@ __device__ __forceinline__ void wave_vote(const uint32_t *bits, int nbits, int r
   }
 }
 
+// parse_stream (amodem_internal.h: modem.js:605-654, 805-849, 793-802) with the same
+// decisions in the same order, reading words instead of bytes: the first 16 bytes in one
+// ds_read_b128, then each field at a data-dependent offset as one pair of words, so a parse
+// is two (chunk / metadata) or three (legacy) dependent LDS round trips (the byte reads
+// were one per field byte)
+__device__ __forceinline__ uint32_t be32_word(const uint32_t *v, int i) {
+  const int wi = i >> 2, sh = 8 * (i & 3);
+  const uint32_t a = v[wi], b = v[wi + 1];
+  return sh ? (a << sh) | (b >> (32 - sh)) : a;
+}
+__device__ __forceinline__ int parse_fast(const uint32_t *v, int nbytes, int mode, amod_result &r) {
+  r.nbytes = nbytes;
+  const int min_bytes = mode == AMOD_MODE_CHUNK ? 6 : 10;
+  if (nbytes < min_bytes) { r.status = AMOD_E_DECODED_SHORT; r.frame_type = -1; return -1; }
+  const uint4 h = *reinterpret_cast<const uint4 *>(v); // bytes 0 .. 15 (MSB-first words)
+  const int t = (int)(h.x >> 24);
+  if (t == 0xFE) {
+    r.frame_type = 0xFE;
+    if (nbytes < 16) { r.status = AMOD_E_META_SHORT; return -1; }
+    r.total_chunks = (int32_t)((h.x << 8) | (h.y >> 24));
+    r.total_size = (int32_t)((h.y << 8) | (h.z >> 24));
+    r.chunk_size = (int32_t)((h.z >> 8) & 0xFFFFu);
+    const int nl = (int)(h.z & 0xFFu);
+    int off = 12;
+    if (off + nl + 4 > nbytes) { r.status = AMOD_E_META_TRUNC; return -1; }
+    r.name_off = off; r.name_len = nl;
+    off += nl;
+    r.expected_crc = be32_word(v, off);
+    r.status = AMOD_OK;
+    return off;
+  }
+  if (t == 0xFF) {
+    r.frame_type = 0xFF;
+    if (nbytes < 11) { r.status = AMOD_E_CHUNK_SHORT; return -1; }
+    r.seq_num = (int32_t)((h.x << 8) | (h.y >> 24));
+    const int dl = (int)((h.y >> 8) & 0xFFFFu);
+    int off = 7;
+    if (off + dl + 4 > nbytes) { r.status = AMOD_E_CHUNK_TRUNC; return -1; }
+    r.data_off = off; r.data_len = dl;
+    off += dl;
+    r.expected_crc = be32_word(v, off);
+    r.status = AMOD_OK;
+    return off;
+  }
+  if (mode == AMOD_MODE_CHUNK) { r.frame_type = t; r.aux = t; r.status = AMOD_E_UNKNOWN_TYPE; return -1; }
+  r.frame_type = 0;
+  const int nl = t;
+  int off = 1;
+  if (off + nl + 4 + 4 > nbytes) { r.status = AMOD_E_SHORT_HEADER; return -1; }
+  r.name_off = off; r.name_len = nl;
+  off += nl;
+  const int32_t dl = (int32_t)be32_word(v, off);
+  off += 4;
+  if (dl <= 0 || (int64_t)off + dl + 4 > nbytes) { r.status = AMOD_E_INVALID_LEN; r.aux = dl; return -1; }
+  r.data_off = off; r.data_len = dl;
+  off += dl;
+  r.expected_crc = be32_word(v, off);
+  r.status = AMOD_OK;
+  return off;
+}
+
 // the longest prefix parse_need reads: a legacy header (1 + 255 + 4 bytes)
 constexpr int kHeaderMaxBytes = 1 + 255 + 4;
 
@@ -1600,22 +1673,40 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   const int bo0 = (lane - sub_start) & 63;
   const int jk = 2 * ndata + 64;
   uint32_t di_pk[2] = {0u, 0u};
-  // the slot rr of this lane's pilot (-1: none); the built-in presets never put two
-  // pilots on one lane (pil_multi selects the general per-slot loop otherwise)
-  int prr = -1, npl = 0;
 #pragma unroll
   for (int rr = 3; rr >= 0; --rr) {
     const int di = bo0 + 64 * rr < nband ? (int)cfg.t.band_di[bo0 + 64 * rr] : -2;
     const int dib = di >= 0 ? di * BPS : BPS * (jk + lane + (di == -2 ? 64 : 0));
     di_pk[rr >> 1] |= ((uint32_t)dib & 0xFFFFu) << (16 * (rr & 1));
-    if (di == -1) { prr = rr; ++npl; }
   }
   auto dib_of = [&](int rr) { return (int)(int16_t)(di_pk[rr >> 1] >> (16 * (rr & 1))); };
-  auto pilot_slot = [&](int rr) { const int b = dib_of(rr); return b >= BPS * jk && b < BPS * (jk + 64); };
-  const bool pil_multi = __ballot(npl > 1) != 0;
-  uint32_t kn_neg = 0; // CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol): bit rr
+  // kn_neg bit rr: the CE sign of the lane's band subcarrier rr is -1 (generateChannelEstSymbol);
+  // bit 4 + rr: slot rr holds no data subcarrier (a pilot, or none: its decision margin is
+  // passed over); bit 8: the lane holds a pilot, bit 9: that pilot's CE sign is -1
+  uint32_t kn_neg = 0;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) kn_neg |= (uint32_t)(bo0 + 64 * rr < nband && cfg.t.known[bo0 + 64 * rr] < 0.f) << rr;
+  for (int rr = 0; rr < 4; ++rr) {
+    kn_neg |= (uint32_t)(bo0 + 64 * rr < nband && cfg.t.known[bo0 + 64 * rr] < 0.f) << rr;
+    kn_neg |= (uint32_t)(dib_of(rr) >= BPS * jk) << (4 + rr);
+  }
+  // The pilots are evaluated on lanes of their own: lane p < npilots takes the list's pilot
+  // p (the reference loops over OFDM.PILOTS, duplicates included, and skips pilots outside
+  // the band: modem.js:398-405), reading its two bins Z[k], Z[512 - k] from the spectrum, so
+  // the phase sums reduce over the first 16 lanes (row 0) for every built-in preset and no
+  // lane selects its pilot slot out of four. paddr: the LDS byte addresses of the two bins
+  // (16 bits each); gp: 1/H at the pilot, set by job 0 like a band slot's G
+  uint32_t paddr;
+  {
+    const int np = cfg.npilots;
+    const int kp = lane < np ? cfg.pilots[min(lane, AMOD_MAX_PILOTS - 1)] : -1;
+    const bool pin = kp >= sub_start && kp <= cfg.sub_end;
+    const int kq = pin ? kp : sub_start; // (a lane without a pilot reads a valid bin)
+    const uint32_t a0 = lds_addr(X2 + spec_idx(kq)), a1 = lds_addr(X2 + spec_idx((kFft - kq) & (kFft - 1)));
+    paddr = a0 | (a1 << 16);
+    kn_neg |= (uint32_t)pin << 8;
+    kn_neg |= (uint32_t)(pin && cfg.t.known[kq - sub_start] < 0.f) << 9;
+  }
+  const bool pil16 = cfg.npilots <= 16; // (wave-uniform) the pilot sums reduce over row 0
 
   // Frames (last-first: frame f1 - 1 - k for the k-th) by a static stride for the first
   // rounds, then one at a time from the claim counter (w.claim). Waves on one SIMD do not
@@ -1688,6 +1779,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
   };
 
   float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
+  f2v gp = {0.f, 0.f};        // G = 1/H at the lane's pilot (job 0)
   float gmax = 0.f, zce = 0.f; // guard scales of the frame (job 0)
   // state of the frame being demodulated (wave-uniform): jobs it takes (shrinks once the
   // header says how many bytes the parse reads), those bytes (-1: not yet known), the
@@ -1773,13 +1865,11 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       }
       DSTAMP(16, jcur == 1);
       DSTAMP(27, jcur == 2); // (job 2 samples ready: minus mark 21 = the wait for its loads)
-#ifdef AMOD_LOAD_FENCE
-      // (experiment) the FFT input formed before the next job's loads are issued: the
-      // compiler otherwise issues the loads first and copies the samples out of their
-      // target registers
+      // the FFT input is formed before the next job's loads are issued (the compiler
+      // otherwise issued the loads first and copied the samples out of their target
+      // registers: eight v_mov_b64 per job; C4 k_demod -1.6 %, C5 -2.5 %)
       asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                    "+v"(v[7])::"memory");
-#endif
       issue_next(); // the samples are in v: the next job's loads fly under this FFT too
       if (!KO(16)) fft512_wave(v, X2, tw1, tw2);
       DSTAMP(17, jcur == 1);
@@ -1787,13 +1877,19 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       asm volatile("" : "+v"(ln)); // per-job lane (keeps debug/bit addresses out of registers)
       // per-job copies of the lane's slot facts: their comparisons are made where they are
       // used instead of held as lane masks across the loop (SGPR pairs that spill)
-      asm volatile("" : "+v"(prr), "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg));
+      asm volatile("" : "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg), "+v"(paddr));
       // the band: slot rr of lane ln is subcarrier b = bo + 64 rr, bins k = k0 + 64 rr and
       // 512 - k (spec_idx(n +- 64) = spec_idx(n) +- 64: one base per side, immediate offsets)
       const int bo = (ln - sub_start) & 63; // (recomputed per job: no VGPR held across the loop)
       const int k0 = sub_start + bo;
       const f2v *const zkp = reinterpret_cast<const f2v *>(X2 + spec_idx(k0));
       const f2v *const znp = reinterpret_cast<const f2v *>(X2 + spec_idx(kFft - 192 - k0));
+      // this lane's pilot bins (lanes without one read a valid bin and mask it)
+      f2v zpk, zpn;
+      {
+        const uint32_t pa = paddr & 0xFFFFu, pb = paddr >> 16;
+        asm volatile("ds_read_b64 %0, %2\n ds_read_b64 %1, %3" : "=v"(zpk), "=v"(zpn) : "v"(pa), "v"(pb));
+      }
       float zm = 0.f;
       // twice the reference's X1, X2 (Z = x1 + i x2: X1 = (Z[k] + conj Z[-k]) / 2,
       // X2 = (Z[k] - conj Z[-k]) / 2i); the 1/2 is folded into G below (exact: powers of 2)
@@ -1804,7 +1900,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         if (rr >= NS) continue; // no subcarrier in this slot
         const f2v zk = zkp[64 * rr], zn = znp[64 * (3 - rr)];
         f2v a = pk_add_conj(zk, zn), c = pk_add_swap_neg(zk, zn);
-        float zz = fmaxf(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y));
+        float zz = max3_raw(fabsf(zk.x) + fabsf(zk.y), fabsf(zn.x) + fabsf(zn.y), zm);
         // chunk mode, `x || 0` semantics on the exact path: a NaN/Inf sample makes every bin
         // of Z non-finite (each bin is a sum over all 512 inputs with non-zero weights, and
         // Inf * 0 is NaN), so one bin pair per lane stands in for the 1024 samples
@@ -1814,31 +1910,41 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           const bool in = bo + 64 * rr < nband;
           a = in ? a : f2v{0.f, 0.f};
           c = in ? c : f2v{0.f, 0.f};
-          zz = in ? zz : 0.f;
+          zz = in ? zz : zm;
         }
-        x1[rr] = a; x2[rr] = c; zm = fmaxf(zm, zz);
+        x1[rr] = a; x2[rr] = c; zm = zz;
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zpk), "+v"(zpn));
+      const f2v x1p = pk_add_conj(zpk, zpn), x2p = pk_add_swap_neg(zpk, zpn);
       if (ce) {
         // channel estimate from the CE symbol: H = Y * known (X = +-1, modem.js:431-438).
         // Here h = 2H and g = G / 2 (so x g = X G); |h|^2 = 4 |H|^2 against 4 x the thresholds
         zce = wmax_nn(zm);
         float gm = 0.f;
         int ch = 0;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int b = bo + 64 * rr;
-          const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
-          const float2 h = const1 ? make_float2(0.f, 0.f) : make_float2(x1[rr].x * kn, x1[rr].y * kn);
+        auto inv = [&](f2v x, bool neg) -> float2 {
+          const float kn = neg ? -1.f : 1.f;
+          const float2 h = const1 ? make_float2(0.f, 0.f) : make_float2(x.x * kn, x.y * kn);
           const float m2 = h.x * h.x + h.y * h.y;
           float2 g;
           if (m2 > 4.f * 1e-10f) { const float im2 = __builtin_amdgcn_rcpf(m2); g = make_float2(h.x * im2, -h.y * im2); } // 1 ulp: inside the eq bound
           else g = make_float2(0.5f, 0.f); // G = 1 (passthrough)
+          return g;
+        };
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int b = bo + 64 * rr;
+          const float2 g = inv(x1[rr], (kn_neg >> rr) & 1);
+          const float2 h = make_float2(x1[rr].x, x1[rr].y);
+          const float m2 = const1 ? 0.f : h.x * h.x + h.y * h.y;
           // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
           ch |= b < nband && !const1 && m2 < 4.f * 1e-6f;
           gl[rr] = g;
           if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
-          if (DBG && b < nband) { D->h_re[b] = 0.5f * h.x; D->h_im[b] = 0.5f * h.y; }
+          if (DBG && b < nband) { const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
+            D->h_re[b] = const1 ? 0.f : 0.5f * h.x * kn; D->h_im[b] = const1 ? 0.f : 0.5f * h.y * kn; }
         }
+        { const float2 g = inv(x1p, (kn_neg >> 9) & 1); gp = f2v{g.x, g.y}; }
         gmax = wmax_nn(gm); // half of max |G|
         if (__ballot(ch)) wflags |= AMOD_FLAG_CHANNEL;
       }
@@ -1851,7 +1957,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         const f2v g = f2v{gl[rr].x, gl[rr].y};
         e1[rr] = pk_cmul(x1[rr], g);
         e2[rr] = pk_cmul(x2[rr], g);
-        em = fmaxf(em, fmaxf(fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y)));
+        em = max3_raw(em, fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y));
         const int b = bo + 64 * rr;
         if (DBG && b < nband && (s1 == 0 || s2 == 0)) {
           const bool one = s1 == 0;
@@ -1867,43 +1973,37 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       float d = 4e-6f * guard * gmax * (zm + em * zce);
       d = wmax_nn(d) + 1e-12f;
       const bool live1 = !ce && !const1, live2 = s2 >= 0 && !const2;
-      // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405);
-      // per lane its pilot (at most one per lane: pil_multi takes the per-slot loop)
-      float ps1 = 0.f, pe1 = 0.f, ps2 = 0.f, pe2 = 0.f;
-      int pc1 = 0, pc2 = 0, pflag1 = 0, pflag2 = 0;
-      auto pilot = [&](bool pil, f2v q1e, f2v q2e) {
+      // pilot phase: mean of eqIm/eqRe over pilots with |eqRe| > 1e-6 (modem.js:398-405), on
+      // the pilot lanes
+      float ps1, pe1, ps2, pe2;
+      int pc1, pc2;
+      bool ph_unc1, ph_unc2;
+      {
+        const f2v q1e = pk_cmul(x1p, gp), q2e = pk_cmul(x2p, gp);
+        const bool pil = (kn_neg >> 8) & 1;
         const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
         const bool w1 = pil && a1 > 1e-6f, w2 = pil && a2 > 1e-6f;
-        pc1 += __popcll(__ballot(w1));
-        pc2 += __popcll(__ballot(w2));
+        // (the counts as two 32-bit popcounts: __popcll's 64-bit result compiled to a 64-bit
+        // integer-to-float conversion sequence below)
+        const unsigned long long bw1 = __ballot(w1), bw2 = __ballot(w2);
+        pc1 = __builtin_popcount((uint32_t)bw1) + __builtin_popcount((uint32_t)(bw1 >> 32));
+        pc2 = __builtin_popcount((uint32_t)bw2) + __builtin_popcount((uint32_t)(bw2 >> 32));
         // v_rcp_f32 (1 ulp): its error is covered by the 1e-6 |ph| term of tau below
         const float q1 = w1 ? __builtin_amdgcn_rcpf(q1e.x) : 0.f;
         const float q2 = w2 ? __builtin_amdgcn_rcpf(q2e.x) : 0.f;
-        ps1 = fmaf(q1, q1e.y, ps1);
-        ps2 = fmaf(q2, q2e.y, ps2);
-        pe1 = fmaf(fabsf(q1), fmaf(fabsf(q1e.y), fabsf(q1), 1.f), pe1);
-        pe2 = fmaf(fabsf(q2), fmaf(fabsf(q2e.y), fabsf(q2), 1.f), pe2);
-        pflag1 |= pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f;
-        pflag2 |= pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f;
-      };
-      if (!pil_multi) { // one pilot slot per lane at most: select it, one evaluation
-        f2v p1 = e1[0], p2 = e2[0];
-#pragma unroll
-        for (int rr = 1; rr < 4; ++rr) {
-          p1 = prr == rr ? e1[rr] : p1;
-          p2 = prr == rr ? e2[rr] : p2;
-        }
-        pilot(prr >= 0, p1, p2);
-      } else {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) pilot(pilot_slot(rr), e1[rr], e2[rr]);
+        ps1 = q1 * q1e.y;
+        ps2 = q2 * q2e.y;
+        pe1 = fabsf(q1) * fmaf(fabsf(q1e.y), fabsf(q1), 1.f);
+        pe2 = fabsf(q2) * fmaf(fabsf(q2e.y), fabsf(q2), 1.f);
+        // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
+        ph_unc1 = __ballot(pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f) != 0;
+        ph_unc2 = __ballot(pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f) != 0;
       }
-      if (!KO(4)) wsum_b4(ps1, pe1, ps2, pe2);
-      else { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
-      // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
-      const bool ph_unc1 = __ballot(pflag1) != 0, ph_unc2 = __ballot(pflag2) != 0;
-      const float ip1 = pc1 > 0 ? __builtin_amdgcn_rcpf((float)pc1) : 0.f;
-      const float ip2 = pc2 > 0 ? __builtin_amdgcn_rcpf((float)pc2) : 0.f;
+      if (KO(4)) { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
+      else if (pil16) wsum16_4(ps1, pe1, ps2, pe2);
+      else wsum_b4(ps1, pe1, ps2, pe2);
+      const float ip1 = pc1 > 0 ? __builtin_amdgcn_rcpf((float)(int32_t)pc1) : 0.f;
+      const float ip2 = pc2 > 0 ? __builtin_amdgcn_rcpf((float)(int32_t)pc2) : 0.f;
       const float ph1 = ps1 * ip1, ph2 = ps2 * ip2;
       const float dp1 = d * pe1 * ip1 + 1e-6f * fabsf(ph1), dp2 = d * pe2 * ip2 + 1e-6f * fabsf(ph2);
       const float tau1 = 4.f * (d * (1.f + fabsf(ph1)) + em * dp1) + 1e-9f;
@@ -1928,65 +2028,85 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
       const int wfirst = gs / DPW, g0 = wfirst * DPW, gend = (ge + DPW - 1) / DPW * DPW;
       asm volatile("" ::: "memory"); // (the band reads above are float2 accesses of the same LDS)
-      if (ln < DPW) { // the first and last words' dwords outside [gs, ge)
-        if (g0 + ln < gs) dec[ln] = 0u;
-        if (ge + ln < gend) dec[ge - g0 + ln] = 0u;
+      // the first and last words' dwords outside [gs, ge) are zeroed (lanes < DPW); every
+      // other lane stores into a junk dword past any decision or junk dword of the job, so
+      // the stores take no exec-mask block
+      {
+        const int jz = jk + ndata + DPW + 128 + ln; // (< 1152 dwords: the exchange buffer)
+        const int z1 = ln < DPW && g0 + ln < gs ? ln : jz;
+        const int z2 = ln < DPW && ge + ln < gend ? ge - g0 + ln : jz;
+        dec[z1] = 0u;
+        dec[z2] = 0u;
       }
       const uint32_t org_bits = (uint32_t)origin_idx << (32 - BPS);
       char *const decg = reinterpret_cast<char *>(dec) - 4 * g0; // (byte base of decision index 0)
-      int dflag1 = 0, dflag2 = 0;
-#pragma unroll
-      for (int which = 0; which < 2; ++which) {
-        const int sidx = which == 0 ? s1 : s2;
-        if (sidx < 0 || KO(2)) continue; // wave-uniform
-        const bool live = which == 0 ? live1 : live2;
-        const f2v phv = which == 0 ? f2v{ph1, ph1} : f2v{ph2, ph2};
-        const float tau = which == 0 ? tau1 : tau2;
-        const uint32_t lm31 = live ? 0x80000000u : 0u, lm30 = live ? 0x40000000u : 0u; // (QPSK)
-        const int sbase = sidx * per_sym;
-        int unc_any = 0;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          if (rr >= NS) continue;
-          const int dib = dib_of(rr);
-          const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], phv);
-          uint32_t db;
-          bool near; // the decision margin is inside the guard band
-          if (MOD == AMOD_QPSK) {
-            // the sign-bit decision with the symbol's liveness folded into its two masks:
-            // QPSK's origin decision is index 0 (four equidistant points, the first kept:
-            // runtime.cpp demap_exact(QPSK, 0, 0)), so a dead symbol's bits are 0 and no
-            // per-slot select is needed
-            const uint32_t a = __float_as_uint(c.x), b = __float_as_uint(c.y);
-            db = (b & lm31) | (((a ^ b) >> 1) & lm30);
-            // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
-            // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
-            float margin;
-            asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(margin) : "v"(c.x), "v"(c.y));
-            near = margin <= tau;
-          } else {
-            float margin;
-            db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
-            near = margin <= tau;
-          }
-          if (MOD != AMOD_QPSK) db = live ? db : org_bits;
-          unc_any |= !KO(0xFFFF) && dib < BPS * jk && live && near;
-          // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
-          // stores into its junk dword: no exec-mask block per store); pos is a multiple of
-          // BPS, so the byte offset is pos * (4 / BPS): one shift-add from the job's base
-          const uint32_t pos = (uint32_t)(sbase + dib);
-          *reinterpret_cast<uint32_t *>(decg + pos * (4 / BPS)) = db >> (pos & 31);
+      // the guard: each symbol's smallest decision margin over the lane's data slots (a slot
+      // without a data subcarrier counts as +inf), compared once with the symbol's band
+      const f2v phv1 = f2v{ph1, ph1}, phv2 = f2v{ph2, ph2};
+      const uint32_t lm31a = live1 ? 0x80000000u : 0u, lm30a = live1 ? 0x40000000u : 0u; // (QPSK)
+      const uint32_t lm31b = live2 ? 0x80000000u : 0u, lm30b = live2 ? 0x40000000u : 0u;
+      const int sbase1 = s1 * per_sym, sbase2 = s2 * per_sym;
+      float mm1 = __builtin_inff(), mm2 = __builtin_inff();
+      // one slot's decision for symbol `which` (0: s1, 1: s2)
+      auto slot_dec = [&](int rr, auto which_c) {
+        constexpr int which = decltype(which_c)::value;
+        const bool nd = (kn_neg >> (4 + rr)) & 1; // a pilot slot, or no subcarrier
+        const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], which == 0 ? phv1 : phv2);
+        uint32_t db;
+        float margin;
+        if (MOD == AMOD_QPSK) {
+          // the sign-bit decision with the symbol's liveness folded into its two masks:
+          // QPSK's origin decision is index 0 (four equidistant points, the first kept:
+          // runtime.cpp demap_exact(QPSK, 0, 0)), so a dead symbol's bits are 0 and no
+          // per-slot select is needed
+          const uint32_t a = __float_as_uint(c.x), b = __float_as_uint(c.y);
+          db = (b & (which == 0 ? lm31a : lm31b)) | (((a ^ b) >> 1) & (which == 0 ? lm30a : lm30b));
+          // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
+          // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
+          asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(margin) : "v"(c.x), "v"(c.y));
+        } else {
+          db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
+          db = (which == 0 ? live1 : live2) ? db : org_bits;
         }
-        if (which == 0) dflag1 = unc_any; else dflag2 = unc_any;
+        margin = nd ? __builtin_inff() : margin;
+        // (v_min_f32 without fminf's canonicalisation: a NaN margin is passed over, as the
+        // comparison of the per-slot form was false for it)
+        float &mm = which == 0 ? mm1 : mm2;
+        asm("v_min_f32 %0, %1, %2" : "=v"(mm) : "v"(mm), "v"(margin));
+        // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
+        // stores into its junk dword: no exec-mask block per store); pos is a multiple of
+        // BPS, so the byte offset is pos * (4 / BPS): one shift-add from the job's base
+        const uint32_t pos = (uint32_t)((which == 0 ? sbase1 : sbase2) + dib_of(rr));
+        *reinterpret_cast<uint32_t *>(decg + pos * (4 / BPS)) = db >> (pos & 31);
+      };
+      using W0 = std::integral_constant<int, 0>;
+      using W1 = std::integral_constant<int, 1>;
+      if (!KO(2)) {
+        // (wave-uniform) both halves data symbols: every job but a frame's first (the CE
+        // half) and, for an even symbol count, its last, as one straight-line block
+        if (s1 >= 0 && s2 >= 0) {
+#pragma unroll
+          for (int rr = 0; rr < NS; ++rr) { slot_dec(rr, W0{}); slot_dec(rr, W1{}); }
+        } else if (s2 >= 0) {
+#pragma unroll
+          for (int rr = 0; rr < NS; ++rr) slot_dec(rr, W1{});
+        } else {
+#pragma unroll
+          for (int rr = 0; rr < NS; ++rr) slot_dec(rr, W0{});
+        }
       }
+      const bool d1u = live1 && !KO(0xFFFF) && __ballot(mm1 <= tau1) != 0;
+      const bool d2u = live2 && !KO(0xFFFF) && __ballot(mm2 <= tau2) != 0;
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       // (lane i reads its NQ 16-byte pieces starting at piece i / (16 / NQ) mod NQ: the 16
       // lanes of each ds_read_b128 group then cover 16 distinct 16-byte bank slots; in
-      // order, lanes i and i + 16 / NQ hit the same slot: 4-way for QPSK)
+      // order, lanes i and i + 16 / NQ hit the same slot: 4-way for QPSK). A job's run is
+      // at most 2 ndata / DPW + 2 words: one pass of the wave for BPSK and QPSK.
       constexpr int NQ = DPW / 4;
       const int rot = (ln / (16 / NQ)) & (NQ - 1);
-      for (int i = ln; i < (KO(2) ? 0 : (gend - g0) / DPW); i += 64) {
+      const int nwj = KO(2) ? 0 : (gend - g0) / DPW;
+      for (int i = ln; i < nwj; i += 64) {
         const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
         uint4 t[NQ]; // (every piece requested before the first is combined: one LDS wait)
 #pragma unroll
@@ -1995,10 +2115,10 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
 #pragma unroll
         for (int k = 0; k < NQ; ++k) word |= (t[k].x | t[k].y) | (t[k].z | t[k].w);
         atomicOr(bits + wfirst + i, word);
+        if (BPS <= 2) break; // (one pass covers a BPSK or QPSK run: <= 2 * 255 / DPW + 2 words)
       }
       asm volatile("" ::: "memory"); // (the next FFT rewrites the buffer)
       {
-        const bool d1u = __ballot(dflag1) != 0, d2u = __ballot(dflag2) != 0;
         if (s1 >= 0 && (d1u || ph_unc1)) {
           flag_sym = min(flag_sym, s1);
           sflags |= (d1u ? AMOD_FLAG_DEMAP : 0) | (ph_unc1 ? AMOD_FLAG_PHASE : 0);
@@ -2071,7 +2191,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
             r.flags = dr.flags; // AMOD_FLAG_REPLAY (+ why) for a replayed detection, else 0
           }
           const int nbytes = (nbits / rep) >> 3;
-          const int crc_len = parse_stream(v, nbytes, cfg.mode, r); // every lane: the same bytes
+          const int crc_len = parse_fast(v, nbytes, cfg.mode, r); // every lane: the same bytes
           if (cfg.mode == AMOD_MODE_RECEIVED) {
             // preambleIdx is reported on legacy success and on every 0xFE/0xFF result (609-620)
             const bool keep = (r.frame_type == 0xFE || r.frame_type == 0xFF) || (r.frame_type == 0 && r.status == AMOD_OK);
@@ -2091,15 +2211,20 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           DSTAMP(25, true);
           const int store_bytes = min(need, nbytes);
           r.payload_valid = store_bytes;
-          // payload bytes, big-endian words -> memory order
-          const int nw = (store_bytes + 3) >> 2;
-          uint32_t *const dst = reinterpret_cast<uint32_t *>(w.payload + (int64_t)f * w.stride);
-          const int cap_w = (int)(w.stride >> 2);
-          for (int i = lane; i < nw && i < cap_w; i += 64) {
-            uint32_t word = v[i];
-            const int keep = store_bytes - 4 * i; // bytes of this word that were decoded
-            if (keep < 4) word &= ~(0xFFFFFFFFu >> (8 * keep));
-            dst[i] = __builtin_bswap32(word);
+          // payload bytes, big-endian words -> memory order, 16 bytes per lane and store
+          // (the slot stride is a multiple of 16; bytes past store_bytes in the last 16 are
+          // written as zero, the value the slot holds past payload_valid)
+          const int nq = (store_bytes + 15) >> 4;
+          uint4 *const dst = reinterpret_cast<uint4 *>(w.payload + (int64_t)f * w.stride);
+          const int cap_q = (int)(w.stride >> 4);
+          for (int i = lane; i < nq && i < cap_q; i += 64) {
+            uint4 q = reinterpret_cast<const uint4 *>(v)[i];
+            const int keep = store_bytes - 16 * i; // bytes of these 16 that were decoded
+            auto msk = [&](uint32_t wd, int k) -> uint32_t {
+              const int b = keep - 4 * k;
+              return __builtin_bswap32(b >= 4 ? wd : b <= 0 ? 0u : wd & ~(0xFFFFFFFFu >> (8 * b)));
+            };
+            dst[i] = make_uint4(msk(q.x, 0), msk(q.y, 1), msk(q.z, 2), msk(q.w, 3));
           }
           if (DBG && lane == 0) D->nsym = cur.M;
           // the record: 24 words, one per lane
