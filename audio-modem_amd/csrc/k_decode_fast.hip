@@ -1393,6 +1393,18 @@ __device__ __forceinline__ uint32_t le_word_pad(const uint32_t *v, int i) {
   const uint32_t hi = wi >= -1 ? v[max(wi + 1, 0)] : 0u;
   return __builtin_bswap32(sh ? (lo << sh) | (hi >> (32 - sh)) : lo);
 }
+// the same product with the matrix's 32 columns already in registers
+__device__ __forceinline__ uint32_t crc_apply_rows(const uint4 (&m)[8], uint32_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r ^= m[k].x & (uint32_t)((int32_t)(c << (31 - 4 * k)) >> 31);
+    r ^= m[k].y & (uint32_t)((int32_t)(c << (30 - 4 * k)) >> 31);
+    r ^= m[k].z & (uint32_t)((int32_t)(c << (29 - 4 * k)) >> 31);
+    r ^= m[k].w & (uint32_t)((int32_t)(c << (28 - 4 * k)) >> 31);
+  }
+  return r;
+}
 __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32_t c) {
   const uint4 *const mq = reinterpret_cast<const uint4 *>(mat + 32 * q);
   uint32_t r = 0;
@@ -1437,6 +1449,14 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const D
   const int pad = kCrcChunk * nch - L;
   const int n = (nch + 63) >> 6; // chunks per lane (wave-uniform)
   const int j0 = n * lane, j1 = min(j0 + n, nch);
+  // this lane's shift matrix (global memory) requested before the chunk steps, so its
+  // reads fly under them
+  uint4 sm[8];
+  {
+    const uint4 *const mq = reinterpret_cast<const uint4 *>(t.crc_mat + 32 * max(0, nch - j1));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sm[k] = mq[k];
+  }
   uint32_t c = lane == 0 ? 0xFFFFFFFFu : 0u;
   for (int q = 0; q < n; ++q) { // (wave-uniform trip count; a lane past its range idles)
     const int j = j0 + q;
@@ -1459,7 +1479,7 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t *v, int L, const D
     }
   }
   if (stp && lane == 0) stp[31] = __builtin_amdgcn_s_memtime(); // (chunk registers)
-  const uint32_t acc = j0 < nch ? crc_shift(t.crc_mat, nch - j1, c) : 0u;
+  const uint32_t acc = j0 < nch ? crc_apply_rows(sm, c) : 0u;
   const uint32_t reg = wave_xor_dpp(acc);
   return (pad ? crc_shift(crc_unpad, pad, reg) : reg) ^ 0xFFFFFFFFu;
 }
@@ -2217,14 +2237,21 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           const int nq = (store_bytes + 15) >> 4;
           uint4 *const dst = reinterpret_cast<uint4 *>(w.payload + (int64_t)f * w.stride);
           const int cap_q = (int)(w.stride >> 4);
-          for (int i = lane; i < nq && i < cap_q; i += 64) {
-            uint4 q = reinterpret_cast<const uint4 *>(v)[i];
-            const int keep = store_bytes - 16 * i; // bytes of these 16 that were decoded
-            auto msk = [&](uint32_t wd, int k) -> uint32_t {
-              const int b = keep - 4 * k;
-              return __builtin_bswap32(b >= 4 ? wd : b <= 0 ? 0u : wd & ~(0xFFFFFFFFu >> (8 * b)));
+          const int nql = min(nq, cap_q);
+          for (int i0 = 0; i0 < nql; i0 += 128) { // (two rows per lane per pass, both read first)
+            const int ia = i0 + lane, ib = ia + 64;
+            const uint4 qa = reinterpret_cast<const uint4 *>(v)[min(ia, nql - 1)];
+            const uint4 qb = reinterpret_cast<const uint4 *>(v)[min(ib, nql - 1)];
+            auto put = [&](int i, uint4 q) {
+              const int keep = store_bytes - 16 * i; // bytes of these 16 that were decoded
+              auto msk = [&](uint32_t wd, int k) -> uint32_t {
+                const int b = keep - 4 * k;
+                return __builtin_bswap32(b >= 4 ? wd : b <= 0 ? 0u : wd & ~(0xFFFFFFFFu >> (8 * b)));
+              };
+              if (i < nql) dst[i] = make_uint4(msk(q.x, 0), msk(q.y, 1), msk(q.z, 2), msk(q.w, 3));
             };
-            dst[i] = make_uint4(msk(q.x, 0), msk(q.y, 1), msk(q.z, 2), msk(q.w, 3));
+            put(ia, qa);
+            put(ib, qb);
           }
           if (DBG && lane == 0) D->nsym = cur.M;
           // the record: 24 words, one per lane
