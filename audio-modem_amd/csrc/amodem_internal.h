@@ -202,6 +202,13 @@ struct GapScan {
 __host__ __device__ inline bool soft_combine_applies(uint32_t options, int rep, int mod) {
   return (options & AMOD_OPT_SOFT_COMBINE) && rep > 1 && (mod == AMOD_BPSK || mod == AMOD_QPSK);
 }
+// ... and k_demod's soft instance decides it (not a parity-debug launch; a repeat group
+// spans at most two symbols; a symbol's (value, bound) pairs and the junk slots of 64
+// lanes fit the wave's 1152-float exchange buffer)
+__host__ __device__ inline bool soft_fast(uint32_t options, const DevCfg &cfg, bool dbg = false) {
+  return soft_combine_applies(options, cfg.rep, cfg.mod) && !dbg && cfg.rep <= cfg.ndata * cfg.bps &&
+         2 * (cfg.bps * cfg.ndata + 8 + 64 * cfg.bps) <= 1152;
+}
 
 
 
@@ -529,7 +536,7 @@ __device__ inline void init_result(amod_result &r) {
 extern "C" {
 hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::DevWork &w, hipStream_t s); // k_detect / k_chunk_prep
 hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s);
-int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds);
+int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds, bool soft);
 void amod_demod_stream_words(const amod::DevCfg &cfg, int mcap, int *stream_words, int *vote_off);
 hipError_t amod_launch_exact(const amod::DevCfg &cfg, const amod::DevWork &w, int nslots, hipStream_t s,
                              bool beside_demod = false); // list A runs beside k_demod

@@ -235,7 +235,7 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     // the detection here and goes back to k_demod (w.rp_count: the caller launches it)
     const bool replay = w.rp_count && w.det && !D && cfg.mode == AMOD_MODE_RECEIVED && flags0 != 0 &&
         (flags0 & ~(AMOD_FLAG_COARSE | AMOD_FLAG_FINE | AMOD_FLAG_THRESH)) == 0 &&
-        !soft_combine_applies(w.options, cfg.rep, cfg.mod);
+        !(soft_combine_applies(w.options, cfg.rep, cfg.mod) && !soft_fast(w.options, cfg));
     if (cfg.mode != AMOD_MODE_CHUNK) {
       // ---- preprocessSignal: the mean is a sequential double sum (modem.js:215-217).
       // Every partial sum of floats is a multiple of 2^emin (the smallest sample ulp) and

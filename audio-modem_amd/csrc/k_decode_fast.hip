@@ -1286,8 +1286,10 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
     d.route = ROUTE_DEMOD; d.flags = 0; d.start = start; d.M = M; d.T = T; d.coarse = sm.coarse;
     d.A = sm.A; d.B = sm.B; d.fbest = sm.fbest; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
     w.det[f] = d;
-    // opt-in soft combining (not reference behaviour): the exact kernel demodulates
-    if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
+    // opt-in soft combining (not reference behaviour): k_demod's soft instance, or the exact
+    // kernel where that does not apply (a parity-debug launch)
+    if (soft_combine_applies(w.options, cfg.rep, cfg.mod) && !soft_fast(w.options, cfg, w.dbg != nullptr))
+      list_exact(w, f, AMOD_FLAG_SOFT);
   }
   return;
 
@@ -1354,7 +1356,8 @@ __global__ __launch_bounds__(WG) void k_chunk_prep(const DevCfg cfg, const DevWo
   d.route = ROUTE_DEMOD; d.flags = 0; d.start = 0; d.M = (N - 3 * SYM) / SYM; d.T = min(d.M, w.mcap); d.coarse = -1;
   d.A = 1.f; d.B = 0.f; d.fbest = 0.f; d.sc_lo = d.sc_hi = -1; d.pad = 0.f;
   w.det[f] = d;
-  if (soft_combine_applies(w.options, cfg.rep, cfg.mod)) list_exact(w, f, AMOD_FLAG_SOFT);
+  if (soft_combine_applies(w.options, cfg.rep, cfg.mod) && !soft_fast(w.options, cfg, w.dbg != nullptr))
+    list_exact(w, f, AMOD_FLAG_SOFT);
 }
 
 // ------------------------------------------------------------ demodulation
@@ -1641,7 +1644,10 @@ __device__ __forceinline__ int frame_jobs(const FrameS &F) { return F.T > 0 ? 1 
 
 // MOD: the launch's modulation as a template argument (decisions and packing unroll)
 // NS: band slots per lane, ceil(nband / 64) (slot rr < NS - 1 is full on every lane)
-template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop() {
+// SOFT: opt-in soft combining (AMOD_OPT_SOFT_COMBINE, BPSK / QPSK, repetition > 1; not
+// reference behaviour): each repeat group is decided by the sign of its
+// |H|^2-weighted soft sum, per symbol as the symbol is demodulated (below)
+template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline__ void demod_loop() {
   constexpr int BPS = MOD == AMOD_BPSK ? 1 : (MOD == AMOD_QPSK ? 2 : 4);
   __shared__ __attribute__((aligned(16))) float2 xch[NWAVE][XCH_F2];
   __shared__ float2 twl[512];   // tw1 rows 1-7 (row q at 64 (q - 1)), then tw2[64]
@@ -1800,6 +1806,8 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
 
   float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
   f2v gp = {0.f, 0.f};        // G = 1/H at the lane's pilot (job 0)
+  float wl[4] = {0.f, 0.f, 0.f, 0.f}; // SOFT: the soft weights |H|^2 of the lane's band subcarriers (job 0)
+  float wmax = 0.f, dW = 0.f;  // SOFT: the frame's largest weight, and the error bound of every weight
   float gmax = 0.f, zce = 0.f; // guard scales of the frame (job 0)
   // state of the frame being demodulated (wave-uniform): jobs it takes (shrinks once the
   // header says how many bytes the parse reads), those bytes (-1: not yet known), the
@@ -1817,7 +1825,9 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
     const int known = min(dsym * per_sym, nbits);
     const int avail = (known / rep) >> 3;
     const uint32_t *src = bits;
-    if (rep > 1) {
+    if (SOFT) {
+      src = voted; // (built symbol by symbol: every complete group of the known symbols)
+    } else if (rep > 1) {
       wave_vote(bits, min(known, kHeaderMaxBytes * 8 * rep), rep, voted);
       __builtin_amdgcn_wave_barrier();
       src = voted;
@@ -1847,9 +1857,10 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
 #endif
     const int f = cur.f;
     amod_debug *const D = DBG ? w.dbg + f : nullptr;
-    if (jcur == 0) { // a new frame: clear its bit stream
-      const int nwz = (cur.T * per_sym + 31) / 32 + 2;
-      for (int i = lane; i < nwz; i += 64) bits[i] = 0u;
+    if (jcur == 0) { // a new frame: clear its bit stream (SOFT: its voted stream, built by ORs)
+      const int nwz = SOFT ? (cur.T * per_sym / rep + 31) / 32 + 3 : (cur.T * per_sym + 31) / 32 + 2;
+      uint32_t *const zs = SOFT ? voted : bits;
+      for (int i = lane; i < nwz; i += 64) zs[i] = 0u;
       live_f = f; fnj = max(frame_jobs(cur), 1); fneed = -1; flag_sym = 0x7fffffff;
       wflags = 0; sflags = 0;
     } else if (jcur >= fnj) { // prefetched before the header showed the frame was complete
@@ -1960,6 +1971,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
           // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
           ch |= b < nband && !const1 && m2 < 4.f * 1e-6f;
           gl[rr] = g;
+          if (SOFT) wl[rr] = b < nband ? 0.25f * m2 : 0.f; // |H|^2 = |h|^2 / 4
           if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
           if (DBG && b < nband) { const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
             D->h_re[b] = const1 ? 0.f : 0.5f * h.x * kn; D->h_im[b] = const1 ? 0.f : 0.5f * h.y * kn; }
@@ -1967,6 +1979,13 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         { const float2 g = inv(x1p, (kn_neg >> 9) & 1); gp = f2v{g.x, g.y}; }
         gmax = wmax_nn(gm); // half of max |G|
         if (__ballot(ch)) wflags |= AMOD_FLAG_CHANNEL;
+        if (SOFT) {
+          // |H_fast - H| <= 2e-6 guard zce (the FFT bound of the guards, |H| <= zce), so the
+          // weight's error is <= (|H_fast| + |H|) |dH| <= 4.1e-6 guard zce^2, plus the fp32
+          // rounding of |h|^2 / 4
+          wmax = wmax_nn(max3_raw(wl[0], wl[1], fmaxf(wl[2], wl[3])));
+          dW = 4.1e-6f * guard * zce * zce + 2.4e-7f * wmax;
+        }
       }
       // equalise both halves (the CE half of job 0 is not a data symbol); em bounds |eq| of
       // both symbols of the job
@@ -2051,7 +2070,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       // the first and last words' dwords outside [gs, ge) are zeroed (lanes < DPW); every
       // other lane stores into a junk dword past any decision or junk dword of the job, so
       // the stores take no exec-mask block
-      {
+      if (!SOFT) {
         const int jz = jk + ndata + DPW + 128 + ln; // (< 1152 dwords: the exchange buffer)
         const int z1 = ln < DPW && g0 + ln < gs ? ln : jz;
         const int z2 = ln < DPW && ge + ln < gend ? ge - g0 + ln : jz;
@@ -2101,7 +2120,89 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       };
       using W0 = std::integral_constant<int, 0>;
       using W1 = std::integral_constant<int, 1>;
-      if (!KO(2)) {
+      if constexpr (SOFT) {
+        // Soft combining, one symbol at a time: every data subcarrier's soft values (BPSK: the
+        // phase-corrected real part; QPSK: the imaginary part for the first bit, the max-log
+        // min(|re|, |im|), negative where the signs differ, for the second; each times the
+        // weight |H|^2 of its subcarrier, as the exact kernel forms them) go to the exchange
+        // buffer at their bit offset in the symbol; then lane l sums repeat group jS + l
+        // (every bit of it in this symbol, plus the carried partial sum of a group that
+        // began in the previous one) and the signs of the complete groups are ORed into the
+        // voted stream by one ballot per 64 groups. The error of each soft value is bounded
+        // by the symbol's decision band tau (2 tau for QPSK's max-log value: a sign change
+        // of a component within tau moves it by at most 2 tau), the weight's dW and the
+        // fp32 roundings; a group whose sum lies within the sum of its values' bounds is
+        // uncertain, and its symbol routes the frame to the exact kernel.
+        // (value, error bound) per bit of the symbol: the bound per value, from the value's own
+        // |eq| (the symbol band tau takes the largest |eq| of the job: several times looser)
+        f2v *const sb = reinterpret_cast<f2v *>(X2);
+        float *const carry = reinterpret_cast<float *>(bits); // (the raw stream is unused here)
+        constexpr float KS = MOD == AMOD_QPSK ? 2.f : 1.f;
+        auto soft_sym = [&](auto which_c, int s, bool live, float ph, float dp) {
+          constexpr int which = decltype(which_c)::value;
+          const f2v phv = f2v{ph, ph};
+          const float aph = 1.f + fabsf(ph);
+#pragma unroll
+          for (int rr = 0; rr < NS; ++rr) {
+            const bool nd = (kn_neg >> (4 + rr)) & 1;
+            const f2v e = which == 0 ? e1[rr] : e2[rr];
+            const f2v c = pk_derot(e, phv);
+            const float w = live ? wl[rr] : 0.f; // (a constant window: the exact values are 0)
+            const float ea = fabsf(e.x) + fabsf(e.y);
+            // this value's |c - c_exact| bound: the guards' tau with its own |eq| in the phase
+            // term (d stays the wave's: the FFT error is set by the whole spectrum's scale)
+            const float tau = 4.f * (d * aph + ea * dp) + 1e-9f;
+            const float ca = ea * aph; // bounds |re|, |im| of c
+            const float ev = live ? KS * tau * (w + dW) + ca * dW + 2.4e-7f * ca * w : 0.f;
+            const int o = nd ? BPS * ndata + 8 + BPS * ln : dib_of(rr); // bit offset (junk past the symbol)
+            if (MOD == AMOD_BPSK) {
+              sb[o] = f2v{c.x * w, ev};
+            } else {
+              float m;
+              asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(m) : "v"(c.x), "v"(c.y));
+              sb[o] = f2v{c.y * w, ev};
+              sb[o + 1] = f2v{((__float_as_uint(c.x) ^ __float_as_uint(c.y)) >> 31 ? -m : m) * w, ev};
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+          const int P0 = s * per_sym, P1 = P0 + per_sym;
+          const int jS = P0 / rep, jE = P1 / rep; // groups [jS, jE) complete here; jE partial
+          const bool strad = jS * rep < P0;
+          const float c0 = carry[0], ce0 = carry[1]; // (the previous symbol's partial group)
+          bool unc = false;
+          for (int g0 = jS; g0 <= jE; g0 += 64) { // (one pass for every built-in preset)
+            const int j = g0 + ln;
+            float sum = 0.f, E = 0.f, sa = 0.f;
+            if (j <= jE) {
+              const int b0 = j * rep;
+              for (int u = 0; u < rep; ++u) {
+                const int b = b0 + u;
+                if (b >= P0 && b < P1) { const f2v t = sb[b - P0]; sum += t.x; E += t.y; sa += fabsf(t.x); }
+              }
+              if (j == jS && strad) { sum += c0; E += ce0; sa += fabsf(c0); }
+            }
+            E += 6e-8f * (float)rep * sa; // (the fp32 sum of at most rep values)
+            const bool full = j < jE;
+            const uint64_t m = __ballot(full && sum < 0.f);
+            unc |= __ballot(full && fabsf(sum) <= E) != 0;
+            if (j == jE && jE * rep < P1) { carry[0] = sum; carry[1] = E; } // (one lane)
+            // groups g0 + l, MSB-first in the voted words: word (g0 >> 5), bit 31 - (g0 & 31) on
+            const uint64_t R = __builtin_bitreverse64(m);
+            const int ob = g0 & 31, W = g0 >> 5;
+            if (ln < 3) {
+              const uint32_t wv = ln == 0 ? (uint32_t)(R >> (32 + ob))
+                                : ln == 1 ? (uint32_t)(R >> ob) : (ob ? (uint32_t)(R << (32 - ob)) : 0u);
+              atomicOr(voted + W + ln, wv);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+          return live && unc;
+        };
+        if (s1 >= 0 && soft_sym(W0{}, s1, live1, ph1, dp1)) mm1 = -1.f; // (mm <= tau: the flags below)
+        if (s2 >= 0 && soft_sym(W1{}, s2, live2, ph2, dp2)) mm2 = -1.f;
+      } else if (!KO(2)) {
         // (wave-uniform) both halves data symbols: every job but a frame's first (the CE
         // half) and, for an even symbol count, its last, as one straight-line block
         if (s1 >= 0 && s2 >= 0) {
@@ -2125,7 +2226,7 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
       // at most 2 ndata / DPW + 2 words: one pass of the wave for BPSK and QPSK.
       constexpr int NQ = DPW / 4;
       const int rot = (ln / (16 / NQ)) & (NQ - 1);
-      const int nwj = KO(2) ? 0 : (gend - g0) / DPW;
+      const int nwj = (KO(2) || SOFT) ? 0 : (gend - g0) / DPW;
       for (int i = ln; i < nwj; i += 64) {
         const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
         uint4 t[NQ]; // (every piece requested before the first is combined: one LDS wait)
@@ -2195,8 +2296,8 @@ template <bool DBG, int MOD, int NS> __device__ __forceinline__ void demod_loop(
         if (lane == 0) list_exact(w, f, wflags);
       } else {
         {
-          const uint32_t *v = bits;
-          if (rep > 1) { // vote only the decoded prefix the parse reads
+          const uint32_t *v = SOFT ? voted : bits;
+          if (!SOFT && rep > 1) { // vote only the decoded prefix the parse reads
             wave_vote(bits, min(decoded, need * 8 * rep), rep, voted);
             __builtin_amdgcn_wave_barrier();
             v = voted;
@@ -2307,6 +2408,11 @@ template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgp
   (void)w_arg;
   demod_loop<false, MOD, NS>();
 }
+template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod_soft(const DevCfg cfg_arg, const DevWork w_arg) {
+  (void)cfg_arg;
+  (void)w_arg;
+  demod_loop<false, MOD, NS, true>();
+}
 template <int MOD, int NS> __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(AMOD_DEMOD_WPE))) void k_demod_dbg(const DevCfg cfg_arg, const DevWork w_arg) {
   (void)cfg_arg;
   (void)w_arg;
@@ -2321,8 +2427,17 @@ template <int MOD> __host__ demod_fn demod_kernel_ns(int ns, bool dbg) {
   default: return dbg ? k_demod_dbg<MOD, 4> : k_demod<MOD, 4>;
   }
 }
-__host__ demod_fn demod_kernel(const DevCfg &cfg, bool dbg) {
+template <int MOD> __host__ demod_fn demod_kernel_soft(int ns) {
+  switch (ns) {
+  case 1: return k_demod_soft<MOD, 1>;
+  case 2: return k_demod_soft<MOD, 2>;
+  case 3: return k_demod_soft<MOD, 3>;
+  default: return k_demod_soft<MOD, 4>;
+  }
+}
+__host__ demod_fn demod_kernel(const DevCfg &cfg, bool dbg, bool soft = false) {
   const int ns = (cfg.nband + 63) / 64; // validate(): 1 <= nband <= 255
+  if (soft && !dbg) return cfg.mod == AMOD_BPSK ? demod_kernel_soft<AMOD_BPSK>(ns) : demod_kernel_soft<AMOD_QPSK>(ns);
   if (cfg.mod == AMOD_BPSK) return demod_kernel_ns<AMOD_BPSK>(ns, dbg);
   if (cfg.mod == AMOD_QPSK) return demod_kernel_ns<AMOD_QPSK>(ns, dbg);
   return demod_kernel_ns<AMOD_QAM16>(ns, dbg);
@@ -2381,14 +2496,14 @@ extern "C" hipError_t amod_launch_detect(const amod::DevCfg &cfg, const amod::De
 }
 extern "C" hipError_t amod_launch_demod(const amod::DevCfg &cfg, const amod::DevWork &w, int nblocks, hipStream_t s) {
   if (w.f1 <= w.f0 || nblocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(amod::demod_kernel(cfg, w.dbg != nullptr), dim3(nblocks), dim3(amod::WG),
+  hipLaunchKernelGGL(amod::demod_kernel(cfg, w.dbg != nullptr, amod::soft_fast(w.options, cfg)), dim3(nblocks), dim3(amod::WG),
                      (unsigned)(4 * amod::NWAVE * w.stream_words), s, cfg, w);
   return hipGetLastError();
 }
 // k_demod blocks resident at once on one CU for a dynamic LDS of lds bytes
-extern "C" int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds) {
+extern "C" int amod_demod_blocks_per_cu(const amod::DevCfg &cfg, int lds, bool soft) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, amod::demod_kernel(cfg, false), amod::WG, lds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, amod::demod_kernel(cfg, false, soft), amod::WG, lds) != hipSuccess ||
       n <= 0)
     n = 4;
   return n;

@@ -249,7 +249,7 @@ struct amod_ctx {
   DevBuf det;          // fast path: per-frame detection records (k_detect -> k_demod)
   hipStream_t aux = nullptr;  // k_demod of chunk c beside k_detect of chunk c + 1
   std::array<hipEvent_t, kMaxChunks + 1> chunk_ev{};
-  int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0;
+  int cu_count = 0, demod_lds = -1, demod_mod = -1, demod_nband = -1, demod_bpc = 0, demod_soft = -1;
   // fb[0 .. 2] are the decode's counts (lists from fb + 64), zeroed by the decode's own first
   // and last launches (DevWork::fb_zero, fb_reset). fb_zeroed: they are zero when this decode's
   // launches run; a reallocation or an aborted launch sequence clears it (memset)
@@ -640,9 +640,10 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   // d.stop_after (diagnostics, AMOD_STOP_AFTER): <= 2 stops after detection
   const bool demod = d.stop_after >= 3;
   const int lds = 4 * 4 * w.stream_words; // k_demod: 4 waves per block
-  if (ctx->demod_lds != lds || ctx->demod_mod != d.mod || ctx->demod_nband != d.nband) {
-    ctx->demod_lds = lds; ctx->demod_mod = d.mod; ctx->demod_nband = d.nband;
-    ctx->demod_bpc = amod_demod_blocks_per_cu(d, lds);
+  const int soft = amod::soft_fast(options, d) ? 1 : 0; // k_demod's soft-combining instance
+  if (ctx->demod_lds != lds || ctx->demod_mod != d.mod || ctx->demod_nband != d.nband || ctx->demod_soft != soft) {
+    ctx->demod_lds = lds; ctx->demod_mod = d.mod; ctx->demod_nband = d.nband; ctx->demod_soft = soft;
+    ctx->demod_bpc = amod_demod_blocks_per_cu(d, lds, soft != 0);
   }
   int64_t per_cu = ctx->demod_bpc;
   if (ctx->knobs.demod_bpc > 0) per_cu = ctx->knobs.demod_bpc; // diagnostics: grid size

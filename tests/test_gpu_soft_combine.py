@@ -74,3 +74,70 @@ def test_soft_combining_qpsk_rep3():
     ok_h = int(((hard["status"] == 0) & (hard["crc_valid"] == 1)).sum())
     ok_s = int(((soft["status"] == 0) & (soft["crc_valid"] == 1)).sum())
     assert ok_s >= ok_h, (ok_h, ok_s)
+
+
+_FIELDS = ["status", "frame_type", "nbytes", "crc_valid", "seq_num", "data_len", "name_len", "expected_crc",
+           "actual_crc", "aux"]
+
+
+def _same(a, ap, b, bp):
+    """per-frame equality of every decoded field and the payload bytes both decoded (not
+    `flags`: the exact kernel marks its frames; not payload_valid: the fast path decodes
+    only the symbols the parse reads, the exact kernel every symbol; not the fast path's
+    approximate fine metric)"""
+    bad = []
+    for i in range(len(a)):
+        pv = min(a["payload_valid"][i], b["payload_valid"][i])
+        if any(a[k][i] != b[k][i] for k in _FIELDS) or ap[i, :pv].tobytes() != bp[i, :pv].tobytes():
+            bad.append(i)
+    return bad
+
+
+@pytest.mark.parametrize("mod,config,rep,length,divs", [
+    ("BPSK", "acoustic", 3, 128, (1.5, 2.0, 3.0, 6.0)),
+    ("QPSK", "standard", 3, 256, (6.0, 8.0, 12.0)),
+    ("BPSK", "narrowband", 5, 64, (2.0, 4.0)),
+])
+def test_fast_soft_equals_exact_soft(mod, config, rep, length, divs):
+    """k_demod's soft-combining instance (per-symbol |H|^2-weighted group sums with error
+    bounds) decides every repeat group as the exact kernel's fp64 soft vote
+    does, frame for frame, on noisy chunk windows from ~1.8 dB up, and most frames stay on
+    the fast path (a group inside its error bound routes its frame to the exact kernel)."""
+    cfg = amodem.preset(config, mod, rep)
+    dm = amodem.Demodulator(0)
+    for d in divs:
+        x, offs, lens = _frames(96, d, 0x5A5A + int(10 * d), rep=rep, mod=mod, config=config, length=length)
+        fast, fp = _decode(dm, cfg, x, offs, lens, L.OPT_SOFT_COMBINE)
+        ex, ep = _decode(dm, cfg, x, offs, lens, L.OPT_SOFT_COMBINE | L.OPT_FORCE_EXACT)
+        assert (ex["flags"] & L.FLAG_EXACT).all()
+        bad = _same(fast, fp, ex, ep)
+        assert not bad, (d, bad[:5])
+        on_fast = int(((fast["flags"] & L.FLAG_EXACT) == 0).sum())
+        # about as many frames stay on the fast path as with the hard vote (whose guard
+        # lists a frame for ANY decision inside its band; at low SNR both list many, QPSK
+        # most: its max-log value is small wherever either component is)
+        hard, _ = _decode(dm, cfg, x, offs, lens, 0)
+        on_fast_hard = int(((hard["flags"] & L.FLAG_EXACT) == 0).sum())
+        assert on_fast + max(4, len(fast) // 16) >= on_fast_hard, (d, on_fast, on_fast_hard)
+        if mod == "BPSK" and d >= 3.0:
+            assert on_fast >= 3 * len(fast) // 4, (d, on_fast)
+    dm.close()
+
+
+def test_fast_soft_received_mode_equals_exact():
+    """the same through decodeReceivedSignal-shaped frames (preamble search, fine timing,
+    legacy parse) with AWGN, BPSK rep 3"""
+    cfg = amodem.preset("acoustic", "BPSK", 3)
+    x, offs, lens = amodem.synth_legacy_batch(cfg, 48, payload_len=96, threads=8)
+    sp = float(np.mean(x[x != 0] ** 2))
+    dm = amodem.Demodulator(0)
+    for snr_db, seed in ((6.0, 3), (9.0, 4), (14.0, 5)):
+        rng = np.random.default_rng(seed)
+        y = (x + rng.standard_normal(len(x)).astype(np.float32) * np.float32(np.sqrt(sp / 10 ** (snr_db / 10)))
+             ).astype(np.float32)
+        fast, fp = dm.decode_batch(y, offs, lens, cfg=cfg, options=L.OPT_SOFT_COMBINE)
+        ex, ep = dm.decode_batch(y, offs, lens, cfg=cfg, options=L.OPT_SOFT_COMBINE | L.OPT_FORCE_EXACT)
+        bad = [i for i in _same(fast, fp, ex, ep)]
+        assert not bad, (snr_db, bad[:5])
+        assert np.array_equal(fast["preamble_idx"], ex["preamble_idx"])
+    dm.close()
