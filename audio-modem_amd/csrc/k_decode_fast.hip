@@ -420,6 +420,7 @@ __device__ __forceinline__ float wsum_b(float v) {
 // instruction wrote needs two wait states, which the three other chains fill (one chain
 // alone pays an s_nop per step)
 __device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) {
+  asm volatile("s_nop 1" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)); // (see AMOD_DPP_GUARD)
 #define AMOD_W4(ctrl)                                                                   \
   { const float ta = AMOD_DPP_F(a, ctrl), tb = AMOD_DPP_F(b, ctrl), tc = AMOD_DPP_F(c, ctrl), td = AMOD_DPP_F(d, ctrl); \
     a += ta; b += tb; c += tc; d += td; }
@@ -438,13 +439,16 @@ __device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) 
                "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
                "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
                "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-               "v_add_f32_dpp %3, %3, %3 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               "v_add_f32_dpp %3, %3, %3 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "s_nop 1" // (the readlanes below: a VALU write of a VGPR needs a wait state before
+                         // v_readlane reads it, which the compiler cannot see inside the block)
                : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
   a = rlane(a, 63); b = rlane(b, 63); c = rlane(c, 63); d = rlane(d, 63);
 }
 // the same four sums over row 0 only (lanes 0 .. 15; the pilot lanes of every built-in
 // preset): the row reductions alone, then lane 0
 __device__ __forceinline__ void wsum16_4(float &a, float &b, float &c, float &d) {
+  asm volatile("s_nop 1" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
 #define AMOD_W4(ctrl)                                                                   \
   { const float ta = AMOD_DPP_F(a, ctrl), tb = AMOD_DPP_F(b, ctrl), tc = AMOD_DPP_F(c, ctrl), td = AMOD_DPP_F(d, ctrl); \
     a += ta; b += tb; c += tc; d += td; }
@@ -463,7 +467,12 @@ __device__ __forceinline__ float wmax_b(float v) {
 // max over the wave of non-negative floats (or NaN): their bit patterns order like the
 // values, so the reduction runs on integers (v_max_i32 with DPP fused, no NaN
 // canonicalisation steps); a wave-uniform result via one readlane. Whole wave active.
+// (inputs of the DPP reductions below may come from inline asm, e.g. max3_raw: the
+// compiler's hazard check does not count an asm block as the VALU write a DPP read must
+// wait two states for, so each reduction starts with its own s_nop tied to the value)
+#define AMOD_DPP_GUARD(x) asm volatile("s_nop 1" : "+v"(x))
 __device__ __forceinline__ float wmax_nn(float x) {
+  AMOD_DPP_GUARD(x);
   int v = __float_as_int(x);
   v = max(v, AMOD_DPP_I(v, 0xB1)); v = max(v, AMOD_DPP_I(v, 0x4E));
   v = max(v, AMOD_DPP_I(v, 0x141)); v = max(v, AMOD_DPP_I(v, 0x140));
@@ -471,7 +480,8 @@ __device__ __forceinline__ float wmax_nn(float x) {
   asm volatile("s_nop 1\n"
                "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
                "s_nop 1\n"
-               "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "s_nop 1" // (before the readlane: see wsum_b4)
                : "+v"(v));
   return __int_as_float(__builtin_amdgcn_readlane(v, 63));
 }
@@ -1425,11 +1435,13 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *mat, int q, uint32
 // broadcasts as DPP xors into v itself (the rows a broadcast does not enable keep theirs)
 __device__ __forceinline__ uint32_t wave_xor_dpp(uint32_t x) {
   int v = (int)x;
+  AMOD_DPP_GUARD(v);
   v ^= AMOD_DPP_I(v, 0xB1); v ^= AMOD_DPP_I(v, 0x4E); v ^= AMOD_DPP_I(v, 0x141); v ^= AMOD_DPP_I(v, 0x140);
   asm volatile("s_nop 1\n"
                "v_xor_b32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
                "s_nop 1\n"
-               "v_xor_b32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               "v_xor_b32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+               "s_nop 1" // (before the readlane: see wsum_b4)
                : "+v"(v));
   return (uint32_t)__builtin_amdgcn_readlane(v, 63);
 }

@@ -392,10 +392,36 @@ function uploadBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
 }
 
 // every record of a batch -> the reference's result objects, in frame order
+// the batch's result objects: successful data-chunk and legacy frames straight from an
+// Int32Array over the records (the same fields, in the same key order, as formatResult,
+// which takes every other outcome)
 function formatBatch(results, payload, stride, n, viaLegacy, share) {
   const view = new DataView(results), u8 = new Uint8Array(payload);
+  const iv = new Int32Array(results, 0, (REC >> 2) * n);
+  const sh = share === true;
   const res = new Array(n);
-  for (let i = 0; i < n; i++) res[i] = formatResult(view, i, payload, stride, viaLegacy, share === true, u8);
+  for (let i = 0; i < n; i++) {
+    const o = (REC >> 2) * i;
+    const frameType = iv[o + 3];
+    if (iv[o] !== 0 || (frameType !== FRAME_DATA && frameType !== 0)) {
+      res[i] = formatResult(view, i, payload, stride, viaLegacy, sh, u8);
+      continue;
+    }
+    const base = i * stride;
+    const dataOff = base + iv[o + 8], dataLen = iv[o + 9];
+    const data = sh ? u8.subarray(dataOff, dataOff + dataLen) : u8.slice(dataOff, dataOff + dataLen);
+    const crcValid = iv[o + 16] !== 0, expectedCRC = iv[o + 14] >>> 0, actualCRC = iv[o + 15] >>> 0;
+    if (frameType === FRAME_DATA) {
+      const r = { frameType: FRAME_DATA, seqNum: iv[o + 10], data, dataLen, crcValid, expectedCRC, actualCRC };
+      if (viaLegacy) r.preambleIdx = iv[o + 1];
+      res[i] = r;
+    } else {
+      res[i] = {
+        data, dataLen, fileName: utf8(u8, base + iv[o + 6], iv[o + 7]), crcValid, expectedCRC, actualCRC,
+        preambleIdx: iv[o + 1], frameType: 'legacy',
+      };
+    }
+  }
   return res;
 }
 

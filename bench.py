@@ -212,7 +212,9 @@ class Workload:
     """One config's synthetic batch on this rank's GPU (built by k_tx, the reference
     transmitter, bit-exact), device-resident, plus its decode step."""
 
-    def __init__(self, env: Env, conf: str, frames: int = 0, snr: float = 20.0):
+    def __init__(self, env: Env, conf: str, frames: int = 0, snr: float = 20.0, rank=None, device=None):
+        # (rank / device: another rank's shard on another device, for the group leg: rank 0
+        # alone building every rank's batch)
         torch, amodem, L = env.torch, env.amodem, env.L
         self.env, self.conf, self.snr = env, conf, snr
         C3, C4, C5 = conf == "c3", conf == "c4", conf == "c5"
@@ -223,9 +225,11 @@ class Workload:
         self.preset = "acoustic" if C5 else "standard"
         F = frames if frames > 0 else (100000 if C3 else (32000 if C4 else 10000))
         self.F = F
-        rank = env.rank
-        dev = env.dev
-        self.dm = amodem.Demodulator(env.local)
+        rank = env.rank if rank is None else rank
+        self.local = env.local if device is None else int(device)
+        dev = env.dev if device is None else torch.device("cuda", self.local)
+        self.dev = dev
+        self.dm = amodem.Demodulator(self.local)
         if C4:
             # the file's chunks this rank owns: chunk seq = rank * F + i, bytes from xorshift32
             pre, post = amodem.tx_silence(self.cfg, L.TX_CHUNK)
@@ -313,7 +317,7 @@ class Workload:
         C5 1.60 -> 1.47; C4, one k_demod launch, no gain). Result buffers alternate, so
         batch i's rows are intact until batch i + 2."""
         torch, amodem = self.env.torch, self.env.amodem
-        self.dm2 = amodem.Demodulator(self.env.local)
+        self.dm2 = amodem.Demodulator(self.local)
         self.dm2.reserve(self.cfg, self.F, int(self.dlens.max()))
         self.d_res2 = torch.zeros_like(self.d_res)
         self.d_pay2 = torch.zeros_like(self.d_pay)
@@ -402,8 +406,20 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     env.barrier()
     elapsed = time.perf_counter() - t0
     if pipe:  # both contexts decoded the same batch: the same records and payload bytes
-        assert wl.d_res2.cpu().numpy().tobytes() == wl.d_res.cpu().numpy().tobytes() and \
-            np.array_equal(wl.d_pay2.cpu().numpy(), wl.d_pay.cpu().numpy()), "pipelined contexts disagree"
+        same_r = wl.d_res2.cpu().numpy().tobytes() == wl.d_res.cpu().numpy().tobytes()
+        same_p = np.array_equal(wl.d_pay2.cpu().numpy(), wl.d_pay.cpu().numpy())
+        if not (same_r and same_p):  # (diagnostics before failing: which frames, which fields)
+            r0 = np.frombuffer(wl.d_res.cpu().numpy().tobytes(), env.amodem.RESULT_DTYPE)
+            r1 = np.frombuffer(wl.d_res2.cpu().numpy().tobytes(), env.amodem.RESULT_DTYPE)
+            p0, p1 = wl.d_pay.view(wl.F, wl.stride).cpu().numpy(), wl.d_pay2.view(wl.F, wl.stride).cpu().numpy()
+            bad = [i for i in range(wl.F) if r0[i].tobytes() != r1[i].tobytes() or p0[i].tobytes() != p1[i].tobytes()]
+            print(f"pipelined contexts disagree on {len(bad)} frames", file=sys.stderr)
+            for i in bad[:8]:
+                print("  frame", i, {n: (r0[n][i].tolist(), r1[n][i].tolist()) for n in r0.dtype.names
+                                     if r0[n][i].tobytes() != r1[n][i].tobytes()}, "flags", hex(int(r0["flags"][i])),
+                      hex(int(r1["flags"][i])), "pv", int(r0["payload_valid"][i]), int(r1["payload_valid"][i]),
+                      "payload bytes differing at", np.nonzero(p0[i] != p1[i])[0][:8].tolist(), file=sys.stderr)
+        assert same_r and same_p, "pipelined contexts disagree"
     L = env.L
     kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
     lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))  # (the profiled steps)
@@ -534,6 +550,7 @@ def gather_leg(env: Env, wl: Workload, reps=3):
         return None
     rec = np.frombuffer(g_res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
     pay = g_pay.cpu().numpy()
+    wl.gathered = rec  # (the group leg compares its records with these)
     noisy = wl.conf == "c5"
     ok = len(rec) == world * F and (noisy or bool(((rec["status"] == 0) & (rec["crc_valid"] == 1)).all()))
     if wl.chunk:
@@ -557,11 +574,15 @@ def scan_phase(env: Env, wl: Workload, reps=20):
     launched with the same LDS footprint so the same number of frames share a CU."""
     amodem, L, lib = env.amodem, env.L, env.lib
     os.environ["AMOD_STOP_AFTER"] = "1"
+    # (its own result buffers: the frames this context lists still go through the exact
+    # kernel, whose full payload rows must not land in the workload's buffers, which the
+    # pipelined steps later compare byte for byte across two contexts)
+    s_res, s_pay = env.torch.zeros_like(wl.d_res), env.torch.zeros_like(wl.d_pay)
     try:
         dm = amodem.Demodulator(env.local)
         dm.reserve(wl.cfg, wl.F, wl.spf)
         run = lambda: dm.decode_device(wl.cfg, L.MODE_RECEIVED, wl.xs.data_ptr(), wl.d_doff.data_ptr(),
-                                       wl.d_dlen.data_ptr(), wl.F, wl.d_res.data_ptr(), wl.d_pay.data_ptr(),
+                                       wl.d_dlen.data_ptr(), wl.F, s_res.data_ptr(), s_pay.data_ptr(),
                                        wl.stride, stream=wl.stream)
         for _ in range(10):  # clocks settle over the first launches
             run()
@@ -575,6 +596,7 @@ def scan_phase(env: Env, wl: Workload, reps=20):
         ms = fm.value / max(1, fn.value)
     finally:
         del os.environ["AMOD_STOP_AFTER"]
+    del s_res, s_pay
     b = 4.0 * wl.ndecoded
     return {"phase": "stream pass + Schmidl-Cox coarse search (k_corr_scan: the same code compiled to stop there, "
                      "results not written; %d launches)" % reps,
@@ -590,20 +612,92 @@ def tx_obj(wl: Workload):
                          "frac": wl.tx_bytes / t / 1e9 / HBM_PEAK_GBS}}
 
 
-def soft_leg(env: Env, wl: Workload, hard_rec):
-    """C5's opt-in soft combining of the repeated bits (AMOD_OPT_SOFT_COMBINE, NOT reference
-    behaviour: the exact kernel demodulates after the fast detection), one timed pass."""
-    torch = env.torch
-    torch.cuda.synchronize()
+def group_leg(env: Env, conf: str, args, snr: float, gathered):
+    """N > 1, rank 0 alone: SURVEY.md §5's one-process design, the drop-in's own multi-GPU
+    path (amod_group_decode_device, Python DeviceGroup; JS decodeBatch({devices})): one host
+    process drives every rank's device, each member context decoding the shard rank k
+    decoded (built again here on device k: the same frames and noise), all at once; K steps
+    of the whole group (enqueue every member, then join), per-device kernel times, and the
+    records compared with the per-rank records the RCCL gather brought to rank 0."""
+    torch, amodem, L, lib = env.torch, env.amodem, env.L, env.lib
+    ndev = max(1, torch.cuda.device_count())
+    devs = [k % ndev for k in range(env.world)]
+    shards = [Workload(env, conf, args.frames, snr, rank=k, device=d) for k, d in enumerate(devs)]
+    g = amodem.DeviceGroup(devs)
+    cfg, mode = shards[0].cfg, shards[0].mode
+    ctxs = [lib.amod_group_context(g._h, k) for k in range(len(devs))]
+    for k, w in enumerate(shards):
+        env.L.check(lib.amod_reserve(ctxs[k], C.byref(cfg), w.F, int(w.dlens.max())))
+    spec = [{"samples": w.xs.data_ptr(), "offsets": w.d_doff.data_ptr(), "lengths": w.d_dlen.data_ptr(),
+             "results": w.d_res.data_ptr(), "payload": w.d_pay.data_ptr(), "payload_stride": w.stride,
+             "nframes": w.F} for w in shards]
+
+    def step():
+        g.decode_device(cfg, mode, spec)
+        g.synchronize()
+
+    warm_up(step, lambda: None, args.warmup)
+    for c in ctxs:
+        lib.amod_set_profiling(c, 1)
     t0 = time.perf_counter()
-    wl.step(options=env.L.OPT_SOFT_COMBINE)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    rec = wl.records()
-    ok_soft = int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum())
-    ok_hard = int(((hard_rec["status"] == 0) & (hard_rec["crc_valid"] == 1)).sum())
-    return {"what": "AMOD_OPT_SOFT_COMBINE (|H|^2-weighted soft vote; not reference behaviour)", "ms": t * 1e3,
-            "frames_crc_valid_soft": ok_soft, "frames_crc_valid_hard": ok_hard}
+    for _ in range(args.steps):
+        step()
+    dt = (time.perf_counter() - t0) / args.steps
+    per_dev = []
+    for k, c in enumerate(ctxs):
+        kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
+        lib.amod_kernel_stages(c, kms, L.STAGE_COUNT, C.byref(kn))
+        lib.amod_set_profiling(c, 0)
+        st = [kms[i] / max(1, kn.value) for i in range(L.STAGE_COUNT)]
+        per_dev.append({"device": devs[k], "frames": shards[k].F, "k_detect_ms": st[L.STAGE_DETECT],
+                        "k_demod_ms": st[L.STAGE_DEMOD], "exact_b_ms": st[L.STAGE_EXACT_B]})
+    rec = np.concatenate([w.records() for w in shards])
+    same = gathered is not None and len(gathered) == len(rec) and \
+        rec.tobytes() == np.ascontiguousarray(gathered).tobytes()
+    nsamp = sum(w.ndecoded for w in shards)
+    out = {"what": "one host process driving %d device contexts (amod_group_decode_device, SURVEY.md section 5), "
+                   "every rank's shard built again on its device; K steps of the whole group" % len(devs),
+           "devices": devs, "ms_per_step": dt * 1e3, "samples_per_s": nsamp / dt, "per_device": per_dev,
+           "records_equal_per_rank": bool(same),
+           "frames_ok": int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum()), "frames": len(rec)}
+    g.close()
+    for w in shards:
+        w.close()
+    return out
+
+
+def soft_leg(env: Env, wl: Workload, steps: int, warmup: int):
+    """C5's opt-in soft combining of the repeated bits (AMOD_OPT_SOFT_COMBINE, NOT reference
+    behaviour: BASELINE C5 names it; k_demod's soft instance, groups whose soft sum lies
+    inside its error bound routed to the exact kernel) against the reference's hard
+    majority vote on the same resident batch: K steps each on one context (no pipelining),
+    per-kernel times, CRC-valid frames and frames the exact kernel decoded."""
+    torch, lib, L = env.torch, env.lib, env.L
+    sync = lambda: torch.cuda.synchronize(env.dev)  # noqa: E731
+    out = {"what": "AMOD_OPT_SOFT_COMBINE (|H|^2-weighted soft vote, k_demod soft instance; not reference "
+                   "behaviour) vs the hard majority vote, K steps each on one context", "frames": wl.F}
+    for name, opt in (("hard", 0), ("soft", L.OPT_SOFT_COMBINE), ("hard_again", 0)):
+        def step(opt=opt):
+            wl.step(options=opt)
+        warm_up(step, sync, warmup)
+        lib.amod_set_profiling(wl.dm.ctx, 1)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync()
+        dt = (time.perf_counter() - t0) / steps
+        kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
+        lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))
+        lib.amod_set_profiling(wl.dm.ctx, 0)
+        st = [kms[i] / max(1, kn.value) for i in range(L.STAGE_COUNT)]
+        rec = wl.records()
+        out[name] = {"ms_per_step": dt * 1e3, "k_detect_ms": st[L.STAGE_DETECT], "k_demod_ms": st[L.STAGE_DEMOD],
+                     "frames_crc_valid": int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum()),
+                     "frames_exact": int(((rec["flags"] & L.FLAG_EXACT) != 0).sum())}
+    hard_ms = min(out["hard"]["ms_per_step"], out["hard_again"]["ms_per_step"])
+    out["soft_over_hard_step"] = out["soft"]["ms_per_step"] / hard_ms
+    return out
 
 
 def e2e_leg(env: Env, wl: Workload, reps=3):
@@ -938,10 +1032,15 @@ def run_leg(env: Env, conf: str, args, frames=0, snr=20.0, primary=False):
     if primary and env.world == 1:  # right after the eager steps, while the clocks are up
         out["graph"] = graph_leg(env, wl, args.steps)
     out["tx"] = tx_obj(wl)
-    if conf == "c5" and args.soft and primary:
-        out["soft_combine"] = soft_leg(env, wl, rec)
+    if conf == "c5" and env.world == 1:
+        progress(f"{conf}: soft combining vs the hard vote")
+        out["soft_combine"] = soft_leg(env, wl, args.steps, args.warmup)
     if env.world > 1:
         out["gather"] = gather_leg(env, wl)
+        if primary and env.rank == 0 and os.environ.get("AMOD_BENCH_GROUP", "1") != "0":
+            progress(f"{conf}: group leg (rank 0 drives every device from one process)")
+            out["group"] = group_leg(env, conf, args, snr, getattr(wl, "gathered", None))
+        env.barrier()
     if primary and not args.no_e2e:
         out["e2e"] = e2e_leg(env, wl)
     # the host entries (Python amod_decode_host, Node decodeBatch) on the batches a host can
@@ -971,7 +1070,8 @@ def main():
                     help="extra legs after the primary one: comma list of c3,c4,c5 (c5 at 10 dB), 'none'; "
                          "auto = c3,c4,c5 with --config c2")
     ap.add_argument("--snr", type=float, default=20.0, help="c5: AWGN SNR in dB (active-sample power)")
-    ap.add_argument("--soft", action="store_true", help="c5: also decode once with AMOD_OPT_SOFT_COMBINE")
+    ap.add_argument("--soft", action="store_true", help="(kept for old command lines: every c5 leg times "
+                    "AMOD_OPT_SOFT_COMBINE against the hard vote)")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames per GPU (0: the config's, C2 10,000 / C3 100,000 / C4 32,000)")
     ap.add_argument("--stream-chunks", type=int, default=-1,
@@ -1014,6 +1114,13 @@ def main():
     for lg in legs:
         name = lg if lg != "c5" else "c5_10db"
         extra[name] = run_leg(env, lg, args, snr=10.0 if lg == "c5" else args.snr)
+    if "c5" in legs and env.world == 1:
+        # soft combining at 7 dB, about the lowest SNR at which the reference still detects
+        # the preambles (it fails at <= 6 dB)
+        progress("c5 at 7 dB: soft combining vs the hard vote")
+        wl7 = Workload(env, "c5", 0, 7.0)
+        extra["c5_soft_7db"] = soft_leg(env, wl7, args.steps, args.warmup)
+        wl7.close()
     if env.rank == 0:
         out = {"metric": METRIC}
         out.update({k: prim[k] for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step")})

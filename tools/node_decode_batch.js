@@ -61,11 +61,12 @@ async function main() {
     modulation: { BPSK: 0, QPSK: 1, QAM16: 2 }[spec.mod], repetition: spec.rep,
   };
   say('native.decodeAsync');
+  const lib = [];
   for (let r = 0; r <= reps; r++) {
     const t0 = process.hrtime.bigint();
-    await modem.native.decodeAsync(x, offs, lens, cfg, spec.chunk ? 1 : 0, 0, spec.device | 0, 1);
+    const o = await modem.native.decodeAsync(x, offs, lens, cfg, spec.chunk ? 1 : 0, 0, spec.device | 0, 1);
     const t1 = process.hrtime.bigint();
-    if (r) nat.push(Number(t1 - t0) / 1e6);
+    if (r) { nat.push(Number(t1 - t0) / 1e6); lib.push(o.nativeMs); }
   }
   // the batch made resident once (uploadBatch), then decodeBatch(DeviceBatch) from HBM:
   // launches, the D2H of records + payload rows and the result objects, no upload
@@ -87,7 +88,7 @@ async function main() {
   process.stdout.write(JSON.stringify({
     what: `decodeBatch(${lens.length} frames) from node ${process.version}: host Float32Array -> N-API -> ` +
       'amod_decode_host -> result objects (fresh data arrays, as the reference), median of ' + reps,
-    ms: med(whole), native_call_ms: med(nat), frames: lens.length, frames_crc_valid: ok,
+    ms: med(whole), native_call_ms: med(nat), library_call_ms: med(lib), frames: lens.length, frames_crc_valid: ok,
     resident: {
       what: 'uploadBatch once, then decodeBatch(DeviceBatch): amod_resident_decode from HBM + D2H + result objects',
       upload_ms, ms: med(resd), frames_crc_valid: rres.filter((r) => r.crcValid === true).length,
