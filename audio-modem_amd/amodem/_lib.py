@@ -108,6 +108,8 @@ class LiveStats(C.Structure):
 
 # (restype, argtypes) for every symbol the header declares
 _P = C.c_void_p
+# amod_progress_fn (include/amodem.h): void (*)(void *user, int32_t frames_done)
+PROGRESS_FN = C.CFUNCTYPE(None, _P, C.c_int32)
 SIGNATURES = {
     "amod_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "amod_close": (C.c_int, [_P]),
@@ -122,6 +124,8 @@ SIGNATURES = {
                                      C.c_uint32, _P]),
     "amod_decode_host": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P, _P,
                                    C.c_int64, C.c_uint32]),
+    "amod_decode_host_progress": (C.c_int, [_P, C.POINTER(Cfg), C.c_int32, _P, C.c_int64, _P, _P, C.c_int32, _P,
+                                            _P, C.c_int64, C.c_uint32, _P, _P]),
     "amod_synchronize": (C.c_int, [_P]),
     "amod_pipe_open": (C.c_int, [_P, _P, C.POINTER(_P)]),
     "amod_pipe_close": (C.c_int, [_P]),

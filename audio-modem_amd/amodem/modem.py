@@ -162,9 +162,12 @@ class Demodulator:
 
     # ---------------------------------------------------------------- host path
     def decode_batch(self, samples: np.ndarray, offsets, lengths, mod="QPSK", rep=1, mode=L.MODE_RECEIVED,
-                     cfg: L.Cfg | None = None, options: int = 0, stride: int | None = None):
+                     cfg: L.Cfg | None = None, options: int = 0, stride: int | None = None, progress=None):
         """Decode frames samples[off:off+len] (host memory, PCIe round trip).
-        Returns (records: RESULT_DTYPE array, payload: uint8 [nframes, stride])."""
+        Returns (records: RESULT_DTYPE array, payload: uint8 [nframes, stride]).
+        progress(done, records, payload): called on this thread whenever frames [0, done)
+        are final in the returned arrays (amod_decode_host_progress), while later frames
+        are still uploading and decoding."""
         samples = np.ascontiguousarray(samples, np.float32)
         offsets = np.ascontiguousarray(offsets, np.int64)
         lengths = np.ascontiguousarray(lengths, np.int32)
@@ -178,10 +181,17 @@ class Demodulator:
         rec = np.zeros(n, RESULT_DTYPE)
         pay = np.zeros((n, stride), np.uint8)
         with self._lock:
-            L.check(self._L.amod_decode_host(self.ctx, C.byref(cfg), mode,
-                                             samples.ctypes.data if samples.size else None, samples.size,
-                                             offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data,
-                                             pay.ctypes.data, stride, options), self.ctx)
+            if progress is None:
+                L.check(self._L.amod_decode_host(self.ctx, C.byref(cfg), mode,
+                                                 samples.ctypes.data if samples.size else None, samples.size,
+                                                 offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data,
+                                                 pay.ctypes.data, stride, options), self.ctx)
+            else:
+                fn = L.PROGRESS_FN(lambda _user, done: progress(int(done), rec, pay))
+                L.check(self._L.amod_decode_host_progress(
+                    self.ctx, C.byref(cfg), mode, samples.ctypes.data if samples.size else None, samples.size,
+                    offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data, pay.ctypes.data, stride, options,
+                    fn, None), self.ctx)
         return rec, pay
 
     def decode_received_signal(self, signal, mod="QPSK", rep=1, options=0) -> dict:

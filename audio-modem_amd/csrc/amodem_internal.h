@@ -167,6 +167,8 @@ struct Knobs {
   bool no_replay = false;   // AMOD_NO_REPLAY: listed frames demodulate in the replica too
   bool exact_serial = false;// AMOD_EXACT_SERIAL: list A after k_demod on the launch stream
   int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
+  int pipe_stagger = 1;     // AMOD_PIPE_STAGGER: a pipe decode starts once the other slot's
+                            // k_detect is done (detections back to back, k_demod beside)
   int64_t mall_flush_mb = 0; // AMOD_MALL_FLUSH_MB: stream this many MB of a scratch buffer
                             // between k_detect and k_demod (experiments: Infinity Cache probe)
   bool demod_static = false;// AMOD_DEMOD_STATIC: k_demod takes every frame by the static stride
@@ -572,6 +574,9 @@ hipError_t amod_launch_gather(const float *y, const int32_t *src, int ng, float 
 int amod_ctx_device(const amod_ctx *ctx);
 hipStream_t amod_ctx_stream(const amod_ctx *ctx);
 const amod::Knobs *amod_ctx_knobs(const amod_ctx *ctx); // read once at amod_open
+// the event recorded on the launch stream right after the latest decode's k_detect (null if
+// that decode had none: chunk mode, chunked or serial diagnostics, a captured decode)
+hipEvent_t amod_ctx_detect_event(const amod_ctx *ctx);
 int amod_ctx_fail(amod_ctx *ctx, const char *msg, int code);
 // per-context state owned by another module (slot: 0 = streaming receiver): *amod_ctx_ext
 // holds it; free_fn runs at amod_close, after the context's streams are drained

@@ -1744,7 +1744,10 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
     kn_neg |= (uint32_t)pin << 8;
     kn_neg |= (uint32_t)(pin && cfg.t.known[kq - sub_start] < 0.f) << 9;
   }
-  const bool pil16 = cfg.npilots <= 16; // (wave-uniform) the pilot sums reduce over row 0
+  // bit 10: (wave-uniform) the pilot sums reduce over row 0; bit 11: chunk mode. Read per
+  // job from the VGPR with one v_readfirstlane: as scalars the two flags were 64-bit lane
+  // masks the full SGPR file spilled and read back (four v_readlane a job)
+  kn_neg |= (cfg.npilots <= 16 ? 1u << 10 : 0u) | (chunk_mode ? 1u << 11 : 0u);
 
   // Frames (last-first: frame f1 - 1 - k for the k-th) by a static stride for the first
   // rounds, then one at a time from the claim counter (w.claim). Waves on one SIMD do not
@@ -1854,6 +1857,13 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
     if (hdr) *hdr = __builtin_amdgcn_readfirstlane(fin);
     return __builtin_amdgcn_readfirstlane(need);
   };
+  // the last data symbol holding bits of the first `need` parsed bytes. need * 8 * rep is
+  // at most the frame's bit count (eval_need never returns more than the decoded bytes), an
+  // int: 32-bit unsigned arithmetic (the int64 division was a ~140-SALU software routine)
+  auto last_sym_of = [&](int need) -> int {
+    const uint32_t nb = (uint32_t)need * 8u * (uint32_t)rep;
+    return (int)((nb + (uint32_t)per_sym - 1u) / (uint32_t)per_sym) - 1;
+  };
   // one job of frame `cur` (jcur = 0 starts the frame; a frame without data symbols has
   // one empty job, so every frame passes through its frame end)
   // c1 / c2: the job's samples; issue_next() refills them with the next job's once they
@@ -1921,6 +1931,8 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       // per-job copies of the lane's slot facts: their comparisons are made where they are
       // used instead of held as lane masks across the loop (SGPR pairs that spill)
       asm volatile("" : "+v"(di_pk[0]), "+v"(di_pk[1]), "+v"(kn_neg), "+v"(paddr));
+      const uint32_t kmode = __builtin_amdgcn_readfirstlane(kn_neg);
+      const bool pil16 = (kmode >> 10) & 1, chunk_j = (kmode >> 11) & 1;
       // the band: slot rr of lane ln is subcarrier b = bo + 64 rr, bins k = k0 + 64 rr and
       // 512 - k (spec_idx(n +- 64) = spec_idx(n) +- 64: one base per side, immediate offsets)
       const int bo = (ln - sub_start) & 63; // (recomputed per job: no VGPR held across the loop)
@@ -1947,7 +1959,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         // chunk mode, `x || 0` semantics on the exact path: a NaN/Inf sample makes every bin
         // of Z non-finite (each bin is a sum over all 512 inputs with non-zero weights, and
         // Inf * 0 is NaN), so one bin pair per lane stands in for the 1024 samples
-        if (rr == 0 && chunk_mode && !KO(8) && __ballot(!isfinite(zk.x + zk.y + zn.x + zn.y)))
+        if (rr == 0 && chunk_j && !KO(8) && __ballot(!isfinite(zk.x + zk.y + zn.x + zn.y)))
           wflags |= AMOD_FLAG_NONFINITE;
         if (rr == NS - 1) { // the last slot may be partly filled
           const bool in = bo + 64 * rr < nband;
@@ -2275,7 +2287,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         if (need < 0 && hdr) need = -1 - need; // header decoded: the byte count is final
         if (need >= 0) {
           // jobs holding the last data symbol the parse reads (job j: symbols 2j-1, 2j)
-          const int ls = need > 0 ? (int)(((int64_t)need * 8 * rep + per_sym - 1) / per_sym) - 1 : 0;
+          const int ls = need > 0 ? last_sym_of(need) : 0;
           const int jn = ls <= 0 ? 1 : (ls + 1) / 2 + 1;
           const int availT = (min(cur.T * per_sym, cur.M * per_sym) / rep) >> 3;
           if (need > availT) {
@@ -2300,7 +2312,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         if (need < 0) wflags |= AMOD_FLAG_SPAN;
       }
       // the last data symbol whose bits the parse reads
-      const int last_sym = need > 0 ? (int)(((int64_t)need * 8 * rep + per_sym - 1) / per_sym) - 1 : -1;
+      const int last_sym = need > 0 ? last_sym_of(need) : -1;
       if (flag_sym <= last_sym) wflags |= sflags;
       DSTAMP(23, true);
       if (KO(0xFFFF)) wflags = 0;
@@ -2367,11 +2379,12 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
             put(ib, qb);
           }
           if (DBG && lane == 0) D->nsym = cur.M;
-          // the record: 24 words, one per lane
+          // the record: 24 words, one per lane (lane writes, not 24 lane==i masks: those are
+          // loop-invariant, get hoisted out of the persistent loop and spill 48 SGPRs)
           const int32_t *const rw = reinterpret_cast<const int32_t *>(&r);
           int32_t val = 0;
 #pragma unroll
-          for (int i = 0; i < 24; ++i) val = lane == i ? rw[i] : val;
+          for (int i = 0; i < 24; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(val) : "s"(__builtin_amdgcn_readfirstlane(rw[i])), "n"(i));
           if (lane < 24) reinterpret_cast<int32_t *>(w.res + f)[lane] = val;
           DSTAMP(26, true);
         }

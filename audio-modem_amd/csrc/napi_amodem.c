@@ -227,6 +227,7 @@ typedef struct {
   void *results, *payload; /* ArrayBuffer backing stores (owned by JS objects) */
   int rc;
   double native_ms; /* wall time of the library call (run_decode), for the bench's split */
+  napi_threadsafe_function progress; /* decodeAsync's onFrames(done, results, payload, stride) */
   char err[256];
   /* async only */
   napi_ref refs[3];
@@ -323,6 +324,39 @@ static int prepare(napi_env env, napi_callback_info info, decode_job *j, napi_va
   return 1;
 }
 
+/* onFrames: called on the JS thread, in order, whenever records [0, done) are in the
+ * results/payload buffers (amod_decode_host_progress), so the caller formats those frames
+ * while the library decodes the rest. The call context outlives the decode job: queued
+ * calls may run after the promise settled (the finalizer frees it) */
+typedef struct {
+  napi_ref res_ref, pay_ref;
+  double stride;
+} progress_ctx;
+
+static void progress_call_js(napi_env env, napi_value cb, void *context, void *data) {
+  progress_ctx *pc = (progress_ctx *)context;
+  if (!env || !cb) return;
+  napi_value argv[4], undef;
+  if (napi_create_int32(env, (int32_t)(intptr_t)data, &argv[0]) != napi_ok ||
+      napi_get_reference_value(env, pc->res_ref, &argv[1]) != napi_ok ||
+      napi_get_reference_value(env, pc->pay_ref, &argv[2]) != napi_ok ||
+      napi_create_double(env, pc->stride, &argv[3]) != napi_ok || napi_get_undefined(env, &undef) != napi_ok)
+    return;
+  napi_call_function(env, undef, cb, 4, argv, NULL);
+}
+
+static void progress_finalize(napi_env env, void *data, void *hint) {
+  (void)hint;
+  progress_ctx *pc = (progress_ctx *)data;
+  napi_delete_reference(env, pc->res_ref);
+  napi_delete_reference(env, pc->pay_ref);
+  free(pc);
+}
+
+static void progress_native(void *user, int32_t done) {
+  napi_call_threadsafe_function((napi_threadsafe_function)user, (void *)(intptr_t)done, napi_tsfn_nonblocking);
+}
+
 static void run_decode(decode_job *j) {
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
@@ -333,6 +367,10 @@ static void run_decode(decode_job *j) {
     j->rc = amod_group_decode_host(j->group, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths,
                                    j->nframes, (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options,
                                    NULL);
+  else if (j->progress)
+    j->rc = amod_decode_host_progress(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths,
+                                      j->nframes, (amod_result *)j->results, (uint8_t *)j->payload, j->stride,
+                                      j->options, progress_native, (void *)j->progress);
   else
     j->rc = amod_decode_host(j->ctx, &j->cfg, j->mode, j->samples, j->nsamples, j->offsets, j->lengths, j->nframes,
                              (amod_result *)j->results, (uint8_t *)j->payload, j->stride, j->options);
@@ -400,7 +438,18 @@ static void async_complete(napi_env env, napi_status status, void *data) {
   napi_delete_reference(env, j->res_ref);
   napi_delete_reference(env, j->pay_ref);
   napi_delete_async_work(env, j->work);
+  if (j->progress) napi_release_threadsafe_function(j->progress, napi_tsfn_release);
   if (j->box && --j->box->busy == 0 && j->box->free_pending) resident_release(j->box);
+  free_job(j);
+  free(j);
+}
+
+/* a job whose promise was never created: drop its references and memory */
+static void async_discard(napi_env env, decode_job *j) {
+  for (int i = 0; i < 3; ++i)
+    if (j->refs[i]) napi_delete_reference(env, j->refs[i]);
+  napi_delete_reference(env, j->res_ref);
+  napi_delete_reference(env, j->pay_ref);
   free_job(j);
   free(j);
 }
@@ -423,8 +472,30 @@ static napi_value js_decode_async(napi_env env, napi_callback_info info) {
   napi_create_reference(env, j->res_ab, 1, &j->res_ref);
   napi_create_reference(env, j->pay_ab, 1, &j->pay_ref);
   napi_value promise, name;
-  NAPI_TRY(env, napi_create_promise(env, &j->deferred, &promise));
   NAPI_TRY(env, napi_create_string_utf8(env, "amodem.decode", NAPI_AUTO_LENGTH, &name));
+  { /* optional 9th argument: onFrames (single-device host decodes) */
+    size_t argc = 9;
+    napi_value argv[9];
+    napi_valuetype t = napi_undefined;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 9) napi_typeof(env, argv[8], &t);
+    if (t == napi_function && j->ctx) {
+      progress_ctx *pc = (progress_ctx *)calloc(1, sizeof *pc);
+      if (!pc) {
+        async_discard(env, j);
+        return throw_msg(env, "out of memory");
+      }
+      pc->stride = (double)j->stride;
+      napi_create_reference(env, j->res_ab, 1, &pc->res_ref);
+      napi_create_reference(env, j->pay_ab, 1, &pc->pay_ref);
+      if (napi_create_threadsafe_function(env, argv[8], NULL, name, 0, 1, pc, progress_finalize, pc, progress_call_js,
+                                          &j->progress) != napi_ok) {
+        progress_finalize(env, pc, NULL);
+        async_discard(env, j);
+        return throw_msg(env, "cannot create the progress callback");
+      }
+    }
+  }
+  NAPI_TRY(env, napi_create_promise(env, &j->deferred, &promise));
   NAPI_TRY(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
   NAPI_TRY(env, napi_queue_async_work(env, j->work));
   return promise;

@@ -100,6 +100,16 @@ extern "C" int amod_pipe_decode_device(amod_pipe *p, const amod_cfg *cfg, int32_
     PIPE_TRY(p, hipEventRecord(p->ev_in, s));
     PIPE_TRY(p, hipStreamWaitEvent(w, p->ev_in, 0));
   }
+  // Staggered slots: this decode starts once the other slot's latest k_detect is done, so
+  // the detections (HBM-bound stream passes) run back to back and each k_demod runs beside
+  // the next batch's detection. Unstaggered, both slots' k_detect ran at once, then both
+  // k_demod: the overlap was only the kernels' tails and gaps
+  if (amod_ctx_knobs(c)->pipe_stagger) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    PIPE_TRY(p, hipStreamIsCapturing(w, &cs));
+    const hipEvent_t ev = amod_ctx_detect_event(p->ctx[k ^ 1]);
+    if (ev && cs == hipStreamCaptureStatusNone) PIPE_TRY(p, hipStreamWaitEvent(w, ev, 0));
+  }
   const int rc = amod_decode_device(c, cfg, mode, samples, offsets, lengths, nframes, results, payload,
                                     payload_stride, options, w);
   if (rc != AMOD_SUCCESS) {

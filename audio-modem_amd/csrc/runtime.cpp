@@ -217,6 +217,20 @@ struct DevBuf {
   }
 };
 
+// Grow-only pinned host buffer (amod_decode_host's per-piece copies of the outputs)
+struct HostBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  ~HostBuf() { if (p) (void)hipHostFree(p); }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+    hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault);
+    if (e == hipSuccess) n = std::max<size_t>(bytes, 256);
+    return e;
+  }
+};
+
 struct TableSet {
   DevBuf buf;
   amod::DevCfg cfg{};
@@ -254,6 +268,7 @@ struct amod_ctx {
   // and last launches (DevWork::fb_zero, fb_reset). fb_zeroed: they are zero when this decode's
   // launches run; a reallocation or an aborted launch sequence clears it (memset)
   bool fb_zeroed = false;
+  bool detect_ev = false; // chunk_ev[0] marks the end of the latest decode's k_detect (pipes)
   bool fb_captured = false; // a decode was captured into a hipGraph: a buffer that grows is
                             // kept (not freed) until amod_close, for the graph's replays
   void *ext[4] = {nullptr, nullptr, nullptr, nullptr}; // other modules' per-context state
@@ -274,6 +289,10 @@ struct amod_ctx {
   // amod_decode_host's pipeline: the upload stream and one event per uploaded piece
   hipStream_t up = nullptr;
   std::vector<hipEvent_t> up_ev;
+  // ... and its outputs: each piece's records and payload slots come back (DMA into pinned
+  // mirrors, one event per piece) while later pieces upload, then go to the caller's buffers
+  HostBuf pin_res, pin_payload;
+  std::vector<hipEvent_t> dn_ev;
   std::mutex mu;
   DevBuf stamps;
   DevBuf flush; // AMOD_MALL_FLUSH_MB scratch (experiments)
@@ -315,6 +334,7 @@ void read_knobs(amod::Knobs &k) {
   k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
   if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
   k.aux_priority = env_int("AMOD_AUX_PRIORITY", 1);
+  k.pipe_stagger = env_int("AMOD_PIPE_STAGGER", 1);
   k.demod_static = getenv("AMOD_DEMOD_STATIC") != nullptr;
   k.claim_rounds = std::max(1, env_int("AMOD_CLAIM_ROUNDS", 2));
   k.claim_min = std::max(2, env_int("AMOD_CLAIM_MIN", 4));
@@ -625,6 +645,7 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
   if (cap != hipStreamCaptureStatusNone) ctx->fb_captured = true;
   if (!ctx->fb_zeroed) HIP_TRY(hipMemsetAsync(fb_base, 0, 256, s)); // after a reallocation or an aborted decode
   ctx->fb_zeroed = false; // until this decode's list-B launch is enqueued with its reset
+  ctx->detect_ev = false;
   std::array<hipEvent_t, 6> ev{};
   if (ctx->profiling) {
     if (ctx->ev_free.empty()) {
@@ -710,15 +731,28 @@ int decode_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *s
       // list A is complete: the exact replica of the frames detection listed (long
       // sequential recurrences) runs on the second stream, under k_demod
       // (AMOD_EXACT_SERIAL, diagnostics: after it, on the same stream)
-      if (ctx->knobs.exact_serial) {
+      // Chunk mode: list A holds only frames routed before any demodulation (FORCE_EXACT,
+      // longer than the fast-path workspace, soft combining off the fast path), usually
+      // none, so it runs after k_demod on the same stream: an empty list then costs one
+      // dispatch instead of a launch parked on the aux stream for all of k_demod and the
+      // join; a batch with such frames decodes them after the fast ones.
+      if (ctx->knobs.exact_serial || mode == AMOD_MODE_CHUNK) {
         wb.f0 = 0; wb.f1 = nframes;
-        HIP_TRY(amod_launch_demod(d, wb, demod_blocks(nframes), s));
+        amod::DevWork wm = wb;
+        if (!ctx->knobs.exact_serial) {
+          wm.tl = tl;
+          wm.claim = ctx->knobs.demod_static ? nullptr : fb + 3;
+          wm.claim_rounds = ctx->knobs.claim_rounds;
+          wm.claim_min = ctx->knobs.claim_min;
+        }
+        HIP_TRY(amod_launch_demod(d, wm, demod_blocks(nframes), s));
         HIP_TRY(mark(2));
         rc = exact_a(s);
         if (rc) return rc;
         HIP_TRY(mark(3));
       } else {
       HIP_TRY(hipEventRecord(ctx->chunk_ev[0], s));
+      ctx->detect_ev = cap == hipStreamCaptureStatusNone;
       HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->chunk_ev[0], 0));
       rc = exact_a(ctx->aux);
       if (rc) return rc;
@@ -892,6 +926,7 @@ int amod_abi_version(void) { return AMOD_ABI_VERSION; }
 
 int amod_close(amod_ctx *ctx);
 const amod::Knobs *amod_ctx_knobs(const amod_ctx *ctx) { return ctx ? &ctx->knobs : nullptr; }
+hipEvent_t amod_ctx_detect_event(const amod_ctx *ctx) { return ctx && ctx->detect_ev ? ctx->chunk_ev[0] : nullptr; }
 
 int amod_ctx_device(const amod_ctx *ctx) { return ctx ? ctx->device : 0; }
 hipStream_t amod_ctx_stream(const amod_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
@@ -958,6 +993,7 @@ int amod_close(amod_ctx *ctx) {
     (void)hipStreamDestroy(ctx->up);
   }
   for (hipEvent_t e : ctx->up_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->dn_ev) (void)hipEventDestroy(e);
   for (void *p : ctx->retired) (void)hipFree(p);
   for (auto &ev : ctx->ev_free) for (auto &e : ev) (void)hipEventDestroy(e);
   delete ctx;
@@ -1042,9 +1078,11 @@ int amod_decode_device_debug(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, c
                      (hipStream_t)stream, debug, -1);
 }
 
-int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, int64_t nsamples,
+namespace {
+int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, int64_t nsamples,
                      const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
-                     uint8_t *payload, int64_t payload_stride, uint32_t options) {
+                     uint8_t *payload, int64_t payload_stride, uint32_t options, amod_progress_fn progress,
+                     void *user) {
   if (!ctx) return fail(nullptr, "null context", AMOD_ERR_ARG);
   if (nframes < 0 || nsamples < 0) return fail(ctx, "negative size", AMOD_ERR_ARG);
   for (int32_t i = 0; i < nframes; ++i)
@@ -1058,6 +1096,8 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   HIP_TRY(ctx->h_len.ensure(sizeof(int32_t) * (size_t)nframes));
   HIP_TRY(ctx->h_res.ensure(sizeof(amod_result) * (size_t)nframes));
   HIP_TRY(ctx->h_payload.ensure((size_t)payload_stride * (size_t)nframes));
+  HIP_TRY(ctx->pin_res.ensure(sizeof(amod_result) * (size_t)nframes));
+  HIP_TRY(ctx->pin_payload.ensure((size_t)payload_stride * (size_t)nframes));
   hipStream_t s = ctx->stream;
   if (!ctx->up) HIP_TRY(hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking));
   HIP_TRY(hipMemcpyAsync(ctx->h_off.p, offsets, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
@@ -1095,6 +1135,31 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
       return rc;
     }
   }
+  // every launch's frames [a, b) come back on the context stream right after it; a piece
+  // whose copy has landed goes to the caller's buffers (and `progress`) between uploads
+  struct Back { hipEvent_t ev; int32_t a, b; };
+  std::vector<Back> back;
+  size_t nback = 0; // back[0 .. nback) are in the caller's buffers
+  auto deliver = [&](const Back &k) {
+    std::memcpy(results + k.a, (const amod_result *)ctx->pin_res.p + k.a, sizeof(amod_result) * (size_t)(k.b - k.a));
+    std::memcpy(payload + (int64_t)k.a * payload_stride, (const uint8_t *)ctx->pin_payload.p + (int64_t)k.a * payload_stride,
+                (size_t)payload_stride * (size_t)(k.b - k.a));
+    if (progress) progress(user, k.b);
+  };
+  auto drain = [&](bool wait) -> hipError_t {
+    for (; nback < back.size(); ++nback) {
+      if (wait) {
+        const hipError_t e = hipEventSynchronize(back[nback].ev);
+        if (e != hipSuccess) return e;
+      } else {
+        const hipError_t e = hipEventQuery(back[nback].ev);
+        if (e == hipErrorNotReady) return hipSuccess;
+        if (e != hipSuccess) return e;
+      }
+      deliver(back[nback]);
+    }
+    return hipSuccess;
+  };
   int32_t a = 0; // the first frame not yet enqueued
   for (int64_t p = 0; p <= npiece; ++p) {
     int64_t covered = nsamples;
@@ -1116,14 +1181,43 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
                                nullptr, call_max);
     if (rc) {
       (void)hipStreamSynchronize(ctx->up);
+      (void)hipStreamSynchronize(s);
       return rc;
     }
+    if (back.size() == ctx->dn_ev.size()) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->dn_ev.push_back(e);
+    }
+    const Back k{ctx->dn_ev[back.size()], a, b};
+    HIP_TRY(hipMemcpyAsync((amod_result *)ctx->pin_res.p + a, (const amod_result *)ctx->h_res.p + a,
+                           sizeof(amod_result) * (size_t)(b - a), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync((uint8_t *)ctx->pin_payload.p + (int64_t)a * payload_stride,
+                           (const uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride,
+                           (size_t)payload_stride * (size_t)(b - a), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(k.ev, s));
+    back.push_back(k);
+    HIP_TRY(drain(false));
     a = b;
   }
-  HIP_TRY(hipMemcpyAsync(results, ctx->h_res.p, sizeof(amod_result) * nframes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(payload, ctx->h_payload.p, (size_t)payload_stride * nframes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(drain(true));
   return AMOD_SUCCESS;
+}
+} // namespace
+
+int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples, int64_t nsamples,
+                     const int64_t *offsets, const int32_t *lengths, int32_t nframes, amod_result *results,
+                     uint8_t *payload, int64_t payload_stride, uint32_t options) {
+  return decode_host_impl(ctx, cfg, mode, samples, nsamples, offsets, lengths, nframes, results, payload,
+                          payload_stride, options, nullptr, nullptr);
+}
+
+int amod_decode_host_progress(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
+                              int64_t nsamples, const int64_t *offsets, const int32_t *lengths, int32_t nframes,
+                              amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options,
+                              amod_progress_fn progress, void *user) {
+  return decode_host_impl(ctx, cfg, mode, samples, nsamples, offsets, lengths, nframes, results, payload,
+                          payload_stride, options, progress, user);
 }
 
 int amod_synchronize(amod_ctx *ctx) {

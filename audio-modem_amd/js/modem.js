@@ -345,21 +345,44 @@ function decodeChunkFrame(frameSamples, modName, repetition) {
 // Every result's `data` is a fresh Uint8Array, as the reference's (bytes.slice,
 // modem.js:636,837); shareBuffers: true makes them views of one payload buffer per call
 // instead (no per-frame copy; `data.buffer` then holds every frame's bytes, and keeping
-// one result keeps that buffer alive).
+// one result keeps that buffer alive). onProgress(done, results): called as results[0 ..
+// done) are final (host samples on one device: after each decoded 64 MB piece; otherwise
+// once), before the promise resolves with the same array.
 function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
   const o = opts || {};
   const mode = o.mode === 'chunk' || o.mode === MODE_CHUNK ? MODE_CHUNK : MODE_RECEIVED;
   const cfg = nativeCfg(modName, rep);
   const share = o.shareBuffers === true;
+  const whole = (out, n) => {
+    const r = formatBatch(out.results, out.payload, out.stride, n, mode === MODE_RECEIVED, share);
+    if (o.onProgress) o.onProgress(n, r);
+    return r;
+  };
   if (samples instanceof DeviceBatch) {
     return native.residentDecodeAsync(samples.handle, cfg, mode, o.forceExact ? 1 : 0)
-      .then((out) => formatBatch(out.results, out.payload, out.stride, samples.nframes, mode === MODE_RECEIVED, share));
+      .then((out) => whole(out, samples.nframes));
   }
   const offs = frameOffsets instanceof Float64Array ? frameOffsets : Float64Array.from(frameOffsets);
   const lens = frameLens instanceof Int32Array ? frameLens : Int32Array.from(frameLens);
+  const n = lens.length, viaLegacy = mode === MODE_RECEIVED;
+  // one device: the frames of each decoded 64 MB piece are formatted as soon as they are
+  // back (onFrames, amod_decode_host_progress), while the library uploads and decodes the
+  // rest; what is left when the promise settles is formatted then
+  const res = new Array(n);
+  let done = 0;
+  const onFrames = (upto, results, payload, stride) => {
+    if (upto > done) {
+      formatBatch(results, payload, stride, upto, viaLegacy, share, res, done);
+      done = upto;
+      if (o.onProgress) o.onProgress(done, res);
+    }
+  };
   return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0,
-    Math.max(1, o.devices | 0))
-    .then((out) => formatBatch(out.results, out.payload, out.stride, lens.length, mode === MODE_RECEIVED, share));
+    Math.max(1, o.devices | 0), onFrames)
+    .then((out) => {
+      onFrames(n, out.results, out.payload, out.stride);
+      return res;
+    });
 }
 
 // A batch made resident on GPUs 0 .. devices-1 once (amod_group_upload: contiguous frame
@@ -395,12 +418,13 @@ function uploadBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
 // the batch's result objects: successful data-chunk and legacy frames straight from an
 // Int32Array over the records (the same fields, in the same key order, as formatResult,
 // which takes every other outcome)
-function formatBatch(results, payload, stride, n, viaLegacy, share) {
+// (into `into` from frame `from` on, when given: decodeBatch formats piece by piece)
+function formatBatch(results, payload, stride, n, viaLegacy, share, into, from) {
   const view = new DataView(results), u8 = new Uint8Array(payload);
   const iv = new Int32Array(results, 0, (REC >> 2) * n);
   const sh = share === true;
-  const res = new Array(n);
-  for (let i = 0; i < n; i++) {
+  const res = into || new Array(n);
+  for (let i = from | 0; i < n; i++) {
     const o = (REC >> 2) * i;
     const frameType = iv[o + 3];
     if (iv[o] !== 0 || (frameType !== FRAME_DATA && frameType !== 0)) {

@@ -49,11 +49,15 @@ async function main() {
         case 'decode_chunk': r = M.decodeChunkFrame(f32(j.file), j.mod, j.rep); break;
         case 'loopback': r = M.analyzeLoopback(f32(j.file), j.mod, j.rep, Uint8Array.from(j.testData)); break;
         case 'decode_batch': {
+          // onProgress: every call's prefix is final (compared with the resolved results below)
+          const progress = [], early = [];
           r = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep,
-            { mode: j.mode, devices: j.devices, shareBuffers: j.share === true });
+            { mode: j.mode, devices: j.devices, shareBuffers: j.share === true,
+              onProgress: (done, res) => { progress.push(done); early.push(JSON.stringify(enc(res.slice(0, done)))); } });
           // data ownership: fresh arrays (the reference's bytes.slice) unless shareBuffers
           const own = r.every((x) => !x.data || (x.data.byteOffset === 0 && x.data.buffer.byteLength === x.data.length));
-          r = { results: r, ownData: own };
+          const prefixes_final = early.every((e, k) => e === JSON.stringify(enc(r.slice(0, progress[k]))));
+          r = { results: r, ownData: own, progress, prefixes_final };
           break;
         }
         case 'decode_resident': {

@@ -82,6 +82,34 @@ def test_host_pipeline_pieces(monkeypatch, piece):
     assert (ref["status"] == 0).all()
 
 
+def test_host_progress_prefixes_final(monkeypatch):
+    """amod_decode_host_progress: each decoded piece's records and payload rows come back
+    while later pieces upload; progress(done) runs with done increasing to nframes, and
+    every prefix it reports is already final (equals the returned arrays and the plain
+    amod_decode_host result). In-order frames report as pieces complete; permuted ones
+    only after the last piece."""
+    cfg, x, offs, lens = _batch()
+    dm = amodem.Demodulator(0)
+    ref, rpay = dm.decode_batch(x, offs, lens, cfg=cfg)
+    dm.close()
+    monkeypatch.setenv("AMOD_UP_PIECE", "40000")
+    dm = amodem.Demodulator(0)
+    for order in (np.arange(len(offs)), np.random.default_rng(3).permutation(len(offs))):
+        seen = []
+        rec, pay = dm.decode_batch(x, offs[order], lens[order], cfg=cfg,
+                                   progress=lambda d, r, p: seen.append((d, r[:d].copy(), p[:d].copy())))
+        done = [d for d, _, _ in seen]
+        assert done[-1] == len(offs) and all(a < b for a, b in zip(done, done[1:])), done
+        for d, r, p in seen:
+            assert r.tobytes() == rec[:d].tobytes() and np.array_equal(p, pay[:d]), d
+        for n in amodem.RESULT_DTYPE.names:
+            assert (rec[n] == ref[n][order]).all(), n
+        assert np.array_equal(pay, rpay[order])
+        if order[0] == 0 and order[-1] == len(offs) - 1:
+            assert len(done) > 2, done  # in order: reported piece by piece
+    dm.close()
+
+
 def _assert_same(rec, pay, ref, rpay):
     for n in amodem.RESULT_DTYPE.names:
         if n == "reserved":

@@ -206,6 +206,31 @@ def test_decode_batch_through_js(tmp_path):
     assert got["ownData"]  # every `data` a fresh Uint8Array, as bytes.slice (modem.js:636,837)
     shared = ok(res, "s")  # shareBuffers: the same results, views of one payload buffer
     assert shared["results"] == got["results"] and not shared["ownData"]
+    assert got["progress"][-1] == len(sel) and got["prefixes_final"]
+
+
+@pytest.mark.gpu
+def test_decode_batch_progress_through_js(tmp_path):
+    """decodeBatch formats each uploaded piece's frames while the library decodes the rest
+    (amod_decode_host_progress, a napi threadsafe callback): with 16 KB upload pieces (the
+    runtime's AMOD_UP_PIECE test knob) the frames come back in many steps; every onProgress
+    prefix is already final and the results equal the golden ones, plain and shared."""
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["mod"] == "QPSK"
+           and f["rep"] == 1]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    job = {"op": "decode_batch", "config": "standard", "file": str(fn), "offsets": offs,
+           "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1}
+    res = run([dict(job, id="b"), dict(job, id="s", share=True)], tmp_path, env={"AMOD_UP_PIECE": "4096"})
+    for key in ("b", "s"):
+        got = ok(res, key)
+        assert got["results"] == [f["result"] for f in sel], key
+        pr = got["progress"]
+        assert len(pr) > 1 and pr[-1] == len(sel) and all(a < b for a, b in zip(pr, pr[1:])), pr
+        assert got["prefixes_final"], key
 
 
 @pytest.mark.gpu
