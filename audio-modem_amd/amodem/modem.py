@@ -165,9 +165,10 @@ class Demodulator:
                      cfg: L.Cfg | None = None, options: int = 0, stride: int | None = None, progress=None):
         """Decode frames samples[off:off+len] (host memory, PCIe round trip).
         Returns (records: RESULT_DTYPE array, payload: uint8 [nframes, stride]).
-        progress(done, records, payload): called on this thread whenever frames [0, done)
-        are final in the returned arrays (amod_decode_host_progress), while later frames
-        are still uploading and decoding."""
+        progress(done, records, payload): called (from the library's helper thread, one
+        call at a time, all before this returns) whenever frames [0, done) are final in the
+        returned arrays (amod_decode_host_progress), while later frames are still
+        uploading and decoding."""
         samples = np.ascontiguousarray(samples, np.float32)
         offsets = np.ascontiguousarray(offsets, np.int64)
         lengths = np.ascontiguousarray(lengths, np.int32)

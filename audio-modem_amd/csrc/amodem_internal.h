@@ -167,7 +167,7 @@ struct Knobs {
   bool no_replay = false;   // AMOD_NO_REPLAY: listed frames demodulate in the replica too
   bool exact_serial = false;// AMOD_EXACT_SERIAL: list A after k_demod on the launch stream
   int64_t up_piece = 0;     // AMOD_UP_PIECE: amod_decode_host upload piece (samples; 0: 64 MB)
-  int pipe_stagger = 1;     // AMOD_PIPE_STAGGER: a pipe decode starts once the other slot's
+  int pipe_stagger = 0;     // AMOD_PIPE_STAGGER: a pipe decode starts once the other slot's
                             // k_detect is done (detections back to back, k_demod beside)
   int64_t mall_flush_mb = 0; // AMOD_MALL_FLUSH_MB: stream this many MB of a scratch buffer
                             // between k_detect and k_demod (experiments: Infinity Cache probe)

@@ -12,10 +12,12 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -334,7 +336,7 @@ void read_knobs(amod::Knobs &k) {
   k.exact_serial = getenv("AMOD_EXACT_SERIAL") != nullptr;
   if (const char *e = getenv("AMOD_UP_PIECE")) k.up_piece = std::max<int64_t>(0, atoll(e));
   k.aux_priority = env_int("AMOD_AUX_PRIORITY", 1);
-  k.pipe_stagger = env_int("AMOD_PIPE_STAGGER", 1);
+  k.pipe_stagger = env_int("AMOD_PIPE_STAGGER", 0);
   k.demod_static = getenv("AMOD_DEMOD_STATIC") != nullptr;
   k.claim_rounds = std::max(1, env_int("AMOD_CLAIM_ROUNDS", 2));
   k.claim_min = std::max(2, env_int("AMOD_CLAIM_MIN", 4));
@@ -1135,31 +1137,55 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
       return rc;
     }
   }
-  // every launch's frames [a, b) come back on the context stream right after it; a piece
-  // whose copy has landed goes to the caller's buffers (and `progress`) between uploads
+  // every launch's frames [a, b) come back on the context stream right after it (DMA into
+  // the pinned mirrors); a helper thread waits for each piece's copy, moves it into the
+  // caller's buffers and reports it, so the calling thread keeps staging the uploads (the
+  // copies into fresh pageable memory fault page by page: on the calling thread they
+  // delayed the next pieces' uploads)
   struct Back { hipEvent_t ev; int32_t a, b; };
+  std::mutex bmu;
+  std::condition_variable bcv;
   std::vector<Back> back;
-  size_t nback = 0; // back[0 .. nback) are in the caller's buffers
-  auto deliver = [&](const Back &k) {
-    std::memcpy(results + k.a, (const amod_result *)ctx->pin_res.p + k.a, sizeof(amod_result) * (size_t)(k.b - k.a));
-    std::memcpy(payload + (int64_t)k.a * payload_stride, (const uint8_t *)ctx->pin_payload.p + (int64_t)k.a * payload_stride,
-                (size_t)payload_stride * (size_t)(k.b - k.a));
-    if (progress) progress(user, k.b);
-  };
-  auto drain = [&](bool wait) -> hipError_t {
-    for (; nback < back.size(); ++nback) {
-      if (wait) {
-        const hipError_t e = hipEventSynchronize(back[nback].ev);
-        if (e != hipSuccess) return e;
-      } else {
-        const hipError_t e = hipEventQuery(back[nback].ev);
-        if (e == hipErrorNotReady) return hipSuccess;
-        if (e != hipSuccess) return e;
+  bool bclosed = false;
+  hipError_t berr = hipSuccess;
+  std::thread deliverer([&] {
+    (void)hipSetDevice(ctx->device);
+    for (size_t i = 0;; ++i) {
+      Back k;
+      {
+        std::unique_lock<std::mutex> lk(bmu);
+        bcv.wait(lk, [&] { return bclosed || i < back.size(); });
+        if (i >= back.size()) return;
+        k = back[i];
       }
-      deliver(back[nback]);
+      const hipError_t e = hipEventSynchronize(k.ev);
+      if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(bmu);
+        berr = e;
+        return;
+      }
+      std::memcpy(results + k.a, (const amod_result *)ctx->pin_res.p + k.a, sizeof(amod_result) * (size_t)(k.b - k.a));
+      std::memcpy(payload + (int64_t)k.a * payload_stride,
+                  (const uint8_t *)ctx->pin_payload.p + (int64_t)k.a * payload_stride,
+                  (size_t)payload_stride * (size_t)(k.b - k.a));
+      if (progress) progress(user, k.b);
     }
-    return hipSuccess;
+  });
+  auto finish = [&](bool drain) -> hipError_t { // stop the helper (after the queued pieces when drain)
+    if (!deliverer.joinable()) return berr;
+    {
+      std::lock_guard<std::mutex> lk(bmu);
+      if (!drain) back.resize(0);
+      bclosed = true;
+    }
+    bcv.notify_one();
+    deliverer.join();
+    return berr;
   };
+  struct Joiner { // every early return (HIP_TRY) stops the helper first
+    std::function<void()> f;
+    ~Joiner() { f(); }
+  } joiner{[&] { (void)finish(false); }};
   int32_t a = 0; // the first frame not yet enqueued
   for (int64_t p = 0; p <= npiece; ++p) {
     int64_t covered = nsamples;
@@ -1179,28 +1205,42 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
                                (const int32_t *)ctx->h_len.p + a, b - a, (amod_result *)ctx->h_res.p + a,
                                (uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride, payload_stride, options, s,
                                nullptr, call_max);
-    if (rc) {
+    hipError_t e = rc ? hipSuccess : hipErrorUnknown;
+    if (!rc) {
+      const size_t nb = back.size(); // (only this thread appends)
+      if (nb == ctx->dn_ev.size()) {
+        hipEvent_t ev;
+        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) ctx->dn_ev.push_back(ev);
+      } else {
+        e = hipSuccess;
+      }
+      if (e == hipSuccess)
+        e = hipMemcpyAsync((amod_result *)ctx->pin_res.p + a, (const amod_result *)ctx->h_res.p + a,
+                           sizeof(amod_result) * (size_t)(b - a), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync((uint8_t *)ctx->pin_payload.p + (int64_t)a * payload_stride,
+                           (const uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride,
+                           (size_t)payload_stride * (size_t)(b - a), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipEventRecord(ctx->dn_ev[nb], s);
+      if (e == hipSuccess) {
+        {
+          std::lock_guard<std::mutex> lk(bmu);
+          back.push_back(Back{ctx->dn_ev[nb], a, b});
+        }
+        bcv.notify_one();
+      }
+    }
+    if (rc || e != hipSuccess) {
+      (void)finish(false);
       (void)hipStreamSynchronize(ctx->up);
       (void)hipStreamSynchronize(s);
-      return rc;
+      if (rc) return rc;
+      HIP_TRY(e);
     }
-    if (back.size() == ctx->dn_ev.size()) {
-      hipEvent_t e;
-      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ctx->dn_ev.push_back(e);
-    }
-    const Back k{ctx->dn_ev[back.size()], a, b};
-    HIP_TRY(hipMemcpyAsync((amod_result *)ctx->pin_res.p + a, (const amod_result *)ctx->h_res.p + a,
-                           sizeof(amod_result) * (size_t)(b - a), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync((uint8_t *)ctx->pin_payload.p + (int64_t)a * payload_stride,
-                           (const uint8_t *)ctx->h_payload.p + (int64_t)a * payload_stride,
-                           (size_t)payload_stride * (size_t)(b - a), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(k.ev, s));
-    back.push_back(k);
-    HIP_TRY(drain(false));
     a = b;
   }
-  HIP_TRY(drain(true));
+  HIP_TRY(finish(true));
   return AMOD_SUCCESS;
 }
 } // namespace

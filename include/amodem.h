@@ -173,10 +173,11 @@ int amod_decode_host(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
                      int64_t nsamples, const int64_t *offsets, const int32_t *lengths, int32_t nframes,
                      amod_result *results, uint8_t *payload, int64_t payload_stride, uint32_t options);
 /* amod_decode_host with progress reports (additive; the Node binding formats decodeBatch's
- * result objects while later frames decode): progress(user, done) runs on the calling
- * thread, with done increasing, whenever records and payload slots [0, done) are in the
- * caller's buffers; its last call has done = nframes, before the call returns (no call for
- * an empty batch). A frame's
+ * result objects while later frames decode): progress(user, done) runs on a helper thread
+ * of the call (one at a time, done increasing) whenever records and payload slots
+ * [0, done) are in the caller's buffers; its last call has done = nframes, and every call
+ * has returned before amod_decode_host_progress does (no call for an empty batch). The
+ * calling thread meanwhile keeps uploading the next pieces. A frame's
  * outputs reach the caller as soon as its uploaded piece (64 MB of samples) is decoded. */
 typedef void (*amod_progress_fn)(void *user, int32_t frames_done);
 int amod_decode_host_progress(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const float *samples,
