@@ -530,14 +530,17 @@ __device__ __forceinline__ int64_t rl_l(int64_t v, int j) {
   return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), j) << 32) |
                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j));
 }
-constexpr int kGapG = 2;  // gaps per wave (measured: 8 -> 0.59 ms, 2 -> 0.40, 1 -> 0.57 on the C4-shaped stream)
-constexpr int kGapS = 65; // LDS row stride (doubles): lanes g of phase B on distinct banks
+#ifndef AMOD_GAPG
+#define AMOD_GAPG 2
+#endif
+constexpr int kGapG = AMOD_GAPG; // gaps per wave (round 4, before the chain lanes: 8 -> 0.59 ms, 2 -> 0.40, 1 -> 0.57 on the 2000-gap stream)
+constexpr int kGapS = 66; // LDS row stride (doubles): 16-byte aligned rows, the chain lanes of phase B on distinct banks
 __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, int64_t n, int64_t lo,
                                                  const int64_t *__restrict__ first, const double2 *__restrict__ barg,
                                                  int nbx, int nranges, int64_t F, int64_t cap, int64_t nblocks,
                                                  int max_blocks, GapScan *__restrict__ out) {
-  __shared__ double inc[3][kGapG][kGapS]; // phase A -> B: increments of each gap's tile positions
-  __shared__ double stt[3][kGapG][kGapS]; // phase B -> C: sums at each tile position, then the tile's end
+  __shared__ __attribute__((aligned(16))) double inc[3][kGapG][kGapS]; // phase A -> B: increments of each gap's tile positions
+  __shared__ __attribute__((aligned(16))) double stt[3][kGapG][kGapS]; // phase B -> C: sums at each tile position, then the tile's end
   constexpr int64_t kBlk = 4096, half = 256;
   const double min_e = 0.001;
   const int lane = threadIdx.x;
@@ -576,9 +579,20 @@ __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, in
       act = false;
     }
   }
-  // ---- the window sums at the start, in order (products on the lanes, sums per gap)
+  // The three running sums of gap g (p, ra, rb) are advanced by three chain lanes, lane
+  // q = c kGapG + g for sum c: each reads its own LDS row (inc[c][g]) and writes its own
+  // (stt[c][g]), so a position costs one read and one write for every gap of the wave (it
+  // was three of each with the gap's lane advancing all three sums: k_gap_scan waited on
+  // LDS issue for 58 % of its wave cycles). Gap lane g reads the sums back at the tile end.
+  const int cg = lane % kGapG;                            // chain lane: its gap
+  const bool chain_lane = lane < 3 * kGapG;
+  double *const irow = &inc[0][0][0] + lane * kGapS;     // (chain lanes) row c kGapG + g
+  double *const srow = &stt[0][0][0] + lane * kGapS;
+  double acc = 0.0;                                       // (chain lanes) the sum
+  // ---- the window sums at the start, in order (products on the lanes, sums per chain)
   {
     const unsigned long long am = __ballot(act);
+    const bool live_chain = chain_lane && ((am >> cg) & 1);
     for (int c = 0; c < (int)half; c += 64) {
       for (int gi = 0; gi < kGapG; ++gi) {
         if (!((am >> gi) & 1)) continue;
@@ -588,8 +602,8 @@ __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, in
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      if (act)
-        for (int m = 0; m < 64; ++m) { p += inc[0][lane][m]; ra += inc[1][lane][m]; rb += inc[2][lane][m]; }
+      if (live_chain)
+        for (int m = 0; m < 64; m += 2) { const double2 v = *reinterpret_cast<const double2 *>(irow + m); acc += v.x; acc += v.y; }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
@@ -623,28 +637,40 @@ __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, in
     load_tile(am, pos + T); // the next tile's samples, in flight under this one
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // (B) lane g: gap g's sums through its tile, in order
-    if (act) {
-      const int tu = (int)min<int64_t>(T, scan_end - pos); // positions with an update (all but scan_end)
-      int t = 0;
-      for (; t + 8 <= tu; t += 8) { // eight increments read ahead of the dependent sums
-        double i0[8], i1[8], i2[8];
+    // (B) chain lane q: its sum through gap g's tile, in order (the value before each
+    // position's update is the sum at that position; T: the sum after the tile)
+    {
+      const int tu_g = act ? (int)min<int64_t>(T, scan_end - pos) : 0; // (lane g) positions with an update
+      int Tq = 0, tq = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { i0[u] = inc[0][lane][t + u]; i1[u] = inc[1][lane][t + u]; i2[u] = inc[2][lane][t + u]; }
+      for (int gi = 0; gi < kGapG; ++gi) {
+        const int Tg = __builtin_amdgcn_readlane(T, gi), ug = __builtin_amdgcn_readlane(tu_g, gi);
+        if (cg == gi) { Tq = Tg; tq = ug; }
+      }
+      if (chain_lane && ((am >> cg) & 1)) {
+        int t = 0;
+        for (; t + 8 <= tq; t += 8) { // eight increments read ahead of the dependent sum, two per read
+          double2 i2[4], s2[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          stt[0][lane][t + u] = p; stt[1][lane][t + u] = ra; stt[2][lane][t + u] = rb;
-          p += i0[u]; ra += i1[u]; rb += i2[u];
+          for (int u = 0; u < 4; ++u) i2[u] = *reinterpret_cast<const double2 *>(irow + t + 2 * u);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            s2[u].x = acc; acc += i2[u].x;
+            s2[u].y = acc; acc += i2[u].y;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) *reinterpret_cast<double2 *>(srow + t + 2 * u) = s2[u];
         }
+        for (; t < Tq; ++t) {
+          srow[t] = acc;
+          if (t < tq) acc += irow[t];
+        }
+        srow[Tq] = acc;
       }
-      for (; t < T; ++t) {
-        stt[0][lane][t] = p; stt[1][lane][t] = ra; stt[2][lane][t] = rb;
-        if (t < tu) { p += inc[0][lane][t]; ra += inc[1][lane][t]; rb += inc[2][lane][t]; }
-      }
-      stt[0][lane][T] = p; stt[1][lane][T] = ra; stt[2][lane][T] = rb;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (act) { p = stt[0][lane][T]; ra = stt[1][lane][T]; rb = stt[2][lane][T]; } // (lane g) the sums after the tile
     // (C) lane t: position t of each live gap
     bool det_here = false; // lane g: gap g detected in this tile
     for (int gi = 0; gi < kGapG; ++gi) {
