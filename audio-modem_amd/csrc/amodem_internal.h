@@ -28,6 +28,7 @@ constexpr int kCrcLanes = 256; // CRC chunks per frame pass (16 bytes each)
 constexpr int kCrcChunk = 16;
 constexpr int kCrcBlock = kCrcLanes * kCrcChunk; // 4096 bytes per pass
 constexpr int kCrcMats = 512; // GF(2) shift matrices: up to 512 16-byte chunks (8 KB) in one wave pass
+constexpr int kFinePositions = 512; // k_fine: fine-sum positions per workgroup (per k_gap_scan argmax record)
 constexpr int kTlHead = 4;    // DevWork::tl: marks before the per-wave k_demod end stamps
 
 // Device-resident tables, built once per configuration by the runtime.

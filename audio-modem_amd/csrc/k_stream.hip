@@ -448,50 +448,75 @@ __global__ __launch_bounds__(256) void k_range_write(const uint8_t *__restrict__
 }
 
 // fine sums for positions first[r] .. first[r] + count[r] - 1 of range r; out index
-// base[r] + j; one lane per position
+// base[r] + j. A thread takes kFineP consecutive positions and slides a register window
+// over the staged samples: every tap's 16-byte LDS read feeds its positions' 2 kFineP
+// fp64 FMAs (one position per lane read a float per FMA pair: 2.7 ms on the 32k-chunk
+// stream, LDS-issue bound). Each position's sums are still the reference's, in its order.
 constexpr int kFineMaxSym = 1024; // symbol_len bound of k_fine's LDS window (presets: 576 .. 768)
+constexpr int kFineT = 128;       // threads per workgroup
+constexpr int kFineP = 4;         // consecutive positions per thread
+static_assert(kFineT * kFineP == kFinePositions, "k_fine's workgroup span (amodem_internal.h)");
 // barg (optional): per workgroup, the first maximum of its positions' metrics (NaN
 // skipped, as the refinement's `metric > best`) as (metric, j), at [r * gridDim.x + bx]
-__global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64_t n, const double *__restrict__ pre1,
-                                              int sym, double pre1_energy, const int64_t *__restrict__ first,
-                                              const int64_t *__restrict__ base, const int64_t *__restrict__ count,
-                                              int nranges, double *__restrict__ out, double *__restrict__ out_dev,
-                                              double2 *__restrict__ barg) {
-  __shared__ double2 red[4];
-  __shared__ float win[256 + kFineMaxSym]; // the workgroup's samples [d0, d0 + 256 + sym)
+__global__ __launch_bounds__(kFineT) void k_fine(const float *__restrict__ y, int64_t n, const double *__restrict__ pre1,
+                                                 int sym, double pre1_energy, const int64_t *__restrict__ first,
+                                                 const int64_t *__restrict__ base, const int64_t *__restrict__ count,
+                                                 int nranges, double *__restrict__ out, double *__restrict__ out_dev,
+                                                 double2 *__restrict__ barg) {
+  __shared__ double2 red[kFineT / 64];
+  // the workgroup's samples [d0, d0 + kFinePositions + sym), plus the register window's
+  // read-ahead (sym is a multiple of 4: amod_config_valid)
+  __shared__ __attribute__((aligned(16))) float win[kFinePositions + kFineMaxSym + 8];
   const int r = blockIdx.y;
   if (r >= nranges) return;
-  const int64_t j0 = (int64_t)blockIdx.x * 256, j = j0 + threadIdx.x;
-  if (j0 >= count[r]) { // (whole workgroup) no position: an empty record
+  const int64_t j0 = (int64_t)blockIdx.x * kFinePositions, cnt = count[r];
+  if (j0 >= cnt) { // (whole workgroup) no position: an empty record
     if (barg && threadIdx.x == 0) barg[(int64_t)r * gridDim.x + blockIdx.x] = make_double2(-__builtin_inf(), (double)j0);
     return;
   }
   {
     const int64_t d0 = first[r] + j0;
-    for (int i = threadIdx.x; i < 256 + sym; i += 256) win[i] = sample_at(y, n, d0 + i);
+    for (int i = threadIdx.x; i < kFinePositions + sym + 8; i += kFineT) win[i] = sample_at(y, n, d0 + i);
     __syncthreads();
   }
-  double m = -__builtin_inf();
-  if (j < count[r]) {
-    double corr = 0.0, se = 0.0;
-    const float *const w = win + threadIdx.x;
+  const int p0 = kFineP * (int)threadIdx.x;
+  const int64_t jt = j0 + p0; // this thread's first position
+  double m = -__builtin_inf(), bj = (double)jt;
+  if (jt < cnt) {
+    double corr[kFineP], se[kFineP];
+#pragma unroll
+    for (int k = 0; k < kFineP; ++k) corr[k] = se[k] = 0.0;
+    const float *const w = win + p0;
+    float4 cur = *reinterpret_cast<const float4 *>(w);
     // f32 x f32 products are exact in double, so fma(s, q, corr) is the reference's
     // corr + s * q with its one rounding: half the fp64 operations of mul + add
-#pragma unroll 8
-    for (int i = 0; i < sym; ++i) {
-      const double s = w[i];
-      corr = __builtin_fma(s, pre1[i], corr);
-      se = __builtin_fma(s, s, se);
+    for (int i = 0; i < sym; i += 4) {
+      const float4 nxt = *reinterpret_cast<const float4 *>(w + i + 4);
+      const double sv[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double q = pre1[i + u];
+#pragma unroll
+        for (int k = 0; k < kFineP; ++k) {
+          corr[k] = __builtin_fma(sv[u + k], q, corr[k]);
+          se[k] = __builtin_fma(sv[u + k], sv[u + k], se[k]);
+        }
+      }
+      cur = nxt;
     }
-    // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
-    const double denom = sqrt(se * pre1_energy);
-    const double v = denom > 0.001 ? corr / denom : __builtin_nan("");
-    if (out) out[base[r] + j] = v;         // (mapped host memory: the host's lookups)
-    if (out_dev) out_dev[base[r] + j] = v; // (the device copy k_gap_refine reads)
-    if (v == v) m = v;
+#pragma unroll
+    for (int k = 0; k < kFineP; ++k) {
+      const int64_t j = jt + k;
+      if (j >= cnt) break;
+      // the metric the refinement compares (app.js:872-875); NaN: the position is skipped
+      const double denom = sqrt(se[k] * pre1_energy);
+      const double v = denom > 0.001 ? corr[k] / denom : __builtin_nan("");
+      if (out) out[base[r] + j] = v;         // (mapped host memory: the host's lookups)
+      if (out_dev) out_dev[base[r] + j] = v; // (the device copy k_gap_refine reads)
+      if (v == v && v > m) { m = v; bj = (double)j; } // (in order: the first maximum)
+    }
   }
   if (!barg) return;
-  double bj = (double)j;
   for (int o = 32; o > 0; o >>= 1) {
     const double om = __shfl_xor(m, o, 64), oj = __shfl_xor(bj, o, 64);
     if (om > m || (om == m && oj < bj)) { m = om; bj = oj; }
@@ -500,7 +525,7 @@ __global__ __launch_bounds__(256) void k_fine(const float *__restrict__ y, int64
   __syncthreads();
   if (threadIdx.x == 0) {
     double2 b = red[0];
-    for (int k = 1; k < 4; ++k)
+    for (int k = 1; k < kFineT / 64; ++k)
       if (red[k].x > b.x || (red[k].x == b.x && red[k].y < b.y)) b = red[k];
     barg[(int64_t)r * gridDim.x + blockIdx.x] = b;
   }
@@ -531,9 +556,12 @@ __device__ __forceinline__ int64_t rl_l(int64_t v, int j) {
                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j));
 }
 #ifndef AMOD_GAPG
-#define AMOD_GAPG 2
+#define AMOD_GAPG 4
 #endif
-constexpr int kGapG = AMOD_GAPG; // gaps per wave (round 4, before the chain lanes: 8 -> 0.59 ms, 2 -> 0.40, 1 -> 0.57 on the 2000-gap stream)
+// gaps per wave. With the chain lanes (round 5), on the 32k-gap stream: 1 -> 1.80 ms, 2 ->
+// 1.06, 4 -> 0.77, 8 -> 0.98 (the 2000-gap stream: 0.24 / 0.25 / 0.32 / 0.46). Round 4,
+// one lane per gap's three sums, 2000 gaps: 8 -> 0.59 ms, 2 -> 0.40, 1 -> 0.57
+constexpr int kGapG = AMOD_GAPG;
 constexpr int kGapS = 66; // LDS row stride (doubles): 16-byte aligned rows, the chain lanes of phase B on distinct banks
 __global__ __launch_bounds__(64) void k_gap_scan(const float *__restrict__ y, int64_t n, int64_t lo,
                                                  const int64_t *__restrict__ first, const double2 *__restrict__ barg,
@@ -955,7 +983,8 @@ hipError_t amod_launch_fine(const float *y, int64_t n, const double *pre1, int s
                             int64_t maxcount, double *out, double *out_dev, double2 *barg, hipStream_t s) {
   if (nranges <= 0 || maxcount <= 0) return hipSuccess;
   if (sym <= 0 || sym > amod::kFineMaxSym) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + 255) / 256), nranges), dim3(256), 0, s, y, n, pre1, sym,
+  hipLaunchKernelGGL(amod::k_fine, dim3((unsigned)((maxcount + amod::kFinePositions - 1) / amod::kFinePositions), nranges),
+                     dim3(amod::kFineT), 0, s, y, n, pre1, sym,
                      pre1_energy, first, base, count, nranges, out, out_dev, barg);
   return hipGetLastError();
 }

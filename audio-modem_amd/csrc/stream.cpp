@@ -1148,7 +1148,7 @@ struct Prepass {
       S_TRY(hipMemcpyAsync(c->d_pre1.p, p1d.data(), sizeof(double) * p1d.size(), hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
-      nbx = (int)((maxc + 255) / 256);
+      nbx = (int)((maxc + amod::kFinePositions - 1) / amod::kFinePositions);
       nfr = nr;
       S_TRY(c->d_barg.alloc(sizeof(double2) * (size_t)nr * nbx));
       for (int r0 = 0; r0 < nr; r0 += 65535) {
