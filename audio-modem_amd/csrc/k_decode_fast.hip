@@ -1819,7 +1819,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
                  __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 256 * m, 4 * p2, 0))};
   };
 
-  float2 gl[4];               // G = 1/H of the lane's band subcarriers (job 0)
+  f2v gl[4];                  // G = 1/H of the lane's band subcarriers (job 0)
   f2v gp = {0.f, 0.f};        // G = 1/H at the lane's pilot (job 0)
   float wl[4] = {0.f, 0.f, 0.f, 0.f}; // SOFT: the soft weights |H|^2 of the lane's band subcarriers (job 0)
   float wmax = 0.f, dW = 0.f;  // SOFT: the frame's largest weight, and the error bound of every weight
@@ -1994,7 +1994,14 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
           const float m2 = const1 ? 0.f : h.x * h.x + h.y * h.y;
           // |H|^2 close to 1e-10 (or tiny but non-zero) decides passthrough differently
           ch |= b < nband && !const1 && m2 < 4.f * 1e-6f;
-          gl[rr] = g;
+          // a slot without a data subcarrier (pilot or none) gets G = NaN, so its eq and
+          // margins are NaN: v_min / v_max pass NaN over, so the QPSK margin needs no
+          // per-slot select and em no mask (the pilots' |eq| enter em from the pilot lanes
+          // below). gm above takes the real G. (parity-debug launches keep the real G:
+          // they report every band slot's eq)
+          const float gx = !DBG && ((kn_neg >> (4 + rr)) & 1) ? __builtin_nanf("") : g.x;
+          const float gy = !DBG && ((kn_neg >> (4 + rr)) & 1) ? __builtin_nanf("") : g.y;
+          gl[rr] = f2v{gx, gy};
           if (SOFT) wl[rr] = b < nband ? 0.25f * m2 : 0.f; // |H|^2 = |h|^2 / 4
           if (b < nband) gm = fmaxf(gm, fabsf(g.x) + fabsf(g.y));
           if (DBG && b < nband) { const float kn = (kn_neg >> rr) & 1 ? -1.f : 1.f;
@@ -2017,7 +2024,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       float em = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const f2v g = f2v{gl[rr].x, gl[rr].y};
+        const f2v g = gl[rr];
         e1[rr] = pk_cmul(x1[rr], g);
         e2[rr] = pk_cmul(x2[rr], g);
         em = max3_raw(em, fabsf(e1[rr].x) + fabsf(e1[rr].y), fabsf(e2[rr].x) + fabsf(e2[rr].y));
@@ -2031,6 +2038,11 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         }
       }
       DSTAMP(18, jcur == 1);
+      // the pilots' eq (pilot lanes; a lane without one has its sub_start bin's, a data
+      // subcarrier's: harmless in the max). Their |eq| joins em: the band slots that hold
+      // pilots pass NaN over (above)
+      const f2v q1e = pk_cmul(x1p, gp), q2e = pk_cmul(x2p, gp);
+      if (!DBG) em = max3_raw(em, fabsf(q1e.x) + fabsf(q1e.y), fabsf(q2e.x) + fabsf(q2e.y));
       // error bound of eq for both symbols (fp32 FFT + channel estimate), DESIGN.md "guards"
       // (gmax is half of max |G|, hence 4e-6)
       float d = 4e-6f * guard * gmax * (zm + em * zce);
@@ -2042,7 +2054,6 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       int pc1, pc2;
       bool ph_unc1, ph_unc2;
       {
-        const f2v q1e = pk_cmul(x1p, gp), q2e = pk_cmul(x2p, gp);
         const bool pil = (kn_neg >> 8) & 1;
         const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
         const bool w1 = pil && a1 > 1e-6f, w2 = pil && a2 > 1e-6f;
@@ -2117,6 +2128,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         const f2v c = pk_derot(which == 0 ? e1[rr] : e2[rr], which == 0 ? phv1 : phv2);
         uint32_t db;
         float margin;
+        float &mm = which == 0 ? mm1 : mm2;
         if (MOD == AMOD_QPSK) {
           // the sign-bit decision with the symbol's liveness folded into its two masks:
           // QPSK's origin decision is index 0 (four equidistant points, the first kept:
@@ -2124,18 +2136,26 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
           // per-slot select is needed
           const uint32_t a = __float_as_uint(c.x), b = __float_as_uint(c.y);
           db = (b & (which == 0 ? lm31a : lm31b)) | (((a ^ b) >> 1) & (which == 0 ? lm30a : lm30b));
-          // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
-          // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
-          asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(margin) : "v"(c.x), "v"(c.y));
+          if (!DBG) {
+            // the symbol's smallest margin min(|re|, |im|) in one v_min3_f32 with |.| source
+            // modifiers; a slot without a data subcarrier has NaN components (G = NaN at the
+            // CE), which v_min passes over
+            asm("v_min3_f32 %0, %0, |%1|, |%2|" : "+v"(mm) : "v"(c.x), "v"(c.y));
+          } else {
+            // min(|re|, |im|) as one v_min_f32 with |.| source modifiers (fminf, and
+            // fmed3 folded into it, canonicalised both inputs first: two more VALU per slot)
+            asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(margin) : "v"(c.x), "v"(c.y));
+            margin = nd ? __builtin_inff() : margin;
+            asm("v_min_f32 %0, %1, %2" : "=v"(mm) : "v"(mm), "v"(margin));
+          }
         } else {
           db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
           db = (which == 0 ? live1 : live2) ? db : org_bits;
+          margin = nd ? __builtin_inff() : margin;
+          // (v_min_f32 without fminf's canonicalisation: a NaN margin is passed over, as the
+          // comparison of the per-slot form was false for it)
+          asm("v_min_f32 %0, %1, %2" : "=v"(mm) : "v"(mm), "v"(margin));
         }
-        margin = nd ? __builtin_inff() : margin;
-        // (v_min_f32 without fminf's canonicalisation: a NaN margin is passed over, as the
-        // comparison of the per-slot form was false for it)
-        float &mm = which == 0 ? mm1 : mm2;
-        asm("v_min_f32 %0, %1, %2" : "=v"(mm) : "v"(mm), "v"(margin));
         // dword pos / BPS - g0 of the buffer (a lane without a data subcarrier in this slot
         // stores into its junk dword: no exec-mask block per store); pos is a multiple of
         // BPS, so the byte offset is pos * (4 / BPS): one shift-add from the job's base
