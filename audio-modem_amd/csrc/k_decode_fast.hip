@@ -2117,7 +2117,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       // the guard: each symbol's smallest decision margin over the lane's data slots (a slot
       // without a data subcarrier counts as +inf), compared once with the symbol's band
       const f2v phv1 = f2v{ph1, ph1}, phv2 = f2v{ph2, ph2};
-      const uint32_t lm31a = live1 ? 0x80000000u : 0u, lm30a = live1 ? 0x40000000u : 0u; // (QPSK)
+      const uint32_t lm31a = live1 ? 0x80000000u : 0u, lm30a = live1 ? 0x40000000u : 0u; // (QPSK, BPSK)
       const uint32_t lm31b = live2 ? 0x80000000u : 0u, lm30b = live2 ? 0x40000000u : 0u;
       const int sbase1 = s1 * per_sym, sbase2 = s2 * per_sym;
       float mm1 = __builtin_inff(), mm2 = __builtin_inff();
@@ -2148,6 +2148,13 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
             margin = nd ? __builtin_inff() : margin;
             asm("v_min_f32 %0, %1, %2" : "=v"(mm) : "v"(mm), "v"(margin));
           }
+        } else if (MOD == AMOD_BPSK && !DBG) {
+          // BPSK: index 1 iff re < 0, the origin decision is index 0: the sign bit under the
+          // liveness mask (re = -0 decides 1 here but has margin 0, inside every band: the
+          // frame goes to the exact kernel); the margin |re| straight into the symbol's
+          // minimum (NaN for a slot without a data subcarrier: passed over)
+          db = __float_as_uint(c.x) & (which == 0 ? lm31a : lm31b);
+          asm("v_min_f32_e64 %0, %0, |%1|" : "+v"(mm) : "v"(c.x));
         } else {
           db = (uint32_t)decide(MOD, c.x, c.y, margin) << (32 - BPS);
           db = (which == 0 ? live1 : live2) ? db : org_bits;
