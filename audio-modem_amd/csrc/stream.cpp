@@ -1206,6 +1206,7 @@ struct WindowDecoder {
   std::vector<uint8_t> zero_row;
   int64_t stride = 16;
   double t_ms = 0, t_launch = 0; // host time in launch + collect (t_launch: launch alone)
+  double t_sub[4] = {}; // (diagnostics) launch: buffers + input copies, k_window, reserve, decode
   // a batch in flight in buffer set k
   struct Flight {
     std::vector<int64_t> pos, woff; // (host arrays kept until the batch is collected)
@@ -1257,13 +1258,22 @@ struct WindowDecoder {
       S_TRY(hipMemcpyAsync(d_len.p, f.len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_woff.p, f.woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)f.stride * nw, s));
+      auto lap = [t = std::chrono::steady_clock::now()](double &acc) mutable {
+        const auto now = std::chrono::steady_clock::now();
+        acc += std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+      };
+      lap(t_sub[0]);
       S_TRY(amod_launch_window(pp.y(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
                                d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
+      lap(t_sub[1]);
       int rc = amod_reserve(ctx, cfg, nw, maxlen);
       if (rc) return rc;
+      lap(t_sub[2]);
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
                               nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), f.stride, 0, s);
       if (rc) return rc;
+      lap(t_sub[3]);
       // the rows go to the host on s3, so the next batch's kernels on s do not queue behind
       // them (a batch's 9 MB of rows took as long as its kernels)
       S_TRY(hipEventRecord(c.w_kern[k], s));
@@ -1546,6 +1556,9 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
               "per-frame loop %.3f ms, chunk copies %.3f ms so far)\n", tr.frames.size(),
               std::chrono::duration<double, std::milli>(clk::now() - t_dd).count(),
               std::chrono::duration<double, std::milli>(t_dd - t_gpu_pre).count(), wd.t_ms, wd.t_launch, t_loop, t_copy);
+    if (kn.stream_diag)
+      fprintf(stderr, "[stream]   launches: buffers + copies %.3f ms, k_window %.3f, reserve %.3f, decode %.3f\n", wd.t_sub[0],
+              wd.t_sub[1], wd.t_sub[2], wd.t_sub[3]);
     if (chg >= 0) {
       // keep what happened up to that frame; re-run the rest with the new window length
       const RxState after = tr.frames[chg].after;
