@@ -1206,7 +1206,7 @@ struct WindowDecoder {
   std::vector<uint8_t> zero_row;
   int64_t stride = 16;
   double t_ms = 0, t_launch = 0; // host time in launch + collect (t_launch: launch alone)
-  double t_sub[4] = {}; // (diagnostics) launch: buffers + input copies, k_window, reserve, decode
+  double t_sub[8] = {}; // (diagnostics) launch: host prep, device buffers + input copies, memset, k_window, reserve, decode, event + wait, D2H enqueue
   // a batch in flight in buffer set k
   struct Flight {
     std::vector<int64_t> pos, woff; // (host arrays kept until the batch is collected)
@@ -1247,6 +1247,12 @@ struct WindowDecoder {
     if (!c.w_done[k]) S_TRY(hipEventCreateWithFlags(&c.w_done[k], hipEventDisableTiming));
     if (!c.w_kern[k]) S_TRY(hipEventCreateWithFlags(&c.w_kern[k], hipEventDisableTiming));
     if (!c.s3) S_TRY(hipStreamCreateWithFlags(&c.s3, hipStreamNonBlocking));
+    auto lap = [t = t0](double &acc) mutable {
+      const auto now = std::chrono::steady_clock::now();
+      acc += std::chrono::duration<double, std::milli>(now - t).count();
+      t = now;
+    };
+    lap(t_sub[0]);
     if (nw) {
       S_TRY(d_pos.alloc(sizeof(int64_t) * nw));
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
@@ -1257,30 +1263,28 @@ struct WindowDecoder {
       S_TRY(hipMemcpyAsync(d_pos.p, f.pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_len.p, f.len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_woff.p, f.woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
+      lap(t_sub[1]);
       S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)f.stride * nw, s));
-      auto lap = [t = std::chrono::steady_clock::now()](double &acc) mutable {
-        const auto now = std::chrono::steady_clock::now();
-        acc += std::chrono::duration<double, std::milli>(now - t).count();
-        t = now;
-      };
-      lap(t_sub[0]);
+      lap(t_sub[2]);
       S_TRY(amod_launch_window(pp.y(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
                                d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
-      lap(t_sub[1]);
+      lap(t_sub[3]);
       int rc = amod_reserve(ctx, cfg, nw, maxlen);
       if (rc) return rc;
-      lap(t_sub[2]);
+      lap(t_sub[4]);
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
                               nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), f.stride, 0, s);
       if (rc) return rc;
-      lap(t_sub[3]);
+      lap(t_sub[5]);
       // the rows go to the host on s3, so the next batch's kernels on s do not queue behind
       // them (a batch's 9 MB of rows took as long as its kernels)
       S_TRY(hipEventRecord(c.w_kern[k], s));
       S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
+      lap(t_sub[6]);
       S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, c.s3));
       S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
       S_TRY(hipEventRecord(c.w_done[k], c.s3));
+      lap(t_sub[7]);
     } else {
       S_TRY(hipEventRecord(c.w_done[k], s));
     }
@@ -1557,8 +1561,9 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
               std::chrono::duration<double, std::milli>(clk::now() - t_dd).count(),
               std::chrono::duration<double, std::milli>(t_dd - t_gpu_pre).count(), wd.t_ms, wd.t_launch, t_loop, t_copy);
     if (kn.stream_diag)
-      fprintf(stderr, "[stream]   launches: buffers + copies %.3f ms, k_window %.3f, reserve %.3f, decode %.3f\n", wd.t_sub[0],
-              wd.t_sub[1], wd.t_sub[2], wd.t_sub[3]);
+      fprintf(stderr, "[stream]   launches: host prep %.3f ms, buffers + input copies %.3f, memset %.3f, k_window %.3f, "
+              "reserve %.3f, decode %.3f, event %.3f, D2H enqueue %.3f\n", wd.t_sub[0], wd.t_sub[1], wd.t_sub[2], wd.t_sub[3],
+              wd.t_sub[4], wd.t_sub[5], wd.t_sub[6], wd.t_sub[7]);
     if (chg >= 0) {
       // keep what happened up to that frame; re-run the rest with the new window length
       const RxState after = tr.frames[chg].after;
