@@ -2052,7 +2052,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       // the pilot lanes
       float ps1, pe1, ps2, pe2;
       int pc1, pc2;
-      bool ph_unc1, ph_unc2;
+      unsigned long long ph_b1, ph_b2; // pilot lanes whose |eqRe| lies within the band of 1e-6
       {
         const bool pil = (kn_neg >> 8) & 1;
         const float a1 = fabsf(q1e.x), a2 = fabsf(q2e.x);
@@ -2070,8 +2070,8 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
         pe1 = fabsf(q1) * fmaf(fabsf(q1e.y), fabsf(q1), 1.f);
         pe2 = fabsf(q2) * fmaf(fabsf(q2e.y), fabsf(q2), 1.f);
         // a pilot |eqRe| near 1e-6 makes that symbol's phase (and every decision) uncertain
-        ph_unc1 = __ballot(pil && live1 && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f) != 0;
-        ph_unc2 = __ballot(pil && live2 && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f) != 0;
+        ph_b1 = __ballot(pil && fabsf(a1 - 1e-6f) <= 2.f * d + 1e-7f);
+        ph_b2 = __ballot(pil && fabsf(a2 - 1e-6f) <= 2.f * d + 1e-7f);
       }
       if (KO(4)) { ps1 = rlane(ps1, 0); pe1 = rlane(pe1, 0); ps2 = rlane(ps2, 0); pe2 = rlane(pe2, 0); }
       else if (pil16) wsum16_4(ps1, pe1, ps2, pe2);
@@ -2267,8 +2267,10 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
           for (int rr = 0; rr < NS; ++rr) slot_dec(rr, W0{});
         }
       }
-      const bool d1u = live1 && !KO(0xFFFF) && __ballot(mm1 <= tau1) != 0;
-      const bool d2u = live2 && !KO(0xFFFF) && __ballot(mm2 <= tau2) != 0;
+      // the job's guard events as lane masks, tested once: any of them is rare, and only
+      // then are the symbols' flags worked out (one scalar test per job, not a chain of
+      // scalar selects per symbol and flag)
+      const unsigned long long dm_b1 = __ballot(mm1 <= tau1), dm_b2 = __ballot(mm2 <= tau2);
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       // (lane i reads its NQ 16-byte pieces starting at piece i / (16 / NQ) mod NQ: the 16
@@ -2291,13 +2293,18 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       }
       asm volatile("" ::: "memory"); // (the next FFT rewrites the buffer)
       {
-        if (s1 >= 0 && (d1u || ph_unc1)) {
-          flag_sym = min(flag_sym, s1);
-          sflags |= (d1u ? AMOD_FLAG_DEMAP : 0) | (ph_unc1 ? AMOD_FLAG_PHASE : 0);
-        }
-        if (s2 >= 0 && (d2u || ph_unc2)) {
-          flag_sym = min(flag_sym, s2);
-          sflags |= (d2u ? AMOD_FLAG_DEMAP : 0) | (ph_unc2 ? AMOD_FLAG_PHASE : 0);
+        // (live1 / live2 imply s1 / s2 >= 0)
+        if (!KO(0xFFFF) && ((live1 ? dm_b1 | ph_b1 : 0ull) | (live2 ? dm_b2 | ph_b2 : 0ull)) != 0) {
+          const bool d1u = live1 && dm_b1 != 0, d2u = live2 && dm_b2 != 0;
+          const bool p1u = live1 && ph_b1 != 0, p2u = live2 && ph_b2 != 0;
+          if (d1u || p1u) {
+            flag_sym = min(flag_sym, s1);
+            sflags |= (d1u ? AMOD_FLAG_DEMAP : 0) | (p1u ? AMOD_FLAG_PHASE : 0);
+          }
+          if (d2u || p2u) {
+            flag_sym = min(flag_sym, s2);
+            sflags |= (d2u ? AMOD_FLAG_DEMAP : 0) | (p2u ? AMOD_FLAG_PHASE : 0);
+          }
         }
       }
       DSTAMP(20, jcur == 1);
