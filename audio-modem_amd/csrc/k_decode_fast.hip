@@ -1805,11 +1805,12 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
   int lane4 = 4 * lane;
   asm volatile("" : "+v"(lane4));
   auto job_loads = [&](const FrameS &F, int j, f2v (&r)[8]) {
-    int s1, s2;
-    job_syms(F, j, s1, s2);
-    const int data0 = F.start + 3 * SYM;
-    const int p1 = (s1 == -2 ? F.start + 2 * SYM : data0 + s1 * SYM) + CP;
-    const int p2 = s2 >= 0 ? data0 + s2 * SYM + CP : p1;
+    // job j's first symbol window starts 2 (j + 1) symbols after the frame start (the CE
+    // symbol for j = 0, data symbol 2j - 1 after it), its second one symbol later when
+    // there is one (symbol 2j < T; job 0's data symbol 0 always): job_syms' windows, in
+    // three scalar operations
+    const int p1 = F.start + CP + 2 * SYM * (j + 1);
+    const int p2 = (j == 0 || 2 * j < F.T) ? p1 + SYM : p1;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)F.X, (short)0, 0x7FFFFFFF, 0x00020000);
     int vo = lane4;
     asm volatile("" : "+v"(vo)); // (one offset register: 256 m goes to the immediate, not 8 hoisted copies)
@@ -1880,7 +1881,7 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
     const int f = cur.f;
     amod_debug *const D = DBG ? w.dbg + f : nullptr;
     if (jcur == 0) { // a new frame: clear its bit stream (SOFT: its voted stream, built by ORs)
-      const int nwz = SOFT ? (cur.T * per_sym / rep + 31) / 32 + 3 : (cur.T * per_sym + 31) / 32 + 2;
+      const int nwz = SOFT ? (int)(((uint32_t)(cur.T * per_sym / rep) + 31) >> 5) + 3 : (int)(((uint32_t)(cur.T * per_sym) + 31) >> 5) + 2;
       uint32_t *const zs = SOFT ? voted : bits;
       for (int i = lane; i < nwz; i += 64) zs[i] = 0u;
       live_f = f; fnj = max(frame_jobs(cur), 1); fneed = -1; flag_sym = 0x7fffffff;
@@ -2100,7 +2101,9 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       constexpr int DPW = 32 / BPS; // decisions per stream word
       uint32_t *const dec = reinterpret_cast<uint32_t *>(X2);
       const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
-      const int wfirst = gs / DPW, g0 = wfirst * DPW, gend = (ge + DPW - 1) / DPW * DPW;
+      // (non-negative: unsigned shifts and masks, not the signed division's sign fix-ups)
+      const int wfirst = (int)((uint32_t)gs / DPW), g0 = wfirst * DPW;
+      const int gend = (int)(((uint32_t)ge + DPW - 1) & ~(uint32_t)(DPW - 1));
       asm volatile("" ::: "memory"); // (the band reads above are float2 accesses of the same LDS)
       // the first and last words' dwords outside [gs, ge) are zeroed (lanes < DPW); every
       // other lane stores into a junk dword past any decision or junk dword of the job, so
@@ -2278,8 +2281,8 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       // order, lanes i and i + 16 / NQ hit the same slot: 4-way for QPSK). A job's run is
       // at most 2 ndata / DPW + 2 words: one pass of the wave for BPSK and QPSK.
       constexpr int NQ = DPW / 4;
-      const int rot = (ln / (16 / NQ)) & (NQ - 1);
-      const int nwj = (KO(2) || SOFT) ? 0 : (gend - g0) / DPW;
+      const int rot = (int)(((uint32_t)ln / (16 / NQ)) & (NQ - 1));
+      const int nwj = (KO(2) || SOFT) ? 0 : (int)((uint32_t)(gend - g0) / DPW);
       for (int i = ln; i < nwj; i += 64) {
         const uint4 *const q = reinterpret_cast<const uint4 *>(dec + DPW * i);
         uint4 t[NQ]; // (every piece requested before the first is combined: one LDS wait)
