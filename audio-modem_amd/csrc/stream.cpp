@@ -705,6 +705,7 @@ struct StreamCache {
   Pinned gaps_h;
   PageBuf yh;
   Pinned yc, hot_h, metric_h;
+  Pinned gsrc_h; // the sparse gather's granule list (pinned: its upload does not block the host)
   Pinned w_res_h[kSets], w_pay_h[kSets];    // window decoder: results and payload rows (pinned D2H)
   // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
   std::vector<uint8_t> sp_need;
@@ -995,9 +996,14 @@ struct Prepass {
       if (!c->gathered) (void)hipEventCreateWithFlags(&c->gathered, hipEventDisableTiming);
       for (auto &e : c->cpiece)
         if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-      bool ok = hipMemcpyAsync(c->d_gsrc.p, src.data(), sizeof(int32_t) * src.size(), hipMemcpyHostToDevice, s_main) == hipSuccess &&
-                amod_launch_gather(c->d_y.as<float>(), c->d_gsrc.as<int32_t>(), (int)npacked, c->d_c.as<float>(), s_main) == hipSuccess &&
-                hipEventRecord(c->gathered, s_main) == hipSuccess && hipStreamWaitEvent(c->s2, c->gathered, 0) == hipSuccess;
+      // the granule list goes up from pinned memory and the gather runs on s2 (which waited
+      // for the EMA): a pageable copy on the launch stream held the host until the gap scans
+      // queued there had run, and the gap scans' wait then also waited for the gather
+      bool ok = c->gsrc_h.alloc(sizeof(int32_t) * src.size()) == hipSuccess;
+      if (ok) std::memcpy(c->gsrc_h.p, src.data(), sizeof(int32_t) * src.size());
+      ok = ok && hipMemcpyAsync(c->d_gsrc.p, c->gsrc_h.p, sizeof(int32_t) * src.size(), hipMemcpyHostToDevice, c->s2) == hipSuccess &&
+           amod_launch_gather(c->d_y.as<float>(), c->d_gsrc.as<int32_t>(), (int)npacked, c->d_c.as<float>(), c->s2) == hipSuccess &&
+           hipEventRecord(c->gathered, c->s2) == hipSuccess;
       for (int q = 0; ok && q < StreamCache::kPieces; ++q) {
         const int64_t a = npacked * q / StreamCache::kPieces, b = npacked * (q + 1) / StreamCache::kPieces;
         if (b > a)
