@@ -1647,9 +1647,10 @@ __device__ __forceinline__ int parse_fast(const uint32_t *v, int nbytes, int mod
 constexpr int kHeaderMaxBytes = 1 + 255 + 4;
 
 struct FrameS {  // wave-uniform facts of one frame on the demodulation path (SGPRs: the
-                // frame-end-only fields are re-read from the detection record there)
+                // frame-end-only fields are re-read from the detection record there; the
+                // normalisation A, B with one scalar load per job: held here they were two of
+                // the SGPRs the full file spilled and read back every job)
   int f, T, M, start;
-  float A, B;
   const float *X;
 };
 __device__ __forceinline__ int frame_jobs(const FrameS &F) { return F.T > 0 ? 1 + F.T / 2 : 0; }
@@ -1786,7 +1787,6 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       const DetRec d = sload(w.det + f);
       if (d.route == (w.dm_list ? ROUTE_REPLAY : ROUTE_DEMOD)) { // (the list launch: replayed frames)
         F.f = f; F.T = d.T; F.M = d.M; F.start = d.start;
-        F.A = d.A; F.B = d.B;
         F.X = w.samples + sload(w.off + f);
         return k;
       }
@@ -1900,7 +1900,9 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       f2v v[8];
       // no second symbol: A = B = 0 zeroes the imaginary half (its samples are finite: the
       // last job re-reads the first symbol's, checked below in chunk mode)
-      const f2v Av = {cur.A, s2 >= 0 ? cur.A : 0.f}, Bv = {cur.B, s2 >= 0 ? cur.B : 0.f};
+      const f2v ab = sload(reinterpret_cast<const f2v *>(&w.det[__builtin_amdgcn_readfirstlane(f)].A)); // scalar: f is wave-uniform
+      const float cA = ab.x, cB = ab.y;
+      const f2v Av = {cA, s2 >= 0 ? cA : 0.f}, Bv = {cB, s2 >= 0 ? cB : 0.f};
 #pragma unroll
       for (int m = 0; m < 8; ++m) v[m] = __builtin_elementwise_fma(c[m], Av, Bv);
       // a window is constant iff every raw sample equals its first one (all-zero spectrum).
