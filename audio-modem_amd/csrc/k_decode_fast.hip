@@ -2102,7 +2102,8 @@ template <bool DBG, int MOD, int NS, bool SOFT = false> __device__ __forceinline
       // word's top bits belong to the previous job).
       constexpr int DPW = 32 / BPS; // decisions per stream word
       uint32_t *const dec = reinterpret_cast<uint32_t *>(X2);
-      const int gs = (ce ? 0 : s1) * ndata, ge = ((s2 >= 0 ? s2 : s1) + 1) * ndata;
+      const int nd = kargs().cfg.ndata; // (a fresh scalar load: ndata itself is spilled by here)
+      const int gs = (ce ? 0 : s1) * nd, ge = ((s2 >= 0 ? s2 : s1) + 1) * nd;
       // (non-negative: unsigned shifts and masks, not the signed division's sign fix-ups)
       const int wfirst = (int)((uint32_t)gs / DPW), g0 = wfirst * DPW;
       const int gend = (int)(((uint32_t)ge + DPW - 1) & ~(uint32_t)(DPW - 1));
