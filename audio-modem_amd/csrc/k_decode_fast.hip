@@ -449,12 +449,16 @@ __device__ __forceinline__ void wsum_b4(float &a, float &b, float &c, float &d) 
 // preset): the row reductions alone, then lane 0
 __device__ __forceinline__ void wsum16_4(float &a, float &b, float &c, float &d) {
   asm volatile("s_nop 1" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
-#define AMOD_W4(ctrl)                                                                   \
-  { const float ta = AMOD_DPP_F(a, ctrl), tb = AMOD_DPP_F(b, ctrl), tc = AMOD_DPP_F(c, ctrl), td = AMOD_DPP_F(d, ctrl); \
-    a += ta; b += tb; c += tc; d += td; }
-  AMOD_W4(0xB1) AMOD_W4(0x4E) AMOD_W4(0x141) AMOD_W4(0x140)
-#undef AMOD_W4
-  a = rlane(a, 0); b = rlane(b, 0); c = rlane(c, 0); d = rlane(d, 0);
+  // row 1 of a (b) takes row 0 of c (d) (v_permlane16_swap: odd rows of the first operand
+  // with even rows of the second), so one row-local butterfly sums a and c (b and d) at
+  // once: the same lanes in the same order as four separate sums over row 0
+  float ac = __uint_as_float(__builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(c), false, false)[0]);
+  float bd = __uint_as_float(__builtin_amdgcn_permlane16_swap(__float_as_uint(b), __float_as_uint(d), false, false)[0]);
+#define AMOD_W2(ctrl)                                                                   \
+  { const float t0 = AMOD_DPP_F(ac, ctrl), t1 = AMOD_DPP_F(bd, ctrl); ac += t0; bd += t1; }
+  AMOD_W2(0xB1) AMOD_W2(0x4E) AMOD_W2(0x141) AMOD_W2(0x140)
+#undef AMOD_W2
+  a = rlane(ac, 0); c = rlane(ac, 16); b = rlane(bd, 0); d = rlane(bd, 16);
 }
 __device__ __forceinline__ float wmax_b(float v) {
   v = fmaxf(v, AMOD_DPP_F(v, 0xB1)); v = fmaxf(v, AMOD_DPP_F(v, 0x4E));

@@ -711,6 +711,8 @@ struct StreamCache {
   std::vector<uint8_t> sp_need;
   std::vector<std::pair<int64_t, int64_t>> sp_reg; // (kept: its pages stay faulted in across calls)
   std::vector<int32_t> sp_cidx;
+  std::vector<amod::GapScan> gaps_keep; // the gap scans' records and refinements (kept: a fresh 3 MB
+  std::vector<GpuRefine> refs_keep;     // vector per call spent ~1 ms in first-touch faults)
   std::unique_ptr<std::atomic<const float *>[]> sp_gptr;
   size_t sp_gcap = 0;
   bool apow_ready = false;
@@ -890,6 +892,10 @@ struct Prepass {
   }
   int gap_scan_finish() {
     if (!gap_launched) return AMOD_SUCCESS;
+    if (gaps.capacity() < c->gaps_keep.capacity()) { gaps.swap(c->gaps_keep); gaps.clear(); }
+    if (refs.capacity() < c->refs_keep.capacity()) { refs.swap(c->refs_keep); refs.clear(); }
+    gaps.reserve((size_t)nfr);
+    refs.reserve((size_t)nfr);
     if (hipStreamSynchronize(s_main) != hipSuccess) return AMOD_ERR_HIP;
     const amod::GapScan *g = c->gaps_h.as<amod::GapScan>();
     refs.clear();
@@ -898,9 +904,16 @@ struct Prepass {
       gaps.push_back(g[r]);
       if (dev_metrics && g[r].ref_ok) refs.push_back({g[r].pre_pos, g[r].ref_pos, g[r].ref_best});
     }
-    std::sort(gaps.begin(), gaps.end(), [](const amod::GapScan &a, const amod::GapScan &b) { return a.s0 < b.s0; });
-    std::sort(refs.begin(), refs.end(), [](const GpuRefine &a, const GpuRefine &b) { return a.pre_pos < b.pre_pos; });
+    // (records come in fine-range order, which is stream order: usually sorted already)
+    auto by_s0 = [](const amod::GapScan &a, const amod::GapScan &b) { return a.s0 < b.s0; };
+    auto by_pre = [](const GpuRefine &a, const GpuRefine &b) { return a.pre_pos < b.pre_pos; };
+    if (!std::is_sorted(gaps.begin(), gaps.end(), by_s0)) std::sort(gaps.begin(), gaps.end(), by_s0);
+    if (!std::is_sorted(refs.begin(), refs.end(), by_pre)) std::sort(refs.begin(), refs.end(), by_pre);
     return AMOD_SUCCESS;
+  }
+  ~Prepass() { // the record vectors' pages go back to the context's cache
+    if (c && gaps.capacity() > c->gaps_keep.capacity()) c->gaps_keep.swap(gaps);
+    if (c && refs.capacity() > c->refs_keep.capacity()) c->refs_keep.swap(refs);
   }
 
   double setup_ms[4] = {}; // diagnostics: marks, index, pointer table, gather + copies
@@ -1212,6 +1225,7 @@ struct WindowDecoder {
   std::vector<uint8_t> zero_row;
   int64_t stride = 16;
   double t_ms = 0, t_launch = 0; // host time in launch + collect (t_launch: launch alone)
+  bool diag = false;      // (AMOD_STREAM_DIAG: slow launch steps reported as they happen)
   double t_sub[8] = {}; // (diagnostics) launch: host prep, device buffers + input copies, memset, k_window, reserve, decode, event + wait, D2H enqueue
   // a batch in flight in buffer set k
   struct Flight {
@@ -1287,10 +1301,17 @@ struct WindowDecoder {
       S_TRY(hipEventRecord(c.w_kern[k], s));
       S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
       lap(t_sub[6]);
+      const double d7 = t_sub[7];
+      const auto tq0 = std::chrono::steady_clock::now();
       S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, c.s3));
+      const auto tq1 = std::chrono::steady_clock::now();
       S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
       S_TRY(hipEventRecord(c.w_done[k], c.s3));
       lap(t_sub[7]);
+      if (diag && t_sub[7] - d7 > 0.5)
+        fprintf(stderr, "[stream]   slow D2H enqueue: set %d, %d windows, rows %zu B: results %.3f ms, rest %.3f ms\n", k, nw,
+                (size_t)f.stride * nw, std::chrono::duration<double, std::milli>(tq1 - tq0).count(),
+                t_sub[7] - d7 - std::chrono::duration<double, std::milli>(tq1 - tq0).count());
     } else {
       S_TRY(hipEventRecord(c.w_done[k], s));
     }
@@ -1440,6 +1461,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   int64_t nfr = 0, frames_decoded = 0, frame_errors = 0, fine_host = 0;
   std::vector<int64_t> fails_out;
   WindowDecoder wd;
+  wd.diag = kn.stream_diag;
   CopyPool copies(std::max(0, std::min(8, nthreads) - 1));
   double t_loop = 0, t_copy = 0; // (diagnostics: the dispatch's per-frame loop and its copies)
 
