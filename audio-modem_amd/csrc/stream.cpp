@@ -697,7 +697,7 @@ struct StreamCache {
   // window decoder: three buffer sets (one batch decoding, one dispatched by the host, one
   // whose chunk bytes the copy pool is still moving into the assembler)
   static constexpr int kSets = 3;
-  DBuf w_pos[kSets], w_len[kSets], w_woff[kSets], w_win[kSets], w_res[kSets], w_pay[kSets];
+  DBuf w_pos[kSets], w_len[kSets], w_woff[kSets], w_win[kSets], w_out[kSets]; // w_out: results, then payload rows
   hipEvent_t w_done[kSets] = {}, w_kern[kSets] = {};
   hipStream_t s3 = nullptr; // window decoder: results and payload rows to the host, beside the next batch's kernels
   DBuf d_c, d_gsrc;                         // sparse copy: packed granules, their stream granules
@@ -706,7 +706,7 @@ struct StreamCache {
   PageBuf yh;
   Pinned yc, hot_h, metric_h;
   Pinned gsrc_h; // the sparse gather's granule list (pinned: its upload does not block the host)
-  Pinned w_res_h[kSets], w_pay_h[kSets];    // window decoder: results and payload rows (pinned D2H)
+  Pinned w_out_h[kSets];                    // window decoder: w_out's host mirror (one pinned D2H)
   // the sparse copy's per-granule tables (kept: no page faults or address-space locks per call)
   std::vector<uint8_t> sp_need;
   std::vector<std::pair<int64_t, int64_t>> sp_reg; // (kept: its pages stay faulted in across calls)
@@ -1233,6 +1233,7 @@ struct WindowDecoder {
     std::vector<int32_t> len;
     std::vector<int> slot;
     int64_t stride = 16;
+    size_t rb = 0; // the results' bytes ahead of the rows in w_out
     int nw = 0;
     size_t a = 0, b = 0;
     bool live = false;
@@ -1260,10 +1261,12 @@ struct WindowDecoder {
     const int nw = f.nw = (int)f.pos.size();
     f.stride = amod_payload_stride(cfg, std::max<int64_t>(maxlen, 1));
     StreamCache &c = *pp.c;
-    DBuf &d_pos = c.w_pos[k], &d_len = c.w_len[k], &d_woff = c.w_woff[k], &d_win = c.w_win[k], &d_res = c.w_res[k],
-         &d_pay = c.w_pay[k];
-    S_TRY(c.w_res_h[k].alloc(sizeof(amod_result) * (size_t)std::max(nw, 1)));
-    S_TRY(c.w_pay_h[k].alloc((size_t)f.stride * std::max(nw, 1)));
+    DBuf &d_pos = c.w_pos[k], &d_len = c.w_len[k], &d_woff = c.w_woff[k], &d_win = c.w_win[k], &d_out = c.w_out[k];
+    // results and rows in one buffer, so they come back in one copy (a separate 400 KB
+    // results copy held the host ~7 ms on the host-sample path: HIP ran it as a blocking copy)
+    const size_t rb = f.rb = (sizeof(amod_result) * (size_t)std::max(nw, 1) + 255) & ~size_t(255);
+    const size_t ob = rb + (size_t)f.stride * std::max(nw, 1);
+    S_TRY(c.w_out_h[k].alloc(ob));
     if (!c.w_done[k]) S_TRY(hipEventCreateWithFlags(&c.w_done[k], hipEventDisableTiming));
     if (!c.w_kern[k]) S_TRY(hipEventCreateWithFlags(&c.w_kern[k], hipEventDisableTiming));
     if (!c.s3) S_TRY(hipStreamCreateWithFlags(&c.s3, hipStreamNonBlocking));
@@ -1278,13 +1281,14 @@ struct WindowDecoder {
       S_TRY(d_len.alloc(sizeof(int32_t) * nw));
       S_TRY(d_woff.alloc(sizeof(int64_t) * nw));
       S_TRY(d_win.alloc(sizeof(float) * (size_t)tot + 64));
-      S_TRY(d_res.alloc(sizeof(amod_result) * nw));
-      S_TRY(d_pay.alloc((size_t)f.stride * nw));
+      S_TRY(d_out.alloc(ob));
+      amod_result *const d_res = reinterpret_cast<amod_result *>(d_out.p);
+      uint8_t *const d_pay = reinterpret_cast<uint8_t *>(d_out.p) + rb;
       S_TRY(hipMemcpyAsync(d_pos.p, f.pos.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_len.p, f.len.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(d_woff.p, f.woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, s));
       lap(t_sub[1]);
-      S_TRY(hipMemsetAsync(d_pay.p, 0, (size_t)f.stride * nw, s));
+      S_TRY(hipMemsetAsync(d_pay, 0, (size_t)f.stride * nw, s));
       lap(t_sub[2]);
       S_TRY(amod_launch_window(pp.y(), pp.n, d_pos.as<int64_t>(), d_len.as<int32_t>(),
                                d_woff.as<int64_t>(), nw, d_win.as<float>(), s));
@@ -1293,7 +1297,7 @@ struct WindowDecoder {
       if (rc) return rc;
       lap(t_sub[4]);
       rc = amod_decode_device(ctx, cfg, AMOD_MODE_CHUNK, d_win.as<float>(), d_woff.as<int64_t>(), d_len.as<int32_t>(),
-                              nw, d_res.as<amod_result>(), d_pay.as<uint8_t>(), f.stride, 0, s);
+                              nw, d_res, d_pay, f.stride, 0, s);
       if (rc) return rc;
       lap(t_sub[5]);
       // the rows go to the host on s3, so the next batch's kernels on s do not queue behind
@@ -1302,14 +1306,18 @@ struct WindowDecoder {
       S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
       lap(t_sub[6]);
       const double d7 = t_sub[7];
+      int busy = 0; // (diagnostics: which streams still have work queued as the copies go in)
+      if (diag) {
+        const hipStream_t qs[5] = {s, c.s2, c.s3, c.s_up, amod_ctx_stream(ctx)};
+        for (int i = 0; i < 5; ++i) busy |= (qs[i] && hipStreamQuery(qs[i]) == hipErrorNotReady) << i;
+      }
       const auto tq0 = std::chrono::steady_clock::now();
-      S_TRY(hipMemcpyAsync(c.w_res_h[k].p, d_res.p, sizeof(amod_result) * nw, hipMemcpyDeviceToHost, c.s3));
+      S_TRY(hipMemcpyAsync(c.w_out_h[k].p, d_out.p, rb + (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
       const auto tq1 = std::chrono::steady_clock::now();
-      S_TRY(hipMemcpyAsync(c.w_pay_h[k].p, d_pay.p, (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
       S_TRY(hipEventRecord(c.w_done[k], c.s3));
       lap(t_sub[7]);
       if (diag && t_sub[7] - d7 > 0.5)
-        fprintf(stderr, "[stream]   slow D2H enqueue: set %d, %d windows, rows %zu B: results %.3f ms, rest %.3f ms\n", k, nw,
+        fprintf(stderr, "[stream]   slow D2H enqueue: set %d, %d windows, busy streams 0x%x (s, s2, s3, s_up, ctx), rows %zu B: copy %.3f ms, event %.3f ms\n", k, nw, busy,
                 (size_t)f.stride * nw, std::chrono::duration<double, std::milli>(tq1 - tq0).count(),
                 t_sub[7] - d7 - std::chrono::duration<double, std::milli>(tq1 - tq0).count());
     } else {
@@ -1328,8 +1336,8 @@ struct WindowDecoder {
     StreamCache &c = *pp.c;
     S_TRY(hipEventSynchronize(c.w_done[k]));
     f.live = false;
-    const amod_result *rh = c.w_res_h[k].as<amod_result>();
-    ph = c.w_pay_h[k].as<uint8_t>();
+    const amod_result *rh = c.w_out_h[k].as<amod_result>();
+    ph = reinterpret_cast<const uint8_t *>(c.w_out_h[k].p) + f.rb;
     stride = f.stride;
     if (zero_row.size() != (size_t)stride) zero_row.assign((size_t)stride, 0);
     slot = f.slot;
