@@ -180,6 +180,8 @@ struct Knobs {
   // streaming receiver (stream.cpp)
   int stream_minseg = 0;    // AMOD_STREAM_MINSEG
   bool stream_diag = false; // AMOD_STREAM_DIAG
+  int stream_d2h = 1;       // AMOD_STREAM_D2H: window rows back by 1 a D2H copy on the launch stream
+                            // (default), 0 one on the copy stream s3, 2 a device copy into mapped pinned memory
   bool no_gap_scan = false; // AMOD_NO_GAP_SCAN
   int stream_threads = -1;  // AMOD_STREAM_THREADS (-1: unset)
   bool stream_fullcopy = false; // AMOD_STREAM_FULLCOPY

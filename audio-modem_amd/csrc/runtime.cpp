@@ -343,6 +343,7 @@ void read_knobs(amod::Knobs &k) {
   k.mall_flush_mb = std::max(0, env_int("AMOD_MALL_FLUSH_MB", 0));
   k.stream_minseg = std::max(0, env_int("AMOD_STREAM_MINSEG", 0));
   k.stream_diag = getenv("AMOD_STREAM_DIAG") != nullptr;
+  k.stream_d2h = std::min(2, std::max(0, env_int("AMOD_STREAM_D2H", 1)));
   k.no_gap_scan = getenv("AMOD_NO_GAP_SCAN") != nullptr;
   k.stream_threads = env_int("AMOD_STREAM_THREADS", -1);
   k.stream_fullcopy = getenv("AMOD_STREAM_FULLCOPY") != nullptr;

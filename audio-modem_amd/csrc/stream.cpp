@@ -1226,6 +1226,7 @@ struct WindowDecoder {
   int64_t stride = 16;
   double t_ms = 0, t_launch = 0; // host time in launch + collect (t_launch: launch alone)
   bool diag = false;      // (AMOD_STREAM_DIAG: slow launch steps reported as they happen)
+  int d2h_mode = 1;       // (AMOD_STREAM_D2H)
   double t_sub[8] = {}; // (diagnostics) launch: host prep, device buffers + input copies, memset, k_window, reserve, decode, event + wait, D2H enqueue
   // a batch in flight in buffer set k
   struct Flight {
@@ -1266,7 +1267,7 @@ struct WindowDecoder {
     // results copy held the host ~7 ms on the host-sample path: HIP ran it as a blocking copy)
     const size_t rb = f.rb = (sizeof(amod_result) * (size_t)std::max(nw, 1) + 255) & ~size_t(255);
     const size_t ob = rb + (size_t)f.stride * std::max(nw, 1);
-    S_TRY(c.w_out_h[k].alloc(ob));
+    S_TRY(c.w_out_h[k].alloc(ob, d2h_mode == 2));
     if (!c.w_done[k]) S_TRY(hipEventCreateWithFlags(&c.w_done[k], hipEventDisableTiming));
     if (!c.w_kern[k]) S_TRY(hipEventCreateWithFlags(&c.w_kern[k], hipEventDisableTiming));
     if (!c.s3) S_TRY(hipStreamCreateWithFlags(&c.s3, hipStreamNonBlocking));
@@ -1300,10 +1301,15 @@ struct WindowDecoder {
                               nw, d_res, d_pay, f.stride, 0, s);
       if (rc) return rc;
       lap(t_sub[5]);
-      // the rows go to the host on s3, so the next batch's kernels on s do not queue behind
-      // them (a batch's 9 MB of rows took as long as its kernels)
-      S_TRY(hipEventRecord(c.w_kern[k], s));
-      S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
+      // the rows go to the host on the launch stream, behind the batch's kernels (round 5,
+      // interleaved on one box: host samples 1.01 -> 1.07e10, device-resident 4.54 -> 4.8e10
+      // samples/s against the copy stream s3, which an earlier layout needed so the next
+      // batch's kernels did not queue behind 9 MB of rows; AMOD_STREAM_D2H=0 keeps that)
+      hipStream_t s_out = d2h_mode == 1 ? s : c.s3;
+      if (s_out != s) {
+        S_TRY(hipEventRecord(c.w_kern[k], s));
+        S_TRY(hipStreamWaitEvent(c.s3, c.w_kern[k], 0));
+      }
       lap(t_sub[6]);
       const double d7 = t_sub[7];
       int busy = 0; // (diagnostics: which streams still have work queued as the copies go in)
@@ -1312,9 +1318,12 @@ struct WindowDecoder {
         for (int i = 0; i < 5; ++i) busy |= (qs[i] && hipStreamQuery(qs[i]) == hipErrorNotReady) << i;
       }
       const auto tq0 = std::chrono::steady_clock::now();
-      S_TRY(hipMemcpyAsync(c.w_out_h[k].p, d_out.p, rb + (size_t)f.stride * nw, hipMemcpyDeviceToHost, c.s3));
+      if (d2h_mode == 2 && c.w_out_h[k].dp)
+        S_TRY(hipMemcpyAsync(c.w_out_h[k].dp, d_out.p, rb + (size_t)f.stride * nw, hipMemcpyDeviceToDevice, s_out));
+      else
+        S_TRY(hipMemcpyAsync(c.w_out_h[k].p, d_out.p, rb + (size_t)f.stride * nw, hipMemcpyDeviceToHost, s_out));
       const auto tq1 = std::chrono::steady_clock::now();
-      S_TRY(hipEventRecord(c.w_done[k], c.s3));
+      S_TRY(hipEventRecord(c.w_done[k], s_out));
       lap(t_sub[7]);
       if (diag && t_sub[7] - d7 > 0.5)
         fprintf(stderr, "[stream]   slow D2H enqueue: set %d, %d windows, busy streams 0x%x (s, s2, s3, s_up, ctx), rows %zu B: copy %.3f ms, event %.3f ms\n", k, nw, busy,
@@ -1470,6 +1479,7 @@ static int stream_receive(amod_ctx *ctx, const amod_cfg *cfg, const float *sampl
   std::vector<int64_t> fails_out;
   WindowDecoder wd;
   wd.diag = kn.stream_diag;
+  wd.d2h_mode = kn.stream_d2h;
   CopyPool copies(std::max(0, std::min(8, nthreads) - 1));
   double t_loop = 0, t_copy = 0; // (diagnostics: the dispatch's per-frame loop and its copies)
 
