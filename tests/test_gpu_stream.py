@@ -223,3 +223,36 @@ def test_gpu_gap_scans_equal_host_scans():
         assert np.array_equal(host[0], other[0]) and host[1] == other[1]
         assert [host[2][k] for k in keys] == [other[2][k] for k in keys]
         assert host[3] == other[3] and host[4] == other[4]
+
+
+def test_streams_back_to_back_on_one_context():
+    """One context decodes a long stream, golden streams of other presets and sizes, then
+    the long one again: every call equals a fresh context's decode (the per-context stream
+    cache — gap-scan record vectors, window-decoder buffer sets, pinned mirrors — keeps no
+    state between calls), with the window rows returned on the launch stream (default) and
+    on the copy stream (AMOD_STREAM_D2H=0)."""
+    n = 120
+    cfg4, x4, data4, _ = c4_stream(n, chunk=1024, seed=0xC4000002)
+    golden = [s for s in streams() if s["name"] in ("qpsk_dc_gain_lead", "qam16_noise20", "qpsk_corrupt_retransmit")]
+    cases = [(cfg4, x4)] + [build_stream(sp)[:2] for sp in golden] + [(cfg4, x4)]
+    keys = ("nframes", "nrefine_fail", "frames_decoded", "frame_errors", "final_state", "final_scan_pos")
+    fresh = [_run(cfg, x, {}) for cfg, x in cases]
+    assert fresh[0][4] == data4
+    for mode in ("1", "0"):
+        old = os.environ.get("AMOD_STREAM_D2H")
+        os.environ["AMOD_STREAM_D2H"] = mode
+        try:
+            dm = amodem.Demodulator(0)
+            for (cfg, x), want in zip(cases, fresh):
+                asm = amodem.ChunkAssembler()
+                fr, rf, st = dm.stream_receive(cfg, x, asm)
+                assert np.array_equal(fr, want[0]) and rf == want[1], mode
+                assert [st[k] for k in keys] == [want[2][k] for k in keys], mode
+                assert asm.state() == want[3]
+                assert (asm.assemble_file() if asm.is_complete() else None) == want[4]
+            dm.close()
+        finally:
+            if old is None:
+                os.environ.pop("AMOD_STREAM_D2H", None)
+            else:
+                os.environ["AMOD_STREAM_D2H"] = old
