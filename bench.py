@@ -966,6 +966,175 @@ def cpu_legs(wl: Workload, rec, js_frames, js_seconds=1.5):
     return cpu
 
 
+# ------------------------------------------------------------- the JSON line --
+LINE_MAX = 8192  # bytes of the printed line (the driver's parser gave up on r05's 20.9 KB line)
+
+
+def _g(v, nd=4):
+    """A float to nd significant digits (the compact line's secondary numbers)."""
+    if isinstance(v, float):
+        return float(f"{v:.{nd}g}")
+    return v
+
+
+def _pick(d, keys, nd=4):
+    """The keys of d that are present, floats rounded; nested (key, subkeys) pairs recurse."""
+    out = {}
+    if not isinstance(d, dict):
+        return out
+    for k in keys:
+        if isinstance(k, tuple):
+            k, sub = k
+            if isinstance(d.get(k), dict):
+                out[k] = _pick(d[k], sub, nd)
+        elif k in d:
+            out[k] = _g(d[k], nd)
+    return out
+
+
+def _leg_summary(leg):
+    """One config leg in a few numbers: rate, step, dominant kernel and its roofline
+    fraction, the chain, oracle agreement; the soft-combine and noisy objects by count."""
+    if not isinstance(leg, dict):
+        return leg
+    if "error" in leg:
+        return {"error": str(leg["error"])[:200]}
+    out = _pick(leg, ["value", "ms_per_step", "payload_MB_per_s", "frames_ok", "frames_exact_fallback"])
+    rf = leg.get("roofline")
+    if isinstance(rf, dict):
+        out["kernel"] = rf.get("kernel")
+        out["kernel_ms"] = _g(rf.get("kernel_ms_avg"))
+        out["frac"] = _g(rf.get("frac"))
+        out["traffic"] = _g(rf.get("traffic"))
+    ch = leg.get("chain")
+    if isinstance(ch, dict):
+        out["chain_ms"] = _g(ch.get("ms_avg"))
+        out["kernels_ms"] = {k: _g(v) for k, v in (ch.get("kernels_ms_avg") or {}).items()}
+    cb = leg.get("cpu_baseline")
+    if isinstance(cb, dict):
+        out["oracle_agree"] = (cb.get("oracle_agree") or cb.get("error", ""))[:80]
+        out["cpu_value"] = _g(cb.get("value"))
+    for k in ("soft_combine", "noisy"):
+        if isinstance(leg.get(k), dict):
+            out[k] = _soft_summary(leg[k])
+    if "hard" in leg or "soft" in leg:  # a soft_leg object itself
+        out.update(_soft_summary(leg))
+    return out
+
+
+def _soft_summary(s):
+    out = {}
+    for name in ("hard", "soft"):
+        if isinstance(s.get(name), dict):
+            out[name] = _pick(s[name], ["ms_per_step", "k_demod_ms", "frames_crc_valid", "frames_exact",
+                                        "frames_payload_ok", "bit_errors", "oracle_agree"])
+    for k in ("soft_over_hard_step", "frames", "snr_db", "noise_divisor", "oracle_agree", "ms_per_step",
+              "frames_listed", "listed_ms"):
+        if k in s:
+            out[k] = _g(s[k]) if not isinstance(s[k], str) else s[k][:80]
+    return out
+
+
+def compact_line(full: dict, full_path=None) -> dict:
+    """The one stdout line the driver parses: the contract's keys and the whole roofline /
+    cpu_baseline objects (long prose cut), then one-number summaries of every other
+    object; `full` (written beside, at full_path) keeps everything. Bounded to LINE_MAX
+    bytes (tests/test_bench_line.py)."""
+    out = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
+    if isinstance(full.get("config"), dict):
+        out["config"] = dict(full["config"])
+    if isinstance(full.get("roofline"), dict):
+        rf = {k: v for k, v in full["roofline"].items() if k != "algorithmic_bytes_what"}
+        rf["per_unit"] = full["roofline"].get("algorithmic_bytes_what", "")[:80]
+        out["roofline"] = rf
+    cb = full.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "single_core", "oracle_agree",
+                                "js_agree_ok", "error") if k in cb}
+        if "sample" in c:
+            c["sample"] = str(c["sample"])[:240]
+        if isinstance(cb.get("c_port"), dict):
+            c["c_port_value"] = cb["c_port"].get("value")
+        if isinstance(cb.get("calibration"), dict):
+            c["js_over_modem_js"] = _g(cb["calibration"].get("js_over_modem_js"))
+        out["cpu_baseline"] = c
+    out.update(_pick(full, ["payload_MB_per_s", "frames_ok", "frames_exact_fallback", "devices"]))
+    out.update(_pick(full, [("pipeline", ["contexts", "one_context_ms_per_step"]),
+                            ("scan_roofline", ["kernel", "kernel_ms_avg", "frac"]),
+                            ("graph", ["ms_per_step", "frames_ok", "error"]),
+                            ("e2e", ["samples_per_s", "ms"]),
+                            ("gather", ["frames", "ms", "GBps", "records_ok", "ranks_joined", "devices"]),
+                            ("group", ["ms_per_step", "samples_per_s", "records_equal_per_rank", "frames_ok",
+                                       "frames"])]))
+    ch = full.get("chain")
+    if isinstance(ch, dict):
+        out["chain"] = {"ms_avg": _g(ch.get("ms_avg")), "frac": _g(ch.get("frac")),
+                        "kernels_ms": {k: _g(v) for k, v in (ch.get("kernels_ms_avg") or {}).items()}}
+    tx = full.get("tx")
+    if isinstance(tx, dict):
+        out["tx"] = {"kernel_ms_avg": _g(tx.get("kernel_ms_avg")),
+                     "frac": _g((tx.get("roofline") or {}).get("frac"))}
+    ha = full.get("host_api")
+    if isinstance(ha, dict):
+        h = {}
+        if isinstance(ha.get("python_decode_host"), dict):
+            h["python_ms"] = _g(ha["python_decode_host"].get("ms"))
+        nb = ha.get("node_decode_batch")
+        if isinstance(nb, dict):
+            h["node_ms"] = _g(nb.get("ms")) if "ms" in nb else str(nb.get("error", ""))[:120]
+            if isinstance(nb.get("resident"), dict):
+                h["node_resident_ms"] = _g(nb["resident"].get("ms"))
+        out["host_api"] = h
+    st = full.get("stream")
+    if isinstance(st, dict):
+        s = _pick(st, ["samples_per_s", "payload_MB_per_s", "frames", "file_ok"])
+        s["phases_ms"] = {k: _g(v) for k, v in (st.get("phases_ms") or {}).items()}
+        dr = st.get("device_resident")
+        if isinstance(dr, dict):
+            s["device_resident"] = _pick(dr, ["samples_per_s", "file_ok", "host_share"])
+            s["device_resident"]["phases_ms"] = {k: _g(v) for k, v in (dr.get("phases_ms") or {}).items()}
+        out["stream"] = s
+    legs = full.get("legs")
+    if isinstance(legs, dict):
+        L = {}
+        for name, leg in legs.items():
+            if name == "c1_latency" and isinstance(leg, dict):
+                L[name] = {"python_ms": _g((leg.get("python_decode_received_signal") or {}).get("median_ms")),
+                           "node_ms": _g((leg.get("node_decode_received_signal") or {}).get("median_ms")),
+                           "cpu_js_ms": _g((leg.get("cpu_js_one_core") or {}).get("ms_per_call")),
+                           "speedup_vs_cpu_js": _g(leg.get("speedup_vs_cpu_js"))}
+            else:
+                L[name] = _leg_summary(leg)
+        out["legs"] = L
+    if full_path:
+        out["full"] = full_path
+    line = json.dumps(out, separators=(",", ":"))
+    if len(line) > LINE_MAX:  # (never expected: drop the summaries, keep the contract)
+        for k in ("legs", "stream", "host_api", "group", "gather", "graph", "e2e", "scan_roofline", "tx"):
+            out.pop(k, None)
+            if len(json.dumps(out, separators=(",", ":"))) <= LINE_MAX:
+                break
+        out["truncated"] = True
+    return out
+
+
+def write_full(full: dict):
+    """The whole result object beside the line: $AMOD_BENCH_FULL, else
+    gpurun_out/bench_full.json under the run's tree. Returns the path (relative to the
+    tree when inside it), or None when it could not be written."""
+    path = os.environ.get("AMOD_BENCH_FULL") or os.path.join(ROOT, "gpurun_out", "bench_full.json")
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as e:
+        print(f"bench.py: could not write {path}: {e}", file=sys.stderr)
+        return None
+    ap = os.path.abspath(path)
+    return os.path.relpath(ap, ROOT) if ap.startswith(ROOT + os.sep) else ap
+
+
 # --------------------------------------------------------------------- main --
 def graph_leg(env: Env, wl: Workload, steps: int):
     """The same decode captured once into a hipGraph (amod_reserve was called; include/
@@ -1134,7 +1303,8 @@ def main():
         out["legs"] = extra
         if lat is not None:
             out["legs"]["c1_latency"] = lat
-        print(json.dumps(out), flush=True)
+        path = write_full(out)
+        print(json.dumps(compact_line(out, path), separators=(",", ":")), flush=True)
     if env.world > 1:
         env.dist.destroy_process_group()
 
