@@ -168,7 +168,9 @@ class Demodulator:
         progress(done, records, payload): called (from the library's helper thread, one
         call at a time, all before this returns) whenever frames [0, done) are final in the
         returned arrays (amod_decode_host_progress), while later frames are still
-        uploading and decoding."""
+        uploading and decoding. The first exception progress raises is re-raised here once
+        the decode has finished (later calls are skipped); progress must not call back into
+        this Demodulator (its lock is held for the whole decode)."""
         samples = np.ascontiguousarray(samples, np.float32)
         offsets = np.ascontiguousarray(offsets, np.int64)
         lengths = np.ascontiguousarray(lengths, np.int32)
@@ -188,11 +190,23 @@ class Demodulator:
                                                  offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data,
                                                  pay.ctypes.data, stride, options), self.ctx)
             else:
-                fn = L.PROGRESS_FN(lambda _user, done: progress(int(done), rec, pay))
+                failed = []
+
+                def call(_user, done):  # (an exception would be printed and lost by ctypes)
+                    if failed:
+                        return
+                    try:
+                        progress(int(done), rec, pay)
+                    except BaseException as e:  # noqa: B902 (re-raised below)
+                        failed.append(e)
+
+                fn = L.PROGRESS_FN(call)
                 L.check(self._L.amod_decode_host_progress(
                     self.ctx, C.byref(cfg), mode, samples.ctypes.data if samples.size else None, samples.size,
                     offsets.ctypes.data, lengths.ctypes.data, n, rec.ctypes.data, pay.ctypes.data, stride, options,
                     fn, None), self.ctx)
+                if failed:
+                    raise failed[0]
         return rec, pay
 
     def decode_received_signal(self, signal, mod="QPSK", rep=1, options=0) -> dict:

@@ -24,10 +24,9 @@ constexpr int XT = 256;     // threads per workgroup
 constexpr int CH = 3072;    // sample chunk staged in LDS (XSmem <= 40 KB: four workgroups per CU)
 
 constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH doubles overlay the FFT arrays)
-#ifndef AMOD_SEG_G
-#define AMOD_SEG_G 1024
+#ifndef AMOD_SC_CQ
+#define AMOD_SC_CQ 4
 #endif
-constexpr int kSegG = AMOD_SEG_G; // samples per certified segment of the mean (at least)
 
 struct alignas(16) XSmem { // (static_assert below: four per CU fit the 160 KB of LDS)
   float chunk[CH + 520];
@@ -52,6 +51,49 @@ static_assert(sizeof(XSmem) <= 40 * 1024, "list A's exact workgroup must fit bes
 
 __device__ __forceinline__ double or_zero(float v) { return (v != v || v == 0.0f) ? 0.0 : (double)v; } // `x || 0`
 __device__ __forceinline__ int rev9(int i) { return (int)(__brev((unsigned)i) >> 23); }
+// a[k] for a wave-uniform k < 4 (a select chain: no private-array indexing)
+__device__ __forceinline__ double sel4(const double (&a)[4], int k) {
+  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+// DPP move of a double: lanes whose source is out of the row (row_shr) or whose row is
+// masked off read 0
+template <int CTRL, int ROWS> __device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROWS, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// inclusive wave scan of doubles (row_shr 1/2/4/8, then row_bcast 15 / 31): exact when
+// every sum of a run of lanes is representable (the caller's certificate)
+__device__ __forceinline__ double wave_scan_f64(double v) {
+  v += dpp_f64<0x111, 0xf>(v);
+  v += dpp_f64<0x112, 0xf>(v);
+  v += dpp_f64<0x114, 0xf>(v);
+  v += dpp_f64<0x118, 0xf>(v);
+  v += dpp_f64<0x142, 0xa>(v);
+  v += dpp_f64<0x143, 0xc>(v);
+  return v;
+}
+// the wave's minimum (DPP: a lane without a source keeps its own value; lane 63 ends
+// with the minimum of all 64)
+template <int CTRL, int ROWS> __device__ __forceinline__ int dpp_min_step(int v) {
+  return min(v, __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+  v = dpp_min_step<0x111, 0xf>(v);
+  v = dpp_min_step<0x112, 0xf>(v);
+  v = dpp_min_step<0x114, 0xf>(v);
+  v = dpp_min_step<0x118, 0xf>(v);
+  v = dpp_min_step<0x142, 0xa>(v);
+  v = dpp_min_step<0x143, 0xc>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+// lane l's double (l wave-uniform)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 // fft(re, 0) of 512 real samples src[0..511] (modem.js:6-13, 26-66), result in sm.re/sm.im
 __device__ void fft_exact(const float *src, XSmem &sm, const double2 *tw) {
@@ -287,21 +329,37 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
       __syncthreads();
       XSTAMP(13);
       if (!exact_par) {
-        // Segments of G >= kSegG samples, certified one by one along the sequential order. A
+        // Segments of G >= 1024 samples, certified one by one along the sequential order. A
         // segment whose sum|x| < 2^(em + 53) (em: its smallest sample ulp exponent) has
         // exact internal sums in any order, so its total comes out exact from one thread's
         // running sum. With S the running (sequential) sum at its start and q the smaller
         // of em and the exponent of S's lowest set bit, every partial sum S + P_j is a
         // multiple of 2^q no larger than |S| + sum|x| in magnitude; below 2^(q + 53) none
-        // of them rounds and S + total is the sequential result. A segment failing either
-        // test (a sample far below the running sum's ulp, or a partial sum that could
-        // round) is summed sample by sample. One thread per segment (the frame is
-        // L2-resident after the pass above): no cross-lane scans.
-        constexpr int SEGCAP = SCH;
+        // of them rounds and S + total is the sequential result.
+        //
+        // A segment failing the test (a partial sum that could round: once S has a full
+        // mantissa, any segment that could carry it across a binade) is walked in pieces of
+        // 256 samples, one per wave at a time: each wave forms its piece's exact prefix sums
+        // Q_j (four consecutive samples per lane, a DPP wave scan); wave 0 then walks the
+        // pieces: with S exact at a piece start, lane j's s_j = fl(S + Q_j) IS the sequential
+        // state after sample j as long as no earlier sum rounded (by induction: state_j =
+        // fl(state_{j-1} + x_j) with state_{j-1} = S + Q_{j-1} exactly). TwoSum finds the
+        // first j* whose sum rounded; its s is still the sequential state (the rounding the
+        // reference makes), and the piece continues from S = s_{j*} with Q_j - Q_{j*}
+        // (exact: a sum within the piece). A piece costs one pass plus one per rounding
+        // event where one lane adding sample by sample cost ≈ 120 cycles a sample (a C5
+        // frame at 7 dB took 13 M cycles). A piece's Q are exact when the segment's
+        // sum|x| < 2^(em + 53) for the piece's own em; a piece failing that is added sample
+        // by sample.
+        constexpr int SEGCAP = SCH, kSegG = 1024;
         double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_e = sm.sc + 2 * SEGCAP;
         const int G = kSegG * max(1, (N + kSegG * SEGCAP - 1) / (kSegG * SEGCAP));
         const int nseg = (N + G - 1) / G;
-        for (int sg = tid; sg < nseg; sg += XT) {
+        // (one wave per segment, lanes on consecutive samples: a thread per segment read
+        // 64 far-apart lines per load instruction and took ~250 K cycles a C5 frame. The
+        // order of the adds is free: ss is used only when certified, where every order is
+        // exact, and sa's rounding is within the slack below)
+        for (int sg = wave; sg < nseg; sg += XT / 64) {
           const int b0 = sg * G, e1 = min(N, b0 + G);
           double ss = 0.0, sa = 0.0;
           int em = 1 << 20;
@@ -311,49 +369,120 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
             const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
             if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
           };
-          int i = b0;
-          for (; i + 8 <= e1; i += 8) {
+          int i = b0 + lane;
+          for (; i + 7 * 64 < e1; i += 8 * 64) {
             float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = xr[i + u];
+            for (int u = 0; u < 8; ++u) v[u] = xr[i + 64 * u];
 #pragma unroll
             for (int u = 0; u < 8; ++u) add(v[u]);
           }
-          for (; i < e1; ++i) add(xr[i]);
-          seg_s[sg] = ss; seg_a[sg] = sa; seg_e[sg] = (double)em;
+          for (; i < e1; i += 64) add(xr[i]);
+          ss = wave_scan_f64(ss);
+          sa = wave_scan_f64(sa);
+          em = wave_min_i32(em);
+          if (lane == 63) { seg_s[sg] = ss; seg_a[sg] = sa; seg_e[sg] = (double)em; }
         }
         __syncthreads();
-        if (wave == 0) { // the chain along the segments: wave-uniform S on every lane
-          double S = 0.0;
-          for (int sg = 0; sg < nseg; ++sg) {
-            const int em = (int)seg_e[sg];
-            if (em >= (1 << 19)) continue; // all zeros
-            // S is a multiple of 2^(exponent of its lowest set bit)
-            int qs = 1 << 20;
-            if (S != 0.0) {
-              const uint64_t b = (uint64_t)__double_as_longlong(S);
-              const int be = (int)((b >> 52) & 0x7FF);
-              const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (be ? (1ull << 52) : 0ull);
-              qs = (be ? be : 1) - 1075 + __builtin_ctzll(m);
-            }
-            const int q = min(em, qs);
-            // (sum|x| in fp64 over G terms: relative error below G 2^-53)
-            const double slack = 1.0 + ldexp((double)G, -52);
-            const bool inner = seg_a[sg] * slack < ldexp(1.0, em + 53);
-            const double reach = (fabs(S) + seg_a[sg]) * slack;
-            if (inner && reach < ldexp(1.0, q + 53)) {
-              S += seg_s[sg];
-            } else { // sample by sample: 64 coalesced loads, then lane by lane in order
-              const int e1 = min(N, (sg + 1) * G);
-              for (int b0 = sg * G; b0 < e1; b0 += 64) {
-                const float v = b0 + lane < e1 ? xr[b0 + lane] : 0.f;
-                const int nj = min(64, e1 - b0);
-                for (int j = 0; j < nj; ++j) S += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-              }
-            }
+        constexpr int PW = 256, NW = XT / 64;
+        double *const qb = reinterpret_cast<double *>(sm.chunk); // one piece per wave
+        uint32_t *const qok = sm.ru;
+        static_assert(sizeof(sm.chunk) >= NW * PW * sizeof(double) && NW <= 16, "piece buffers");
+        // (sum|x| in fp64 over G terms: relative error below G 2^-53)
+        const double slack = 1.0 + ldexp((double)G, -52);
+        double S = 0.0; // (every thread holds the same)
+        for (int sg = 0; sg < nseg; ++sg) {
+          const int em = (int)seg_e[sg];
+          if (em >= (1 << 19)) continue; // all zeros
+          // S is a multiple of 2^(exponent of its lowest set bit)
+          int qs = 1 << 20;
+          if (S != 0.0) {
+            const uint64_t b = (uint64_t)__double_as_longlong(S);
+            const int be = (int)((b >> 52) & 0x7FF);
+            const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (be ? (1ull << 52) : 0ull);
+            qs = (be ? be : 1) - 1075 + __builtin_ctzll(m);
           }
-          if (lane == 0) sm.mean = S / (double)N;
+          const int q = min(em, qs);
+          const double sa = seg_a[sg] * slack;
+          if (sa < ldexp(1.0, em + 53) && (fabs(S) * slack + sa) < ldexp(1.0, q + 53)) {
+            S += seg_s[sg];
+            continue;
+          }
+          const int e1 = min(N, (sg + 1) * G);
+          for (int p0 = sg * G; p0 < e1; p0 += NW * PW) {
+            { // every wave: its piece's exact prefix sums
+              const int i0 = p0 + wave * PW + 4 * lane;
+              float xv[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) xv[k] = i0 + k < e1 ? xr[i0 + k] : 0.f;
+              double l[4];
+              int eb = 1 << 20;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                l[k] = (k ? l[k - 1] : 0.0) + (double)xv[k];
+                const uint32_t e = (__float_as_uint(xv[k]) >> 23) & 0xFFu;
+                if (xv[k] != 0.0f) eb = min(eb, e == 0 ? -149 : (int)e - 150);
+              }
+              const double ex = wave_scan_f64(l[3]) - l[3]; // exclusive (exact: a sub-range sum)
+              eb = wave_min_i32(eb);
+              double2 *const qd = reinterpret_cast<double2 *>(qb + wave * PW) + 2 * lane;
+              qd[0] = make_double2(ex + l[0], ex + l[1]);
+              qd[1] = make_double2(ex + l[2], ex + l[3]);
+              if (lane == 0) qok[wave] = eb >= (1 << 19) || sa < ldexp(1.0, eb + 53);
+            }
+            __syncthreads();
+            if (wave == 0) {
+              for (int pi = 0; pi < NW; ++pi) {
+                const int ps = p0 + pi * PW;
+                if (ps >= e1) break;
+                const int nv = min(PW, e1 - ps);
+                if (qok[pi]) {
+                  const double2 *const q2 = reinterpret_cast<const double2 *>(qb + pi * PW) + 2 * lane;
+                  const double2 qa = q2[0], qc = q2[1];
+                  const double qv[4] = {qa.x, qa.y, qc.x, qc.y};
+                  double base = 0.0;
+                  int j0 = -1;
+                  while (true) {
+                    double sv[4];
+                    uint64_t m[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                      const double pj = qv[k] - base; // exact
+                      const double s = S + pj;
+                      const double bq = s - S, aq = s - bq; // TwoSum: s + (da + db) = S + pj
+                      const double da = S - aq, db = pj - bq;
+                      const int j = 4 * lane + k;
+                      sv[k] = s;
+                      m[k] = __ballot(j > j0 && j < nv && da + db != 0.0);
+                    }
+                    const uint64_t any = m[0] | m[1] | m[2] | m[3];
+                    if (any == 0) {
+                      const int jl = nv - 1;
+                      S = readlane_f64(sel4(sv, jl & 3), jl >> 2);
+                      break;
+                    }
+                    const int L0 = __builtin_ctzll(any);
+                    const int k = (m[0] >> L0) & 1 ? 0 : (m[1] >> L0) & 1 ? 1 : (m[2] >> L0) & 1 ? 2 : 3;
+                    S = readlane_f64(sel4(sv, k), L0);
+                    base = readlane_f64(sel4(qv, k), L0);
+                    j0 = 4 * L0 + k;
+                    if (j0 == nv - 1) break;
+                  }
+                } else { // sample by sample: 64 coalesced loads, then lane by lane in order
+                  for (int c = 0; c < nv; c += 64) {
+                    const float v = c + lane < nv ? xr[ps + c + lane] : 0.f;
+                    const int nj = min(64, nv - c);
+                    for (int j = 0; j < nj; ++j) S += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+                  }
+                }
+              }
+              if (lane == 0) sm.phase = S; // (the state after these pieces, to every wave)
+            }
+            __syncthreads();
+            S = sm.phase; // (its next write follows the next round's barrier)
+          }
         }
+        if (tid == 0) sm.mean = S / (double)N;
       }
       __syncthreads();
       XSTAMP(14);
@@ -436,140 +565,119 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
         double acc = 0.0;
         double bm = 0.0;                     // > best = 0 like the reference's first test
         int bi = -1;
-        double *const tp = sm.sc, *const tra = sm.sc + SCH, *const trb = sm.sc + 2 * SCH;
         if (tid < 3) { // P(0), Ra(0), Rb(0) (modem.js:292-298), one sum per lane
           for (int m = 0; m < half; ++m) {
             const double a = xs[m], b = xs[m + half];
             acc += tid == 0 ? a * b : (tid == 1 ? a * a : b * b);
           }
         }
-        // positions [0, P1) before the hull: only the running sums matter, in a pipeline of
-        // half-chunks (HB positions): wave 0's lanes 0-2 add the increments of half h while
-        // waves 1-3 form those of half h + 1 in the other half of the buffer
+        // Positions [0, d_hi] in halves of HB positions, pipelined over two buffers: in step
+        // h, wave 0's lanes 0-2 run the three sequential additions through half h (buffer
+        // h & 1: increments in, the states at each position out when the half holds a
+        // compared position) while each thread of waves 1-3 forms the metrics of its
+        // positions of half h - 1 (the other buffer, states of the step before) and then
+        // overwrites the same slots with the increments of half h + 1 (the same positions:
+        // no other thread reads them), from samples it loaded a step earlier. The chain is
+        // the only sequential work; every other step hides under it.
         constexpr int HB = SCH / 2;
-        const int P1 = (d_lo / HB) * HB;
-        if (P1 > 0) {
-          const int nh = P1 / HB;
-          // increments of half h's positions from samples (a_out, mid, b_in), into buffer h & 1
-          auto put = [&](int h, int k, float a_out_f, float mid_f, float b_in_f) {
-            double *const bp = sm.sc + (h & 1) * 3 * HB;
-            const int d = h * HB + k;
-            double ip = 0.0, ia = 0.0, ib = 0.0;
-            if (d < end) {
-              const double a_out = a_out_f, mid = mid_f, b_in = b_in_f;
-              ip = mid * b_in - a_out * mid;
-              ia = mid * mid - a_out * a_out;
-              ib = b_in * b_in - mid * mid;
-            }
-            bp[k] = ip; bp[HB + k] = ia; bp[2 * HB + k] = ib;
-          };
-          auto ld = [&](int d) { return d < N ? xs[d] : 0.f; };
-          for (int k = tid; k < HB; k += XT) put(0, k, ld(k), ld(k + half), ld(k + 2 * half));
-          // waves 1-3: thread tt forms positions tt, tt + 192, tt + 384 of a half; its samples
-          // for half h + 2 are loaded while half h + 1's increments are formed from registers
-          constexpr int PT = (HB + XT - 65) / (XT - 64);
-          const int tt = tid - 64;
-          float ra[PT], rm[PT], rb[PT];
-          auto load_half = [&](int h) {
-#pragma unroll
-            for (int j = 0; j < PT; ++j) {
-              const int k = tt + (XT - 64) * j, d = h * HB + k;
-              const bool v = k < HB;
-              ra[j] = v ? ld(d) : 0.f; rm[j] = v ? ld(d + half) : 0.f; rb[j] = v ? ld(d + 2 * half) : 0.f;
-            }
-          };
-          if (wave > 0 && nh > 1) load_half(1);
-          __syncthreads();
-          for (int h = 0; h < nh; ++h) {
-            if (wave == 0) {
-              if (lane < 3) {
-                const double2 *const v = reinterpret_cast<const double2 *>(sm.sc + (h & 1) * 3 * HB + lane * HB);
-                // (the next eight pairs are read while these are added: the adds are the chain)
-                double2 t[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) t[j] = v[j];
-                for (int k = 0; k < HB / 2; k += 8) {
-                  double2 u[8];
-                  const int kn = k + 8 < HB / 2 ? k + 8 : k;
-#pragma unroll
-                  for (int j = 0; j < 8; ++j) u[j] = v[kn + j];
-#pragma unroll
-                  for (int j = 0; j < 8; ++j) { acc += t[j].x; acc += t[j].y; }
-#pragma unroll
-                  for (int j = 0; j < 8; ++j) t[j] = u[j];
-                }
-              }
-            } else {
-              if (h + 1 < nh) {
-#pragma unroll
-                for (int j = 0; j < PT; ++j) {
-                  const int k = tt + (XT - 64) * j;
-                  if (k < HB) put(h + 1, k, ra[j], rm[j], rb[j]);
-                }
-              }
-              if (h + 2 < nh) load_half(h + 2);
-            }
-            __syncthreads();
+        const int nh = d_hi / HB + 1;  // halves covering [0, d_hi]
+        const int h_keep = d_lo / HB;  // the first half holding a compared position
+        auto put = [&](int h, int k, float a_out_f, float mid_f, float b_in_f) {
+          double *const bp = sm.sc + (h & 1) * 3 * HB;
+          const int d = h * HB + k;
+          double ip = 0.0, ia = 0.0, ib = 0.0;
+          if (d < end) { // zero past `end`: adding +0.0 changes no state at or before `end`
+            const double a_out = a_out_f, mid = mid_f, b_in = b_in_f;
+            ip = mid * b_in - a_out * mid;
+            ia = mid * mid - a_out * a_out;
+            ib = b_in * b_in - mid * mid;
           }
-        }
-        for (int c0 = P1; c0 <= d_hi; c0 += SCH) {
-          const int n = min(SCH, d_hi + 1 - c0);
-          const int ns = n + 2 * half; // samples [c0, c0 + n + 512) <= N
-          for (int i = tid; i < ns; i += XT) sm.chunk[i] = c0 + i < N ? xs[c0 + i] : 0.f;
-          __syncthreads();
-          for (int k = tid; k < n; k += XT) {
-            double ip = 0.0, ia = 0.0, ib = 0.0;
-            if (c0 + k < end) {
-              const double a_out = sm.chunk[k], mid = sm.chunk[k + half], b_in = sm.chunk[k + 2 * half];
-              ip = mid * b_in - a_out * mid;
-              ia = mid * mid - a_out * a_out;
-              ib = b_in * b_in - mid * mid;
-            }
-            tp[k] = ip; tra[k] = ia; trb[k] = ib;
+          bp[k] = ip; bp[HB + k] = ia; bp[2 * HB + k] = ib;
+        };
+        auto ld = [&](int d) { return d < N ? xs[d] : 0.f; };
+        for (int k = tid; k < HB; k += XT) put(0, k, ld(k), ld(k + half), ld(k + 2 * half));
+        // waves 1-3: thread tt owns positions tt, tt + 192, tt + 384 of every half
+        constexpr int PT = (HB + XT - 65) / (XT - 64);
+        const int tt = tid - 64;
+        float ra[PT], rm[PT], rb[PT];
+        auto load_half = [&](int h) {
+#pragma unroll
+          for (int j = 0; j < PT; ++j) {
+            const int k = tt + (XT - 64) * j, d = h * HB + k;
+            const bool v = k < HB;
+            ra[j] = v ? ld(d) : 0.f; rm[j] = v ? ld(d + half) : 0.f; rb[j] = v ? ld(d + 2 * half) : 0.f;
           }
-          __syncthreads();
-          const bool keep = c0 + n > d_lo; // some position of this chunk is compared
-          if (tid < 3) {
-            double2 *const v = reinterpret_cast<double2 *>(sm.sc + tid * SCH);
-            int k = 0;
-            if (!keep) { // states not needed: the running sum only
-              for (; k + 8 <= n; k += 8) {
-                double2 t[4];
+        };
+        if (wave > 0 && nh > 1) load_half(1);
+        __syncthreads();
+        for (int h = 0; h <= nh; ++h) {
+          if (wave == 0) {
+            if (h < nh && lane < 3) {
+              double2 *const v = reinterpret_cast<double2 *>(sm.sc + (h & 1) * 3 * HB + lane * HB);
+              // A rotating pipeline: pair k + Q is requested as pair k is added, so Q loads
+              // are always in flight and each add waits only for its own (the adds are the
+              // chain; reads past the half land in the next lane's half or other LDS fields
+              // and are never used)
+              constexpr int Q = AMOD_SC_CQ;
+              double2 t[Q];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) t[j] = v[(k >> 1) + j];
+              for (int j = 0; j < Q; ++j) t[j] = v[j];
+              if (h < h_keep) { // states not needed: the running sums only
+                for (int k = 0; k < HB / 2; k += Q) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) { acc += t[j].x; acc += t[j].y; }
-              }
-            } else {
-              for (; k + 8 <= n; k += 8) {
-                double2 t[4];
+                  for (int j = 0; j < Q; ++j) {
+                    const double2 c = t[j];
+                    t[j] = v[k + Q + j];
+                    acc += c.x;
+                    acc += c.y;
+                  }
+                }
+              } else {
+                for (int k = 0; k < HB / 2; k += Q) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) t[j] = v[(k >> 1) + j];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) { // state at the position, then its update
-                  const double s0 = acc;
-                  acc += t[j].x; // zero past `end`: adding +0.0 changes nothing
-                  const double s1 = acc;
-                  acc += t[j].y;
-                  v[(k >> 1) + j] = make_double2(s0, s1);
+                  for (int j = 0; j < Q; ++j) { // the state at each position, then its update
+                    const double2 c = t[j];
+                    t[j] = v[k + Q + j];
+                    const double s0 = acc;
+                    acc += c.x;
+                    const double s1 = acc;
+                    acc += c.y;
+                    v[k + j] = make_double2(s0, s1);
+                  }
                 }
               }
             }
-            double *const vs = sm.sc + tid * SCH;
-            for (; k < n; ++k) {
-              const double t = vs[k];
-              vs[k] = acc;
-              acc += t;
+          } else {
+            const int hm = h - 1;
+            if (hm >= h_keep) { // metrics of half h - 1, first strict maximum per thread
+              const double *const bp = sm.sc + (hm & 1) * 3 * HB;
+#pragma unroll
+              for (int j = 0; j < PT; ++j) {
+                const int k = tt + (XT - 64) * j, d = hm * HB + k;
+                if (k < HB && d >= d_lo && d <= d_hi) {
+                  const double pp = bp[k], a = bp[HB + k], b = bp[2 * HB + k];
+#ifndef AMOD_KO_METRIC
+                  // (the division only where the metric may beat bm: with q = fl(pp pp) and
+                  // r = fl(a b), q < fl(r bm) (1 - 2^-40) means q / r < bm, so fl(q / r) <= bm)
+                  if (a > 0.01 && b > 0.01) {
+                    const double q = pp * pp, r = a * b;
+                    if (!(q < (r * bm) * (1.0 - 0x1p-40))) {
+                      const double metric = q / r;
+                      if (metric > bm) { bm = metric; bi = d; }
+                    }
+                  }
+#endif
+                }
+              }
             }
-          }
-          __syncthreads();
-          for (int k = tid; keep && k < n; k += XT) {
-            if (c0 + k < d_lo) continue;
-            const double pp = tp[k], a = tra[k], b = trb[k];
-            if (a > 0.01 && b > 0.01) {
-              const double metric = (pp * pp) / (a * b);
-              if (metric > bm) { bm = metric; bi = c0 + k; }
+            if (h + 1 < nh) {
+#pragma unroll
+              for (int j = 0; j < PT; ++j) {
+                const int k = tt + (XT - 64) * j;
+                if (k < HB) put(h + 1, k, ra[j], rm[j], rb[j]);
+              }
             }
+            if (h + 2 < nh) load_half(h + 2);
           }
           __syncthreads();
         }

@@ -27,6 +27,10 @@
 // error bound; a frame with a decision inside its band is listed
 // for k_decode_exact (IEEE double, reference operation order).
 #include "amodem_internal.h"
+// cache policy of the stream pass's sample loads (experiments: 2 = nt)
+#ifndef AMOD_STREAM_CPOL
+#define AMOD_STREAM_CPOL 0
+#endif
 
 #include <algorithm>
 #include <type_traits>
@@ -680,7 +684,7 @@ template <bool SCAN_ONLY, bool DBG> __device__ __forceinline__ void detect() {
       float sacc = 0.f;
       float mn = INFINITY, mxv = -INFINITY;
       auto LD = [&](int q) -> float4 {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * q, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * q, AMOD_STREAM_CPOL);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
       };
       // per-sample work on packed pairs (v_pk_add/mul/fma_f32): u = x - x[0] of a chunk is

@@ -342,7 +342,13 @@ static void progress_call_js(napi_env env, napi_value cb, void *context, void *d
       napi_get_reference_value(env, pc->pay_ref, &argv[2]) != napi_ok ||
       napi_create_double(env, pc->stride, &argv[3]) != napi_ok || napi_get_undefined(env, &undef) != napi_ok)
     return;
-  napi_call_function(env, undef, cb, 4, argv, NULL);
+  /* modem.js's onFrames keeps any error of its own for the promise; should a callback
+   * throw anyway, the exception is cleared here (a threadsafe-function call has no caller
+   * to propagate it to, and left pending it would end the process) */
+  if (napi_call_function(env, undef, cb, 4, argv, NULL) == napi_pending_exception) {
+    napi_value exc;
+    napi_get_and_clear_last_exception(env, &exc);
+  }
 }
 
 static void progress_finalize(napi_env env, void *data, void *hint) {

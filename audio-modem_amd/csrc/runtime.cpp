@@ -1099,8 +1099,6 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
   HIP_TRY(ctx->h_len.ensure(sizeof(int32_t) * (size_t)nframes));
   HIP_TRY(ctx->h_res.ensure(sizeof(amod_result) * (size_t)nframes));
   HIP_TRY(ctx->h_payload.ensure((size_t)payload_stride * (size_t)nframes));
-  HIP_TRY(ctx->pin_res.ensure(sizeof(amod_result) * (size_t)nframes));
-  HIP_TRY(ctx->pin_payload.ensure((size_t)payload_stride * (size_t)nframes));
   hipStream_t s = ctx->stream;
   if (!ctx->up) HIP_TRY(hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking));
   HIP_TRY(hipMemcpyAsync(ctx->h_off.p, offsets, sizeof(int64_t) * nframes, hipMemcpyHostToDevice, s));
@@ -1138,6 +1136,33 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
       return rc;
     }
   }
+  if (!progress && (npiece <= 1 || !mono)) {
+    // one launch and nobody to tell about prefixes: the samples go up, one decode, the
+    // records and payload rows straight back into the caller's buffers (no helper thread,
+    // no pinned mirrors)
+    for (int64_t p = 0; p < npiece; ++p) {
+      const int64_t lo = p * piece, n = std::min(piece, nsamples - lo);
+      HIP_TRY(hipMemcpyAsync((float *)ctx->h_samples.p + lo, samples + lo, sizeof(float) * n, hipMemcpyHostToDevice,
+                             ctx->up));
+    }
+    HIP_TRY(hipEventRecord(ctx->up_ev[0], ctx->up));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->up_ev[0], 0));
+    const int rc = decode_impl(ctx, cfg, mode, (const float *)ctx->h_samples.p, (const int64_t *)ctx->h_off.p,
+                               (const int32_t *)ctx->h_len.p, nframes, (amod_result *)ctx->h_res.p,
+                               (uint8_t *)ctx->h_payload.p, payload_stride, options, s, nullptr, call_max);
+    if (rc) {
+      (void)hipStreamSynchronize(ctx->up);
+      (void)hipStreamSynchronize(s);
+      return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(results, ctx->h_res.p, sizeof(amod_result) * (size_t)nframes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(payload, ctx->h_payload.p, (size_t)payload_stride * (size_t)nframes,
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return AMOD_SUCCESS;
+  }
+  HIP_TRY(ctx->pin_res.ensure(sizeof(amod_result) * (size_t)nframes));
+  HIP_TRY(ctx->pin_payload.ensure((size_t)payload_stride * (size_t)nframes));
   // every launch's frames [a, b) come back on the context stream right after it (DMA into
   // the pinned mirrors); a helper thread waits for each piece's copy, moves it into the
   // caller's buffers and reports it, so the calling thread keeps staging the uploads (the
@@ -1183,10 +1208,16 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
     deliverer.join();
     return berr;
   };
-  struct Joiner { // every early return (HIP_TRY) stops the helper first
+  struct Joiner { // every return stops the helper first, then waits out the streams (an
+                  // upload or a copy into the pinned mirrors may still be in flight after an
+                  // early return through HIP_TRY; the next call reuses those buffers)
     std::function<void()> f;
     ~Joiner() { f(); }
-  } joiner{[&] { (void)finish(false); }};
+  } joiner{[&] {
+    (void)finish(false);
+    (void)hipStreamSynchronize(ctx->up);
+    (void)hipStreamSynchronize(s);
+  }};
   int32_t a = 0; // the first frame not yet enqueued
   for (int64_t p = 0; p <= npiece; ++p) {
     int64_t covered = nsamples;
@@ -1232,13 +1263,8 @@ int decode_host_impl(amod_ctx *ctx, const amod_cfg *cfg, int32_t mode, const flo
         bcv.notify_one();
       }
     }
-    if (rc || e != hipSuccess) {
-      (void)finish(false);
-      (void)hipStreamSynchronize(ctx->up);
-      (void)hipStreamSynchronize(s);
-      if (rc) return rc;
-      HIP_TRY(e);
-    }
+    if (rc) return rc; // (the joiner stops the helper and drains both streams)
+    HIP_TRY(e);
     a = b;
   }
   HIP_TRY(finish(true));

@@ -367,20 +367,26 @@ function decodeBatch(samples, frameOffsets, frameLens, modName, rep, opts) {
   const n = lens.length, viaLegacy = mode === MODE_RECEIVED;
   // one device: the frames of each decoded 64 MB piece are formatted as soon as they are
   // back (onFrames, amod_decode_host_progress), while the library uploads and decodes the
-  // rest; what is left when the promise settles is formatted then
+  // rest; what is left when the promise settles is formatted then. An error thrown while
+  // formatting or by onProgress (which runs from the library's progress callback, where no
+  // caller could catch it) is kept, and the promise rejects with it.
   const res = new Array(n);
-  let done = 0;
+  let done = 0, failed = null;
   const onFrames = (upto, results, payload, stride) => {
-    if (upto > done) {
+    if (failed !== null || upto <= done) return;
+    try {
       formatBatch(results, payload, stride, upto, viaLegacy, share, res, done);
       done = upto;
       if (o.onProgress) o.onProgress(done, res);
+    } catch (e) {
+      failed = e;
     }
   };
   return native.decodeAsync(asFloat32(samples), offs, lens, cfg, mode, o.forceExact ? 1 : 0, o.device | 0,
     Math.max(1, o.devices | 0), onFrames)
     .then((out) => {
       onFrames(n, out.results, out.payload, out.stride);
+      if (failed !== null) throw failed;
       return res;
     });
 }

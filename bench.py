@@ -217,12 +217,15 @@ class Workload:
         # alone building every rank's batch)
         torch, amodem, L = env.torch, env.amodem, env.L
         self.env, self.conf, self.snr = env, conf, snr
-        C3, C4, C5 = conf == "c3", conf == "c4", conf == "c5"
-        self.chunk = C4
-        self.cfg = amodem.preset("acoustic", "BPSK", 3) if C5 else \
+        C3, C4, C5, C5C = conf == "c3", conf == "c4", conf == "c5", conf == "c5c"
+        # c5c: C5's acoustic BPSK rep3 as 256 B data-chunk windows (decodeChunkFrame) in
+        # heavy AWGN, where combining the repeats matters (soft_chunk_leg)
+        self.chunk = C4 or C5C
+        self.noisy = C5 or C5C
+        self.cfg = amodem.preset("acoustic", "BPSK", 3) if (C5 or C5C) else \
             amodem.preset("standard", "QAM16" if C3 else "QPSK", 1)
-        self.mod = "QAM16" if C3 else ("BPSK" if C5 else "QPSK")
-        self.preset = "acoustic" if C5 else "standard"
+        self.mod = "QAM16" if C3 else ("BPSK" if (C5 or C5C) else "QPSK")
+        self.preset = "acoustic" if (C5 or C5C) else "standard"
         F = frames if frames > 0 else (100000 if C3 else (32000 if C4 else 10000))
         self.F = F
         rank = env.rank if rank is None else rank
@@ -230,12 +233,14 @@ class Workload:
         dev = env.dev if device is None else torch.device("cuda", self.local)
         self.dev = dev
         self.dm = amodem.Demodulator(self.local)
-        if C4:
+        if self.chunk:
             # the file's chunks this rank owns: chunk seq = rank * F + i, bytes from xorshift32
+            cb = CHUNK if C4 else PAYLOAD_C5
             pre, post = amodem.tx_silence(self.cfg, L.TX_CHUNK)
-            self.win = amodem.estimate_frame_samples(CHUNK + 11, "QPSK", 1)  # the receiver's window (app.js:853)
+            # the receiver's window (app.js:853: estimateFrameSamples(chunkSize + 11))
+            self.win = int(env.lib.amod_estimate_frame_samples(C.byref(self.cfg), cb + 11))
             spf = pre + self.win + post
-            pkts = [amodem.packet_chunk(amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), CHUNK), rank * F + i)
+            pkts = [amodem.packet_chunk(amodem.synth_payload(0x9E3779B9 ^ (rank * F + i), cb), rank * F + i)
                     for i in range(F)]
             pl = np.array([len(p) for p in pkts], np.int32)
             po = np.concatenate([[0], np.cumsum(pl)[:-1]]).astype(np.int64)
@@ -253,11 +258,12 @@ class Workload:
         self.nsamples = int(self.lens.sum())
         # what one step decodes: whole legacy frames, or the C4 windows (pre1 .. end of the
         # estimated frame, as StreamingReceiver cuts them) in decodeChunkFrame mode
-        self.mode = L.MODE_CHUNK if C4 else L.MODE_RECEIVED
-        self.doffs = self.offs + pre if C4 else self.offs
-        self.dlens = np.full(F, self.win, np.int32) if C4 else self.lens
+        self.mode = L.MODE_CHUNK if self.chunk else L.MODE_RECEIVED
+        self.doffs = self.offs + pre if self.chunk else self.offs
+        self.dlens = np.full(F, self.win, np.int32) if self.chunk else self.lens
         self.ndecoded = int(self.dlens.sum())
-        self.payload_bytes = CHUNK if C4 else (PAYLOAD_C5 if C5 else PAYLOAD)
+        self.payload_bytes = CHUNK if C4 else (PAYLOAD_C5 if (C5 or C5C) else PAYLOAD)
+        self.packets = (pk, po, pl) if C5C else None  # (the soft leg counts bit errors against them)
         self.xs = torch.empty(self.nsamples + 16, dtype=torch.float32, device=dev)
         d_pk = torch.from_numpy(pk).to(dev)
         d_po, d_pl = torch.from_numpy(po).to(dev), torch.from_numpy(pl).to(dev)
@@ -289,12 +295,12 @@ class Workload:
         self.tx_ms = sum(tx_ms) / len(tx_ms)
         self.tx_bytes = 4.0 * self.nsamples + float(pl.sum())  # samples written + packet bytes read
         self.sigma = None
-        if C5:  # AWGN on the GPU, seeded per rank; power from the first frame's active samples
+        if self.noisy:  # AWGN on the GPU, seeded per rank; power from the first frame's active samples
             x0 = self.xs[: int(self.lens[0])]
             act = x0[x0 != 0]
             self.sigma = float(torch.sqrt((act.double() ** 2).mean() / 10 ** (snr / 10)).item())
             gen = torch.Generator(device=dev)
-            gen.manual_seed(0xC5 + rank)
+            gen.manual_seed((0xC5C if C5C else 0xC5) + rank)
             self.xs[: self.nsamples] += torch.randn(self.nsamples, generator=gen, device=dev,
                                                     dtype=torch.float32) * self.sigma
             torch.cuda.synchronize(dev)
@@ -354,9 +360,12 @@ class Workload:
         self.env.torch.cuda.empty_cache()
 
     def name(self):
-        return {"c2": "C2", "c3": "C3", "c4": "C4", "c5": "C5"}[self.conf]
+        return {"c2": "C2", "c3": "C3", "c4": "C4", "c5": "C5", "c5c": "C5c"}[self.conf]
 
     def workload_text(self):
+        if self.conf == "c5c":
+            return (f"C5 as chunks: {self.F // 1000}k acoustic BPSK rep3 256 B data-chunk windows per GPU + AWGN at "
+                    f"{self.snr:.2f} dB (decodeChunkFrame)")
         if self.chunk:
             return (f"C4: {self.F // 1000}k QPSK 2 KB data-chunk windows per GPU (decodeChunkFrame; value counts the "
                     f"window samples decoded, 25,344 of each 28,431-sample frame)")
@@ -447,7 +456,7 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
     pay = wl.d_pay.view(wl.F, wl.stride).cpu().numpy()
     for i in range(0, wl.F, max(1, wl.F // 64)):
         r = amodem.to_reference(rec[i], pay[i].tobytes(), not wl.chunk)
-        if wl.conf == "c5" and not r.get("crcValid"):
+        if wl.noisy and not r.get("crcValid"):
             continue
         want = amodem.synth_payload(0x9E3779B9 ^ (env.rank * wl.F + i), wl.payload_bytes)
         assert r.get("data") == want, (wl.conf, i, r.get("error"))
@@ -551,7 +560,7 @@ def gather_leg(env: Env, wl: Workload, reps=3):
     rec = np.frombuffer(g_res.cpu().numpy().tobytes(), amodem.RESULT_DTYPE)
     pay = g_pay.cpu().numpy()
     wl.gathered = rec  # (the group leg compares its records with these)
-    noisy = wl.conf == "c5"
+    noisy = wl.noisy
     ok = len(rec) == world * F and (noisy or bool(((rec["status"] == 0) & (rec["crc_valid"] == 1)).all()))
     if wl.chunk:
         ok = ok and bool((rec["seq_num"] == np.arange(world * F)).all())
@@ -666,19 +675,41 @@ def group_leg(env: Env, conf: str, args, snr: float, gathered):
     return out
 
 
-def soft_leg(env: Env, wl: Workload, steps: int, warmup: int):
+def soft_leg(env: Env, wl: Workload, steps: int, warmup: int, oracle: bool = False):
     """C5's opt-in soft combining of the repeated bits (AMOD_OPT_SOFT_COMBINE, NOT reference
     behaviour: BASELINE C5 names it; k_demod's soft instance, groups whose soft sum lies
     inside its error bound routed to the exact kernel) against the reference's hard
     majority vote on the same resident batch: K steps each on one context (no pipelining),
-    per-kernel times, CRC-valid frames and frames the exact kernel decoded."""
+    per-kernel times, CRC-valid frames and frames the exact kernel decoded; for chunk
+    windows (wl.packets) also the frames whose bytes equal the synthetic payload and the
+    post-vote bit errors against the transmitted packets. oracle: the hard vote's records
+    (the reference's behaviour) against the C oracle over the whole batch."""
     torch, lib, L = env.torch, env.lib, env.L
     sync = lambda: torch.cuda.synchronize(env.dev)  # noqa: E731
     out = {"what": "AMOD_OPT_SOFT_COMBINE (|H|^2-weighted soft vote, k_demod soft instance; not reference "
-                   "behaviour) vs the hard majority vote, K steps each on one context", "frames": wl.F}
+                   "behaviour) vs the hard majority vote, K steps each (received mode: through the two-context "
+                   "pipe as the primary measurement, kernel times from K steps on one context)", "frames": wl.F,
+           "snr_db": wl.snr}
+    ref = None
+    if wl.packets is not None:
+        pk, po, pl = wl.packets
+        ref = np.zeros((wl.F, int(pl.max())), np.uint8)
+        for i in range(wl.F):
+            ref[i, : pl[i]] = pk[po[i]: po[i] + pl[i]]
+    # received mode: consecutive batches through the library's two-context pipe, as the
+    # primary measurement (measure()); the per-kernel times from K steps on one context
+    pipe = not wl.chunk and os.environ.get("AMOD_BENCH_PIPELINE", "1") != "0"
+    if pipe and getattr(wl, "pipe", None) is None:
+        wl.enable_pipeline()
     for name, opt in (("hard", 0), ("soft", L.OPT_SOFT_COMBINE), ("hard_again", 0)):
         def step(opt=opt):
             wl.step(options=opt)
+
+        def step_p(opt=opt):
+            k, wl.pi = wl.pi, wl.pi ^ 1
+            res, pay = (wl.d_res, wl.d_pay) if k == 0 else (wl.d_res2, wl.d_pay2)
+            wl.pipe.decode_device(wl.cfg, wl.mode, wl.xs.data_ptr(), wl.d_doff.data_ptr(), wl.d_dlen.data_ptr(),
+                                  wl.F, res.data_ptr(), pay.data_ptr(), wl.stride, options=opt)
         warm_up(step, sync, warmup)
         lib.amod_set_profiling(wl.dm.ctx, 1)
         sync()
@@ -686,17 +717,70 @@ def soft_leg(env: Env, wl: Workload, steps: int, warmup: int):
         for _ in range(steps):
             step()
         sync()
-        dt = (time.perf_counter() - t0) / steps
+        dt1 = (time.perf_counter() - t0) / steps
         kms, kn = (C.c_double * L.STAGE_COUNT)(), C.c_int64()
         lib.amod_kernel_stages(wl.dm.ctx, kms, L.STAGE_COUNT, C.byref(kn))
         lib.amod_set_profiling(wl.dm.ctx, 0)
         st = [kms[i] / max(1, kn.value) for i in range(L.STAGE_COUNT)]
+        dt = dt1
+        if pipe:
+            warm_up(step_p, sync, warmup, min_s=0.3)
+            wl.pipeline_flush()
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step_p()
+            wl.pipeline_flush()
+            sync()
+            dt = (time.perf_counter() - t0) / steps
         rec = wl.records()
-        out[name] = {"ms_per_step": dt * 1e3, "k_detect_ms": st[L.STAGE_DETECT], "k_demod_ms": st[L.STAGE_DEMOD],
-                     "frames_crc_valid": int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum()),
-                     "frames_exact": int(((rec["flags"] & L.FLAG_EXACT) != 0).sum())}
+        o = {"ms_per_step": dt * 1e3, "one_context_ms_per_step": dt1 * 1e3,
+             "k_detect_ms": st[L.STAGE_DETECT], "k_demod_ms": st[L.STAGE_DEMOD],
+             "exact_chain_ms": st[L.STAGE_AUX] + st[L.STAGE_EXACT_B],
+             "frames_crc_valid": int(((rec["status"] == 0) & (rec["crc_valid"] == 1)).sum()),
+             "frames_exact": int(((rec["flags"] & L.FLAG_EXACT) != 0).sum())}
+        if ref is not None:
+            pay = wl.d_pay.view(wl.F, wl.stride).cpu().numpy()
+            n = np.minimum(rec["payload_valid"].astype(np.int64), wl.packets[2].astype(np.int64))
+            cols = np.arange(ref.shape[1])[None, :]
+            diff = np.where(cols < n[:, None], pay[:, : ref.shape[1]] ^ ref, 0).astype(np.uint8)
+            o["bit_errors"] = int(np.unpackbits(diff).sum())
+            o["bits_compared"] = int(n.sum() * 8)
+            o["frames_payload_ok"] = int(sum(
+                1 for i in range(wl.F) if rec["status"][i] == 0 and rec["crc_valid"][i] == 1 and
+                amodem_payload(env, rec[i], pay[i]) == wl_payload(wl, env, i)))
+        out[name] = o
+        if name == "hard" and oracle and env.world == 1:
+            chk = oracle_check(wl, wl.xs[: wl.nsamples].cpu().numpy(), rec)
+            out["oracle_agree"] = chk["oracle_agree"]
+            out["oracle_ok"] = chk["agree"] == wl.F
+            if chk["agree"] != wl.F:
+                print(f"{wl.name()} {wl.snr} dB: hard-vote records differ from the oracle on "
+                      f"{wl.F - chk['agree']} frames", file=sys.stderr)
     hard_ms = min(out["hard"]["ms_per_step"], out["hard_again"]["ms_per_step"])
     out["soft_over_hard_step"] = out["soft"]["ms_per_step"] / hard_ms
+    return out
+
+
+def amodem_payload(env, rec, slot):
+    return env.amodem.to_reference(rec, slot.tobytes(), False).get("data")
+
+
+def wl_payload(wl, env, i):
+    return env.amodem.synth_payload(0x9E3779B9 ^ (env.rank * wl.F + i), wl.payload_bytes)
+
+
+def soft_chunk_leg(env: Env, args, div=1.5):
+    """BASELINE C5's noisy-channel mode where it matters: acoustic BPSK rep3 256 B chunk
+    windows (decodeChunkFrame) with AWGN at signal/noise power `div` (1.5: 1.76 dB; where
+    tests/test_gpu_soft_combine.py shows the soft vote gaining), soft vs hard."""
+    wl = Workload(env, "c5c", 0, 10 * np.log10(div))
+    try:
+        out = soft_leg(env, wl, args.steps, args.warmup, oracle=True)
+    finally:
+        wl.close()
+    out["noise_divisor"] = div
+    out["workload"] = wl.workload_text()
     return out
 
 
@@ -1026,10 +1110,10 @@ def _soft_summary(s):
     out = {}
     for name in ("hard", "soft"):
         if isinstance(s.get(name), dict):
-            out[name] = _pick(s[name], ["ms_per_step", "k_demod_ms", "frames_crc_valid", "frames_exact",
-                                        "frames_payload_ok", "bit_errors", "oracle_agree"])
-    for k in ("soft_over_hard_step", "frames", "snr_db", "noise_divisor", "oracle_agree", "ms_per_step",
-              "frames_listed", "listed_ms"):
+            out[name] = _pick(s[name], ["ms_per_step", "one_context_ms_per_step", "k_demod_ms", "exact_chain_ms",
+                                        "frames_crc_valid",
+                                        "frames_exact", "frames_payload_ok", "bit_errors", "bits_compared"])
+    for k in ("soft_over_hard_step", "frames", "snr_db", "noise_divisor", "oracle_agree", "oracle_ok"):
         if k in s:
             out[k] = _g(s[k]) if not isinstance(s[k], str) else s[k][:80]
     return out
@@ -1288,8 +1372,10 @@ def main():
         # the preambles (it fails at <= 6 dB)
         progress("c5 at 7 dB: soft combining vs the hard vote")
         wl7 = Workload(env, "c5", 0, 7.0)
-        extra["c5_soft_7db"] = soft_leg(env, wl7, args.steps, args.warmup)
+        extra["c5_soft_7db"] = soft_leg(env, wl7, args.steps, args.warmup, oracle=True)
         wl7.close()
+        progress("c5 chunk windows at 1.76 dB: soft combining vs the hard vote")
+        extra["c5_soft_chunk"] = soft_chunk_leg(env, args)
     if env.rank == 0:
         out = {"metric": METRIC}
         out.update({k: prim[k] for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step")})

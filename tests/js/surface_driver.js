@@ -60,6 +60,20 @@ async function main() {
           r = { results: r, ownData: own, progress, prefixes_final };
           break;
         }
+        case 'decode_batch_throw': {
+          // onProgress throws on its first call: the promise rejects with that error (the
+          // process keeps running), and the next decode on the same addon works
+          let calls = 0, rejected = null;
+          try {
+            await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep,
+              { onProgress: () => { calls++; throw new Error('onProgress boom'); } });
+          } catch (e) {
+            rejected = String(e && e.message);
+          }
+          const again = await M.decodeBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep);
+          r = { rejected, calls, again: again.length };
+          break;
+        }
         case 'decode_resident': {
           // uploadBatch once, decodeBatch(DeviceBatch) twice: both from HBM
           const b = M.uploadBatch(f32(j.file), j.offsets, j.lengths, j.mod, j.rep, { devices: j.devices });

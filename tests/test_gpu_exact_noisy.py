@@ -125,6 +125,61 @@ def test_exact_mean_is_the_sequential_sum():
     assert d.mean == seq
 
 
+def _mean_frames(n, seed):
+    """Frames whose sequential mean rounds in many places: a large DC offset (the running
+    sum climbs through many binades, rounding at the crossings), tiny samples far below
+    its ulp, and samples of random exponents (64-sample blocks whose own prefix sums are
+    not exact, summed sample by sample)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(4):
+        x = rng.standard_normal(n).astype(np.float64) * 0.3
+        if k == 0:
+            x += 3.7
+        elif k == 1:
+            x += -0.9
+            x[rng.integers(0, n, 200)] = rng.choice([1e-30, -3e-12, 7e-9, -2e-20], 200)
+        elif k == 2:
+            x = np.sign(x) * np.exp2(rng.uniform(-45, 4, n))
+        else:
+            x = np.cumsum(x) * 1e-2  # slow drift: long runs in one binade, both signs
+        out.append(x.astype(np.float32))
+    return out
+
+
+@pytest.mark.parametrize("n", [4096 + 77, 111300])
+def test_exact_mean_rounding_events(n):
+    """The mean's failing segments walk 64-sample blocks: every lane's fl(S + P_j), the
+    first rounded one by TwoSum, the block continued from it. Bit-equal to numpy's
+    sequential cumsum on frames built to round often (and to not be certifiable)."""
+    import torch
+    cfg = amodem.preset("acoustic", "BPSK", 3)
+    frs = _mean_frames(n, seed=n)
+    x = np.concatenate(frs + [np.zeros(4, np.float32)])
+    F = len(frs)
+    dev = torch.device("cuda", 0)
+    xs = torch.from_numpy(x).to(dev)
+    off = torch.tensor([i * n for i in range(F)], dtype=torch.int64, device=dev)
+    ln = torch.full((F,), n, dtype=torch.int32, device=dev)
+    stride = amodem.payload_stride(cfg, n)
+    res = torch.zeros(96 * F, dtype=torch.uint8, device=dev)
+    pay = torch.zeros(stride * F, dtype=torch.uint8, device=dev)
+    dsz = L.C.sizeof(L.Debug)
+    dbg = torch.zeros(dsz * F, dtype=torch.uint8, device=dev)
+    dm = amodem.Demodulator(0)
+    dm.reserve(cfg, F, n)
+    torch.cuda.synchronize()
+    dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), off.data_ptr(), ln.data_ptr(), F, res.data_ptr(),
+                     pay.data_ptr(), stride, options=L.OPT_FORCE_EXACT, debug_ptr=dbg.data_ptr())
+    dm.synchronize()
+    raw = dbg.cpu().numpy().tobytes()
+    dm.close()
+    for i, fr in enumerate(frs):
+        seq = np.cumsum(fr.astype(np.float64))[-1] / n
+        d = L.Debug.from_buffer_copy(raw[i * dsz:(i + 1) * dsz])
+        assert d.mean == seq, (i, d.mean, seq, np.sum(fr.astype(np.float64)) / n)
+
+
 @pytest.mark.parametrize("preset,snr_db", [("acoustic", 8), ("acoustic", 9), ("standard", 7)])
 def test_replayed_detection_equals_full_exact_path(preset, snr_db):
     """Detection replay: a frame listed only for detection-stage guards gets its

@@ -110,6 +110,27 @@ def test_host_progress_prefixes_final(monkeypatch):
     dm.close()
 
 
+def test_host_progress_exception_raised(monkeypatch):
+    """A progress callback that raises: the decode still completes, the callback is not
+    called again, and decode_batch re-raises that exception (ctypes alone would print it
+    and return as if nothing failed); the Demodulator decodes normally afterwards."""
+    cfg, x, offs, lens = _batch()
+    monkeypatch.setenv("AMOD_UP_PIECE", "40000")
+    dm = amodem.Demodulator(0)
+    calls = []
+
+    def bad(done, r, p):
+        calls.append(done)
+        raise KeyError("progress boom")
+
+    with pytest.raises(KeyError, match="progress boom"):
+        dm.decode_batch(x, offs, lens, cfg=cfg, progress=bad)
+    assert len(calls) == 1
+    rec, _ = dm.decode_batch(x, offs, lens, cfg=cfg)
+    assert (rec["status"] == 0).all()
+    dm.close()
+
+
 def _assert_same(rec, pay, ref, rpay):
     for n in amodem.RESULT_DTYPE.names:
         if n == "reserved":

@@ -234,6 +234,26 @@ def test_decode_batch_progress_through_js(tmp_path):
 
 
 @pytest.mark.gpu
+def test_decode_batch_progress_throws(tmp_path):
+    """An onProgress that throws (it runs from the library's progress callback, where no
+    caller could catch it) rejects decodeBatch's promise with that error, is not called
+    again, and leaves the addon usable: the next decodeBatch resolves normally."""
+    from oracle import oracle as O
+    sel = [f for f in frames() if f["config"] == "standard" and f["rx"] == "legacy" and f["mod"] == "QPSK"
+           and f["rep"] == 1]
+    xs = [np.ascontiguousarray(O.build_case(f), np.float32) for f in sel]
+    offs = np.cumsum([0] + [len(x) for x in xs[:-1]]).tolist()
+    fn = tmp_path / "batch.f32"
+    np.concatenate(xs).astype(np.float32).tofile(fn)
+    job = {"op": "decode_batch_throw", "config": "standard", "file": str(fn), "offsets": offs,
+           "lengths": [len(x) for x in xs], "mod": "QPSK", "rep": 1}
+    res = run([dict(job, id="t")], tmp_path, env={"AMOD_UP_PIECE": "4096"})
+    got = ok(res, "t")
+    assert got["rejected"] == "onProgress boom" and got["calls"] == 1, got
+    assert got["again"] == len(sel), got
+
+
+@pytest.mark.gpu
 def test_resident_batch_through_js(tmp_path):
     """uploadBatch (amod_group_upload) makes the batch resident on two GPU contexts
     (device 0 twice on the one-GPU box) once; decodeBatch(DeviceBatch) decodes it from
