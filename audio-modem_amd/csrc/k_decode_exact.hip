@@ -115,6 +115,82 @@ __device__ void fft_exact(const float *src, XSmem &sm, const double2 *tw) {
   }
 }
 
+// fft(re, 0) of 512 real samples src[0..511] on one wave (modem.js:6-13, 26-66): the same
+// butterflies as fft_exact with the same operations in the same order, three stages at a
+// time inside each lane's registers, the element-to-lane map changed between the groups
+// by two transposes through the wave's LDS slot `buf` (512 doubles, re then im):
+//   A: e = 8 l + r                         stages half 1, 2, 4   (pairs differ in r)
+//   B: e = (l & 7) | r << 3 | (l >> 3) << 6  stages half 8, 16, 32
+//   C: e = l | r << 6                       stages half 64, 128, 256; bin k = l + 64 r
+// (e: the element index of fft_exact's arrays; the input is bit-reversed, rev9(e)).
+__device__ __forceinline__ void fft_stage3(double (&re)[8], double (&im)[8], const double2 *tw, int s0, int ebase,
+                                           int rshift) {
+  // stages half = 2^s0, 2^(s0+1), 2^(s0+2); slot r's element index: ebase | r << rshift
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int half = 1 << (s0 + q), sb = 1 << q; // the pair differs in slot bit q
+    // (no twiddle load hoisted past a stage: all 36 in flight at once spilled the kernel)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (r & sb) continue;
+      const int a = r, b = r | sb;
+      const int e = ebase | (r << rshift);
+      const double2 w = tw[half - 1 + (e & (half - 1))];
+      const double t_re = w.x * re[b] - w.y * im[b];
+      const double t_im = w.x * im[b] + w.y * re[b];
+      re[b] = re[a] - t_re;
+      im[b] = im[a] - t_im;
+      re[a] = re[a] + t_re;
+      im[a] = im[a] + t_im;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// buf[from(r)] = v[r] for the lane's slots, then v[r] = buf[to(r)]
+template <typename F, typename G>
+__device__ __forceinline__ void wave_permute(double (&v)[8], double *buf, F &&from, G &&to) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) buf[from(r)] = v[r];
+  wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = buf[to(r)];
+  wave_lds_sync();
+}
+
+// the lane's eight input samples of a symbol window (layout A: element 8 lane + r, read
+// from src[rev9(8 lane + r)]: for each r the lanes read 64 consecutive samples)
+__device__ __forceinline__ void wave_fft_load(const float *src, float (&xv)[8], int lane) {
+  asm volatile("" : "+v"(lane)); // (addresses formed here, not eight 64-bit ones held across the loop)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) xv[r] = src[rev9(8 * lane + r)];
+}
+
+__device__ void wave_fft_exact(const float (&xv)[8], double (&re)[8], double (&im)[8], const double2 *tw, int lane,
+                               double *buf) {
+  // (an opaque lane per call: every lane-derived address is invariant across symbols, and
+  // hoisted out of the symbol loop they held the registers that spilled the kernel)
+  asm volatile("" : "+v"(lane));
+#pragma unroll
+  for (int r = 0; r < 8; ++r) { re[r] = or_zero(xv[r]); im[r] = 0.0; }
+  fft_stage3(re, im, tw, 0, 8 * lane, 0);                        // A
+  const int eb = (lane & 7) | ((lane >> 3) << 6);
+  auto fa = [&](int r) { return 8 * lane + r; };
+  auto fb = [&](int r) { return eb | (r << 3); };
+  wave_permute(re, buf, fa, fb);
+  wave_permute(im, buf, fa, fb);
+  fft_stage3(re, im, tw, 3, eb, 3);                              // B
+  auto fc = [&](int r) { return lane | (r << 6); };
+  wave_permute(re, buf, fb, fc);
+  wave_permute(im, buf, fb, fc);
+  fft_stage3(re, im, tw, 6, lane, 6);                            // C
+}
+
 // Make this workgroup's global stores (plain or atomic) visible to its own later
 // plain loads: drain them to L2, barrier, then drop this CU's L1 copies.
 __device__ __forceinline__ void wg_global_sync() {
@@ -857,68 +933,105 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
                        (int64_t)nbits <= w.soft_stride)
                           ? w.soft + (int64_t)blockIdx.x * w.soft_stride
                           : nullptr;
-    for (int s = 0; s < M; ++s) {
+    // Data symbols s = wave, wave + 4, ...: one wave per symbol, the four waves on four
+    // symbols at once (a workgroup-wide transform with nine barriers per symbol kept three
+    // of the four waves waiting: a frame with 101 data symbols took ~0.8 ms). Per symbol:
+    // the reference's radix-2 transform in registers (wave_fft_exact, its transposes
+    // through the wave's LDS slot), the equaliser per bin on the lane that holds it, the
+    // bins of the band into the same slot, the pilot phase on lane 0 in the pilot list's
+    // order, the demap of the band on all lanes.
+    {
+      double2 *const eqb = (wave < 2 ? reinterpret_cast<double2 *>(sm.re) : reinterpret_cast<double2 *>(sm.er)) +
+                           (wave & 1) * kMaxBand;
+      static_assert(2 * kMaxBand * sizeof(double2) == 2 * kFft * sizeof(double), "two wave slots per array pair");
+      // the transform's twiddles in LDS (the fine stage's sample buffer is free now): read
+      // from global memory each of the nine stages waited out an L2 round trip
+      double2 *const twl = reinterpret_cast<double2 *>(sm.chunk);
+      static_assert(sizeof(sm.chunk) >= (kFft - 1) * sizeof(double2), "twiddles in the chunk area");
+      for (int i = tid; i < kFft - 1; i += XT) twl[i] = cfg.t.tw_exact[i];
       __syncthreads();
-      fft_exact(sig + data0 + s * SYM + CP, sm, cfg.t.tw_exact);
-      for (int k = tid; k < kFft; k += XT) {
-        double er = 0.0, ei = 0.0;
-        if (k >= cfg.sub_start && k <= cfg.sub_end) {
-          const double hr = sm.hr[k], hi = sm.hi[k];
-          const double hmag = hr * hr + hi * hi;
-          if (hmag > 1e-10) {
-            er = (sm.re[k] * hr + sm.im[k] * hi) / hmag;
-            ei = (sm.im[k] * hr - sm.re[k] * hi) / hmag;
-          } else {
-            er = sm.re[k]; ei = sm.im[k];
-          }
-          if (D && s == 0) {
+      float xv[8]; // the next symbol's samples, requested a symbol ahead
+      if (wave < M) wave_fft_load(sig + data0 + wave * SYM + CP, xv, lane);
+      for (int s = wave; s < M; s += XT / 64) {
+        double re[8], im[8];
+        // (the debug record's address opaque per symbol: its 32 per-slot store addresses,
+        // hoisted out of the loop, held 64 VGPRs across it)
+        amod_debug *Ds = D;
+        asm volatile("" : "+s"(Ds));
+        {
+          float cur[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) cur[r] = xv[r];
+          if (s + XT / 64 < M) wave_fft_load(sig + data0 + (s + XT / 64) * SYM + CP, xv, lane);
+          wave_fft_exact(cur, re, im, twl, lane, reinterpret_cast<double *>(eqb));
+        }
+        // equalise the lane's bins k = lane + 64 r of the band (demodulateOFDM 386-395)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int k = lane + 64 * r;
+          if (k >= cfg.sub_start && k <= cfg.sub_end) {
+            const double hr = sm.hr[k], hi = sm.hi[k];
+            const double hmag = hr * hr + hi * hi;
+            double er, ei;
+            if (hmag > 1e-10) {
+              er = (re[r] * hr + im[r] * hi) / hmag;
+              ei = (im[r] * hr - re[r] * hi) / hmag;
+            } else {
+              er = re[r]; ei = im[r];
+            }
             const int b = k - cfg.sub_start;
-            D->x_re[b] = sm.re[k]; D->x_im[b] = sm.im[k]; D->eq_re[b] = er; D->eq_im[b] = ei;
+            eqb[b] = make_double2(er, ei);
+            if (Ds && s == 0) { Ds->x_re[b] = re[r]; Ds->x_im[b] = im[r]; Ds->eq_re[b] = er; Ds->eq_im[b] = ei; }
           }
         }
-        sm.er[k] = er; sm.ei[k] = ei;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        double ps = 0.0;
-        int pc = 0;
-        for (int i = 0; i < cfg.npilots; ++i) {
-          const int p = cfg.pilots[i];
-          if (p >= cfg.sub_start && p <= cfg.sub_end && fabs(sm.er[p]) > 1e-6) { ps += sm.ei[p] / sm.er[p]; pc++; }
-        }
-        sm.phase = pc > 0 ? ps / (double)pc : 0.0;
-        if (D && s < AMOD_DBG_SYMS) D->phase[s] = sm.phase;
-      }
-      __syncthreads();
-      const double ph = sm.phase;
-      for (int b = tid; b < cfg.nband; b += XT) {
-        const int di = cfg.t.band_di[b];
-        if (di < 0) continue;
-        const int k = cfg.sub_start + b;
-        const double cr = sm.er[k] + sm.ei[k] * ph;
-        const double ci = sm.ei[k] - sm.er[k] * ph;
-        double md = __builtin_inf();
-        int mi = 0;
-        for (int i = 0; i < npts; ++i) {
-          const double dr = cr - cfg.t.points[i].x, dd = ci - cfg.t.points[i].y;
-          const double dist = dr * dr + dd * dd;
-          if (dist < md) { md = dist; mi = i; }
-        }
-        const int pos = (s * cfg.ndata + di) * cfg.bps;
-        if (sv) {
-          // weighted by |H|^2: the equaliser's division amplifies noise where the channel
-          // estimate is weak, so each bit counts in proportion to its channel power (MRC)
-          const double wgt = sm.hr[k] * sm.hr[k] + sm.hi[k] * sm.hi[k];
-          if (cfg.mod == AMOD_BPSK) {
-            sv[pos] = (float)(cr * wgt);
-          } else {
-            const double m = fmin(fabs(cr), fabs(ci)) * wgt;
-            sv[pos] = (float)(ci * wgt);
-            sv[pos + 1] = (float)(((cr < 0.0) != (ci < 0.0)) ? -m : m);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (the wave reads other lanes' bins below)
+        __builtin_amdgcn_wave_barrier();
+        double ph = 0.0;
+        if (lane == 0) {
+          double ps = 0.0;
+          int pc = 0;
+          for (int i = 0; i < cfg.npilots; ++i) {
+            const int p = cfg.pilots[i];
+            if (p >= cfg.sub_start && p <= cfg.sub_end) {
+              const double2 e = eqb[p - cfg.sub_start];
+              if (fabs(e.x) > 1e-6) { ps += e.y / e.x; pc++; }
+            }
           }
+          ph = pc > 0 ? ps / (double)pc : 0.0;
+          if (Ds && s < AMOD_DBG_SYMS) Ds->phase[s] = ph;
         }
-        const uint32_t val = (uint32_t)mi << (32 - cfg.bps - (pos & 31));
-        if (val) atomicOr(&bits[pos >> 5], val);
+        ph = readlane_f64(ph, 0);
+        for (int b = lane; b < cfg.nband; b += 64) {
+          const int di = cfg.t.band_di[b];
+          if (di < 0) continue;
+          const double2 e = eqb[b];
+          const double cr = e.x + e.y * ph;
+          const double ci = e.y - e.x * ph;
+          double md = __builtin_inf();
+          int mi = 0;
+          for (int i = 0; i < npts; ++i) {
+            const double dr = cr - cfg.t.points[i].x, dd = ci - cfg.t.points[i].y;
+            const double dist = dr * dr + dd * dd;
+            if (dist < md) { md = dist; mi = i; }
+          }
+          const int pos = (s * cfg.ndata + di) * cfg.bps;
+          if (sv) {
+            // weighted by |H|^2: the equaliser's division amplifies noise where the channel
+            // estimate is weak, so each bit counts in proportion to its channel power (MRC)
+            const int k = cfg.sub_start + b;
+            const double wgt = sm.hr[k] * sm.hr[k] + sm.hi[k] * sm.hi[k];
+            if (cfg.mod == AMOD_BPSK) {
+              sv[pos] = (float)(cr * wgt);
+            } else {
+              const double m = fmin(fabs(cr), fabs(ci)) * wgt;
+              sv[pos] = (float)(ci * wgt);
+              sv[pos + 1] = (float)(((cr < 0.0) != (ci < 0.0)) ? -m : m);
+            }
+          }
+          const uint32_t val = (uint32_t)mi << (32 - cfg.bps - (pos & 31));
+          if (val) atomicOr(&bits[pos >> 5], val);
+        }
+        __builtin_amdgcn_wave_barrier(); // (the slot is rewritten by the next symbol)
       }
     }
     wg_global_sync();
@@ -946,6 +1059,7 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     }
     finish_frame(v, nv, cfg, r, w.res + f, w.payload + (int64_t)f * w.stride, w.stride, sm.ru, nullptr, nv >> 3);
     __syncthreads();
+    XSTAMP(16); // (diagnostics: frame end)
   }
 }
 
