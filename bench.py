@@ -520,7 +520,7 @@ def measure(env: Env, wl: Workload, steps: int, warmup: int):
 def traffic_for(wl, kernel):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_traffic.py) when it was taken on this workload."""
-    for rnd in ("r05", "r04", "r03", "r02"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         tf = os.path.join(ROOT, "profiles", rnd, "traffic.json")
         if not os.path.exists(tf):
             continue
