@@ -167,6 +167,8 @@ struct FineTable {
   // one, a window clamped to the ring) fetches its range's metrics once, on first use,
   // instead of correlating every position on the host
   const double *dmetric = nullptr;
+  hipStream_t fetch_stream = nullptr; // (non-blocking: a null-stream copy waited for queued decodes)
+  double *fetch_bounce = nullptr;     // pinned, >= the longest range (device-to-pageable copies were slow)
   mutable std::mutex fmu;
   mutable std::unordered_map<size_t, std::vector<double>> fetched;
   const double *range_metrics(size_t r) const {
@@ -176,8 +178,12 @@ struct FineTable {
     auto it = fetched.find(r);
     if (it == fetched.end()) {
       std::vector<double> v((size_t)count[r]);
-      if (hipMemcpy(v.data(), dmetric + base[r], sizeof(double) * v.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      double *const dst = fetch_bounce ? fetch_bounce : v.data();
+      if (hipMemcpyAsync(dst, dmetric + base[r], sizeof(double) * v.size(), hipMemcpyDeviceToHost, fetch_stream) !=
+              hipSuccess ||
+          hipStreamSynchronize(fetch_stream) != hipSuccess)
         return nullptr;
+      if (fetch_bounce) std::memcpy(v.data(), fetch_bounce, sizeof(double) * v.size());
       it = fetched.emplace(r, std::move(v)).first;
     }
     return it->second.data();
@@ -717,6 +723,8 @@ struct StreamCache {
   size_t sp_gcap = 0;
   bool apow_ready = false;
   hipStream_t s2 = nullptr;                 // the cleaned stream's device-to-host copy
+  hipStream_t s_fetch = nullptr;            // sparse copy: granules fetched on demand
+  Pinned fetch_h, mfetch_h;                 // their pinned bounce buffers (granules, a range's metrics)
   hipStream_t s_up = nullptr;               // host samples: the upload, in pieces
   std::vector<hipEvent_t> up_ev;            // one per uploaded piece (the EMA of a piece waits on it)
   static constexpr int kPieces = 16;
@@ -724,6 +732,7 @@ struct StreamCache {
   ~StreamCache() {
     if (s2) { (void)hipStreamSynchronize(s2); (void)hipStreamDestroy(s2); }
     if (s3) { (void)hipStreamSynchronize(s3); (void)hipStreamDestroy(s3); }
+    if (s_fetch) { (void)hipStreamSynchronize(s_fetch); (void)hipStreamDestroy(s_fetch); }
     if (s_up) { (void)hipStreamSynchronize(s_up); (void)hipStreamDestroy(s_up); }
     for (auto e : up_ev) (void)hipEventDestroy(e);
     for (auto e : w_kern)
@@ -847,8 +856,21 @@ struct Prepass {
       std::lock_guard<std::mutex> lk(mu);
       if ((p = gptr[g].load(std::memory_order_acquire))) return p;
       const int64_t g1 = std::min(ng, g + 16);
-      (void)hipMemcpy(c->yh.as<float>() + g * kGran, c->d_y.as<float>() + g * kGran,
-                      sizeof(float) * (size_t)((g1 - g) * kGran), hipMemcpyDeviceToHost);
+      // on a non-blocking stream of its own, after the EMA: a plain hipMemcpy went on the
+      // null stream and waited for every decode batch queued on the context's stream
+      // (281 granules fetched this way took 7-9 ms of the host phase, AMOD_STREAM_DIAG)
+      // (and into pinned memory: a device-to-pageable copy went through HIP's staging path
+      // and still took ≈ 0.5 ms per 64 KB under the running decode)
+      if (!c->s_fetch) (void)hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking);
+      const size_t nb = sizeof(float) * (size_t)((g1 - g) * kGran);
+      if (c->fetch_h.alloc(sizeof(float) * 16 * kGran) == hipSuccess) {
+        (void)hipStreamWaitEvent(c->s_fetch, c->ema_done, 0);
+        (void)hipMemcpyAsync(c->fetch_h.p, c->d_y.as<float>() + g * kGran, nb, hipMemcpyDeviceToHost, c->s_fetch);
+        (void)hipStreamSynchronize(c->s_fetch);
+        std::memcpy(c->yh.as<float>() + g * kGran, c->fetch_h.p, nb);
+      } else {
+        (void)hipMemcpy(c->yh.as<float>() + g * kGran, c->d_y.as<float>() + g * kGran, nb, hipMemcpyDeviceToHost);
+      }
       fetch_us += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
       fallbacks += g1 - g;
       for (int64_t k = g + 1; k < g1; ++k)
@@ -1160,6 +1182,8 @@ struct Prepass {
       if (dev_metrics) {
         S_TRY(c->d_metric.alloc(sizeof(double) * (size_t)total));
         ft.dmetric = c->d_metric.as<double>();
+        if (!c->s_fetch) S_TRY(hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking));
+        ft.fetch_stream = c->s_fetch; // (the metrics are read after this prepass's final sync)
       }
       std::vector<double> p1d(p1.begin(), p1.end()); // (exact: k_fine's fma operand)
       S_TRY(c->d_pre1.alloc(sizeof(double) * p1.size()));
@@ -1167,6 +1191,9 @@ struct Prepass {
       S_TRY(hipMemcpyAsync(c->d_pre1.p, p1d.data(), sizeof(double) * p1d.size(), hipMemcpyHostToDevice, s));
       S_TRY(hipMemcpyAsync(c->d_base.p, ft.base.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, s));
       const int64_t maxc = *std::max_element(ft.count.begin(), ft.count.end());
+      ft.fetch_bounce = nullptr;
+      if (dev_metrics && c->mfetch_h.alloc(sizeof(double) * (size_t)maxc) == hipSuccess)
+        ft.fetch_bounce = c->mfetch_h.as<double>(); // (fetches hold FineTable's lock: one at a time)
       nbx = (int)((maxc + amod::kFinePositions - 1) / amod::kFinePositions);
       nfr = nr;
       S_TRY(c->d_barg.alloc(sizeof(double2) * (size_t)nr * nbx));
