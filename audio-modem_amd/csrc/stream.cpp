@@ -872,6 +872,7 @@ struct Prepass {
         (void)hipMemcpy(c->yh.as<float>() + g * kGran, c->d_y.as<float>() + g * kGran, nb, hipMemcpyDeviceToHost);
       }
       fetch_us += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (kn->stream_diag && fallbacks.load() < 400) fprintf(stderr, "[stream] fetch granule %lld\n", (long long)g);
       fallbacks += g1 - g;
       for (int64_t k = g + 1; k < g1; ++k)
         if (!gptr[k].load(std::memory_order_acquire) && cidx[k] < 0)
@@ -987,10 +988,13 @@ struct Prepass {
     const int64_t F = amod_estimate_frame_samples(cfg, maxp);
     const int64_t R = 3 * (int64_t)cfg->cp_len + cfg->symbol_len + 64; // refine radius + correlation
     const int64_t W = 2048;                                             // the metric's drop after the plateau
-    // the scan from local position p to the detection in the first hot region after it
+    // the scan from local position p to the detection in the first hot region after it,
+    // and through that region (the detection, its 0.7 drop and refinement read there: with
+    // the GPU gap scans nothing else marks it, and every speculative segment's first scan
+    // fetched its region on demand, AMOD_STREAM_DIAG)
     auto scan_from = [&](int64_t p) {
       auto it = std::lower_bound(reg.begin(), reg.end(), std::make_pair(p, (int64_t)0));
-      mark(p - 1024, it == reg.end() ? p + F + W : it->first);
+      mark(p - 1024, it == reg.end() ? p + F + W : it->second + R + W);
     };
     for (size_t k = 0; k < reg.size(); ++k) {
       if (gap_launched) { // the scans come from the GPU: the refinement window only (and with
