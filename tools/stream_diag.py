@@ -14,7 +14,9 @@ def main():
     import bench
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 32000
     env = bench.Env()
-    bench.stream_leg(env, 2000)  # warm-up run (tables, kernels, pinned buffers)
+    # warm-up run (tables, kernels, pinned buffers): 2000 chunks, or `same` = n chunks (the
+    # bench's own warm-up: every buffer and the assembler arena at their final size)
+    bench.stream_leg(env, n if len(sys.argv) > 2 and sys.argv[2] == "same" else 2000)
     os.environ["AMOD_STREAM_DIAG"] = "1"
     r = bench.stream_leg(env, n)
     print(json.dumps(r, indent=1))
