@@ -934,12 +934,16 @@ def stream_leg(env: Env, nchunks=2000, chunk=2048):
     del sig
     asm = amodem.ChunkAssembler()
     # warm-up: one whole call (tables, kernels, the context's grow-only buffers: a receiver
-    # serving recordings keeps its context), then the timed call
-    dm.stream_receive(cfg, x, amodem.ChunkAssembler())
+    # serving recordings keeps its context, and each finished assembler hands its file
+    # arena to the next), then the timed calls
+    warm = amodem.ChunkAssembler()
+    dm.stream_receive(cfg, x, warm)
+    warm.close()
     t0 = time.perf_counter()
     frames, _, st = dm.stream_receive(cfg, x, asm)
     t = time.perf_counter() - t0
     ok = asm.is_complete() and asm.assemble_file() == data
+    asm.close()  # (its file arena goes back to the process's pool for the next receiver)
     # the same stream already resident in HBM (amod_stream_receive_device)
     dx = torch.from_numpy(x).to(torch.device("cuda", device))
     torch.cuda.synchronize()
