@@ -360,45 +360,77 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
       // at most sum|x| in magnitude; when sum|x| < 2^(emin + 53) no partial sum rounds, in
       // any order, so the parallel sum is bit-equal to the sequential one. Otherwise (or
       // with non-finite samples) the sum runs sequentially.
-      // (one pass: the parallel sum and its certificate, and the extremes, from which
-      // the peak below follows without a pass of its own)
-      double ps = 0.0, pa = 0.0;
-      int emin = 1 << 20, nonfin = 0;
-      float xmn = INFINITY, xmx = -INFINITY;
-      stream4(xr, N, [&](int, float x) {
-        ps += (double)x;
-        pa += fabs((double)x);
-        xmn = fminf(xmn, x);
-        xmx = fmaxf(xmx, x);
-        const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
-        if (e == 0xFFu) nonfin = 1;
-        else if (x != 0.0f) emin = min(emin, e == 0 ? -149 : (int)e - 150);
-      });
-      for (int o = 32; o > 0; o >>= 1) {
-        ps += __shfl_xor(ps, o, 64);
-        pa += __shfl_xor(pa, o, 64);
-        emin = min(emin, __shfl_xor(emin, o, 64));
-        nonfin |= __shfl_xor(nonfin, o, 64);
-        xmn = fminf(xmn, __shfl_xor(xmn, o, 64));
-        xmx = fmaxf(xmx, __shfl_xor(xmx, o, 64));
+      // One pass, one wave per G-sample segment (lanes on consecutive samples): each
+      // segment's sum, sum|x| and smallest sample ulp (the certificate of the sequential
+      // chain below), and the frame's extremes; the frame's parallel sum and its certificate
+      // then come from the segment table (round 6: a second pass re-read the frame for the
+      // segment sums, ≈ 90 K cycles per listed C5 frame).
+      constexpr int SEGCAP = SCH, kSegG = 1024;
+      double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_e = sm.sc + 2 * SEGCAP;
+      const int G = kSegG * max(1, (N + kSegG * SEGCAP - 1) / (kSegG * SEGCAP));
+      const int nseg = (N + G - 1) / G;
+      {
+        int nonfin = 0;
+        float xmn = INFINITY, xmx = -INFINITY;
+        for (int sg = wave; sg < nseg; sg += XT / 64) {
+          const int b0 = sg * G, e1 = min(N, b0 + G);
+          double ss = 0.0, sa = 0.0;
+          int em = 1 << 20;
+          auto add = [&](float x) {
+            ss += (double)x;
+            sa += fabs((double)x);
+            xmn = fminf(xmn, x);
+            xmx = fmaxf(xmx, x);
+            const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
+            if (e == 0xFFu) nonfin = 1;
+            else if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
+          };
+          int i = b0 + lane;
+          for (; i + 7 * 64 < e1; i += 8 * 64) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = xr[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) add(v[u]);
+          }
+          for (; i < e1; i += 64) add(xr[i]);
+          // (the order of the adds is free: ss is used only where certified or non-finite,
+          // where every order gives the same result, and sa's rounding is within its slack)
+          ss = wave_scan_f64(ss);
+          sa = wave_scan_f64(sa);
+          em = wave_min_i32(em);
+          if (lane == 63) { seg_s[sg] = ss; seg_a[sg] = sa; seg_e[sg] = (double)em; }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          nonfin |= __shfl_xor(nonfin, o, 64);
+          xmn = fminf(xmn, __shfl_xor(xmn, o, 64));
+          xmx = fmaxf(xmx, __shfl_xor(xmx, o, 64));
+        }
+        if (lane == 0) { sm.ri[XT / 64 + wave] = nonfin; sm.rf[wave] = xmn; sm.ru[wave] = __float_as_uint(xmx); }
       }
-      if (lane == 0) { sm.rd[wave] = ps; sm.ri[wave] = emin; sm.ri[XT / 64 + wave] = nonfin; }
-      if (lane == 0) { sm.er[wave] = pa; sm.rf[wave] = xmn; sm.ei[wave] = (double)xmx; }
       __syncthreads();
       bool exact_par = true;
-      if (tid == 0) {
+      if (wave == 0) { // the frame's sums over the segment table (any order: see below)
         double S = 0.0, PA = 0.0;
-        int EM = 1 << 20, NF = 0;
-        float MN = INFINITY, MX = -INFINITY;
-        for (int i = 0; i < XT / 64; ++i) {
-          S += sm.rd[i]; PA += sm.er[i]; EM = min(EM, sm.ri[i]); NF |= sm.ri[XT / 64 + i];
-          MN = fminf(MN, sm.rf[i]); MX = fmaxf(MX, (float)sm.ei[i]);
+        int EM = 1 << 20;
+        for (int sg = lane; sg < nseg; sg += 64) { S += seg_s[sg]; PA += seg_a[sg]; EM = min(EM, (int)seg_e[sg]); }
+        S = wave_scan_f64(S);
+        PA = wave_scan_f64(PA);
+        EM = wave_min_i32(EM);
+        if (lane == 63) {
+          int NF = 0;
+          float MN = INFINITY, MX = -INFINITY;
+          for (int i = 0; i < XT / 64; ++i) {
+            NF |= sm.ri[XT / 64 + i];
+            MN = fminf(MN, sm.rf[i]); MX = fmaxf(MX, __uint_as_float(sm.ru[i]));
+          }
+          sm.xmn = MN; sm.xmx = MX; sm.nonfin = NF;
+          // non-finite samples: NaN, or +-Inf, whatever the order (finite sums stay finite);
+          // (sum|x| in fp64 over N terms: relative error below N 2^-53 < 2^-40)
+          exact_par = NF || EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53);
+          sm.mean = S / (double)N;
+          sm.status = exact_par;
         }
-        sm.xmn = MN; sm.xmx = MX; sm.nonfin = NF;
-        // non-finite samples: NaN, or +-Inf, whatever the order (finite sums stay finite)
-        exact_par = NF || EM >= (1 << 19) || PA * (1.0 + 0x1p-40) < ldexp(1.0, EM + 53);
-        sm.mean = S / (double)N;
-        sm.status = exact_par;
       }
       __syncthreads();
       exact_par = sm.status != 0;
@@ -427,39 +459,7 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
         // frame at 7 dB took 13 M cycles). A piece's Q are exact when the segment's
         // sum|x| < 2^(em + 53) for the piece's own em; a piece failing that is added sample
         // by sample.
-        constexpr int SEGCAP = SCH, kSegG = 1024;
-        double *const seg_s = sm.sc, *const seg_a = sm.sc + SEGCAP, *const seg_e = sm.sc + 2 * SEGCAP;
-        const int G = kSegG * max(1, (N + kSegG * SEGCAP - 1) / (kSegG * SEGCAP));
-        const int nseg = (N + G - 1) / G;
-        // (one wave per segment, lanes on consecutive samples: a thread per segment read
-        // 64 far-apart lines per load instruction and took ~250 K cycles a C5 frame. The
-        // order of the adds is free: ss is used only when certified, where every order is
-        // exact, and sa's rounding is within the slack below)
-        for (int sg = wave; sg < nseg; sg += XT / 64) {
-          const int b0 = sg * G, e1 = min(N, b0 + G);
-          double ss = 0.0, sa = 0.0;
-          int em = 1 << 20;
-          auto add = [&](float x) {
-            ss += (double)x;
-            sa += fabs((double)x);
-            const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
-            if (x != 0.0f) em = min(em, e == 0 ? -149 : (int)e - 150);
-          };
-          int i = b0 + lane;
-          for (; i + 7 * 64 < e1; i += 8 * 64) {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = xr[i + 64 * u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) add(v[u]);
-          }
-          for (; i < e1; i += 64) add(xr[i]);
-          ss = wave_scan_f64(ss);
-          sa = wave_scan_f64(sa);
-          em = wave_min_i32(em);
-          if (lane == 63) { seg_s[sg] = ss; seg_a[sg] = sa; seg_e[sg] = (double)em; }
-        }
-        __syncthreads();
+        // (the segment table is pass 1's)
         constexpr int PW = 256, NW = XT / 64;
         double *const qb = reinterpret_cast<double *>(sm.chunk); // one piece per wave
         uint32_t *const qok = sm.ru;
