@@ -35,11 +35,11 @@ def main():
         dm.reserve(cfg, F, int(lens.max()))
         run = lambda: dm.decode_device(cfg, L.MODE_RECEIVED, xs.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), F,
                                        res.data_ptr(), pay.data_ptr(), stride)
-        for _ in range(3):
+        for _ in range(int(os.environ.get("WARM", "3"))):
             run()
         dm.synchronize()
         lib.amod_set_profiling(dm.ctx, 1)
-        for _ in range(10):
+        for _ in range(int(os.environ.get("REPS", "10"))):
             run()
         ms, n = (C.c_double * 3)(), C.c_int64()
         lib.amod_kernel_breakdown(dm.ctx, ms, C.byref(n))
