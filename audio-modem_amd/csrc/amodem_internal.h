@@ -450,6 +450,26 @@ __device__ inline int soft_vote(const float *sv, int nbits, int rep, uint32_t *v
 __device__ inline int block_vote(const uint32_t *bits, int nbits, int rep, uint32_t *voted) {
   const int nv = nbits / rep;
   const int nw = (nv + 31) >> 5;
+  if (rep == 3) {
+    // voted word w is raw bits [96 w, 96 w + 96) = raw words 3w .. 3w + 2 (MSB-first): the
+    // majority of bits k, k + 1, k + 2 lands at bit k of maj(p, p << 1, p << 2) (shifts
+    // across the three words), and bits k = 0, 3, ..., 93 are gathered into the word.
+    // (The raw words read past nbits are zero: the callers clear nwords + 8.)
+    for (int w = ltid(); w < nw; w += blockDim.x) {
+      const uint32_t p0 = bits[3 * w], p1 = bits[3 * w + 1], p2 = bits[3 * w + 2];
+      const uint32_t q0 = (p0 << 1) | (p1 >> 31), q1 = (p1 << 1) | (p2 >> 31), q2 = p2 << 1;
+      const uint32_t r0 = (p0 << 2) | (p1 >> 30), r1 = (p1 << 2) | (p2 >> 30), r2 = p2 << 2;
+      const uint32_t m[3] = {(p0 & q0) | (p0 & r0) | (q0 & r0), (p1 & q1) | (p1 & r1) | (q1 & r1),
+                             (p2 & q2) | (p2 & r2) | (q2 & r2)};
+      uint32_t word = 0;
+#pragma unroll
+      for (int o = 0; o < 32; ++o) word |= ((m[(3 * o) >> 5] >> (31 - ((3 * o) & 31))) & 1u) << (31 - o);
+      const int left = nv - 32 * w; // voted bits in this word (the rest stay 0)
+      if (left < 32) word &= ~(0xFFFFFFFFu >> left);
+      voted[w] = word;
+    }
+    return nv;
+  }
   const int thr = (rep + 1) >> 1; // sum >= rep/2  <=>  sum >= ceil(rep/2)
   for (int w = ltid(); w < nw; w += blockDim.x) {
     uint32_t word = 0;

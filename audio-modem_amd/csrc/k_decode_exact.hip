@@ -192,11 +192,14 @@ __device__ void wave_fft_exact(const float (&xv)[8], double (&re)[8], double (&i
 }
 
 // Make this workgroup's global stores (plain or atomic) visible to its own later
-// plain loads: drain them to L2, barrier, then drop this CU's L1 copies.
+// plain loads. Workgroup scope is enough: every wave of the workgroup runs on one CU and
+// shares its L1 (the LLVM AMDGPU memory model for gfx942/gfx950 without threadgroup
+// split). Agent scope compiled to buffer_wbl2 sc1 + buffer_inv sc1 at each call: a write-
+// back and invalidate of the XCD's L2 under every k_demod and exact workgroup sharing it.
 __device__ __forceinline__ void wg_global_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // fn(i, p[i]) for this thread's strided indices i = tid + k XT < N, in ascending order,
@@ -923,6 +926,16 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     const int M = max(0, N - data0) / SYM;
     const int nbits = M * cfg.ndata * cfg.bps;
     const int nwords = (nbits + 31) >> 5;
+    // The bit stream lives in LDS past the transform's twiddles when it fits (chunk windows
+    // and short frames): the demap's ORs, the vote, the parse, the CRC and the payload rows
+    // then read and write LDS. In the slot's global words, the vote and frame end waited out
+    // a cache round trip per word or byte read (~175 K cycles per 101-symbol chunk window).
+    // The voted stream goes to the transform arrays, free once every symbol is demapped.
+    constexpr int kTwBytes = (((kFft - 1) * (int)sizeof(double2)) + 15) & ~15;
+    constexpr int kLdsStreamWords = ((int)sizeof(sm.chunk) - kTwBytes) / 4;
+    static_assert(kLdsStreamWords > 0, "room for a stream past the twiddles");
+    const bool lds_stream = nwords + 8 <= kLdsStreamWords;
+    if (lds_stream) bits = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(sm.chunk) + kTwBytes);
     for (int i = tid; i < nwords + 8; i += XT) bits[i] = 0u;
     wg_global_sync();
     const int npts = cfg.mod == AMOD_BPSK ? 2 : (cfg.mod == AMOD_QPSK ? 4 : 16);
@@ -1041,11 +1054,13 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     const uint32_t *v = bits;
     int nv = nbits;
     if (cfg.rep > 1) {
-      uint32_t *voted = bits + ((nwords + 3) & ~3);
+      uint32_t *voted = lds_stream ? reinterpret_cast<uint32_t *>(sm.re) : bits + ((nwords + 3) & ~3);
+      static_assert(6 * sizeof(sm.re) / 4 >= sizeof(sm.chunk) / 4, "a voted stream no longer than the raw one fits");
       nv = sv ? soft_vote(sv, nbits, cfg.rep, voted) : block_vote(bits, nbits, cfg.rep, voted);
       wg_global_sync();
       v = voted;
     }
+    XSTAMP(17); // (diagnostics: voted)
     if (loop) {  // analyzeLoopback parses nothing: the raw decoded bytes go back to the caller
       const int nbytes = nv >> 3, nw = (nbytes + 3) >> 2, cap_w = (int)(w.stride >> 2);
       uint32_t *dst = reinterpret_cast<uint32_t *>(w.payload + (int64_t)f * w.stride);

@@ -2,7 +2,7 @@
 """Diagnostics: where the exact kernel's time goes on chunk windows it demodulates
 (AMOD_STAMPS: s_memtime marks per listed frame): C5 acoustic BPSK rep3 256 B chunk windows
 at noise divisor 1.5 (the soft chunk leg's batch), hard vote (DEMAP-listed frames).
-8 -> 11 frame start, 11 -> 12 channel estimate + data symbols, 12 -> 16 vote + frame end."""
+8 -> 11 frame start, 11 -> 12 channel estimate + data symbols, 12 -> 17 vote, 17 -> 16 frame end."""
 import os
 import sys
 
@@ -27,7 +27,8 @@ def main():
     st = st[:n].reshape(-1, 32).astype(np.int64)
     listed = np.nonzero(rec["flags"] & env.L.FLAG_EXACT)[0]
     print(f"{wl.F} windows, {len(listed)} listed; symbols per window {(int(wl.dlens[0]) - 3 * wl.cfg.symbol_len) // wl.cfg.symbol_len}")
-    for a, b, what in ((8, 11, "start"), (11, 12, "CE + symbols"), (12, 16, "vote + end"), (8, 16, "whole")):
+    for a, b, what in ((8, 11, "start"), (11, 12, "CE + symbols"), (12, 17, "vote"), (17, 16, "parse + CRC + rows"),
+                       (12, 16, "vote + end"), (8, 16, "whole")):
         ok = (st[:, a] != 0) & (st[:, b] != 0) & (st[:, b] >= st[:, a])
         if ok.any():
             d = st[ok, b] - st[ok, a]
