@@ -1000,20 +1000,28 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (the wave reads other lanes' bins below)
         __builtin_amdgcn_wave_barrier();
         double ph = 0.0;
-        if (lane == 0) {
-          double ps = 0.0;
-          int pc = 0;
-          for (int i = 0; i < cfg.npilots; ++i) {
-            const int p = cfg.pilots[i];
+        {
+          // lane i forms pilot i's quotient eqIm / eqRe (the divisions at once, each the
+          // same IEEE operation; npilots <= AMOD_MAX_PILOTS = 32), then every lane adds the
+          // used ones in the pilot list's order (modem.js:398-405): the same sum, one
+          // dependent add per pilot
+          static_assert(AMOD_MAX_PILOTS <= 64, "one lane per pilot");
+          double q = 0.0;
+          bool used = false;
+          if (lane < cfg.npilots) {
+            const int p = cfg.pilots[lane];
             if (p >= cfg.sub_start && p <= cfg.sub_end) {
               const double2 e = eqb[p - cfg.sub_start];
-              if (fabs(e.x) > 1e-6) { ps += e.y / e.x; pc++; }
+              if (fabs(e.x) > 1e-6) { q = e.y / e.x; used = true; }
             }
           }
+          uint64_t um = __ballot(used);
+          const int pc = __popcll(um);
+          double ps = 0.0;
+          for (; um; um &= um - 1) ps += readlane_f64(q, __builtin_ctzll(um));
           ph = pc > 0 ? ps / (double)pc : 0.0;
-          if (Ds && s < AMOD_DBG_SYMS) Ds->phase[s] = ph;
         }
-        ph = readlane_f64(ph, 0);
+        if (Ds && lane == 0 && s < AMOD_DBG_SYMS) Ds->phase[s] = ph;
         for (int b = lane; b < cfg.nband; b += 64) {
           const int di = cfg.t.band_di[b];
           if (di < 0) continue;
