@@ -932,7 +932,12 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
     // a cache round trip per word or byte read (~175 K cycles per 101-symbol chunk window).
     // The voted stream goes to the transform arrays, free once every symbol is demapped.
     constexpr int kTwBytes = (((kFft - 1) * (int)sizeof(double2)) + 15) & ~15;
-    constexpr int kLdsStreamWords = ((int)sizeof(sm.chunk) - kTwBytes) / 4;
+    // the demap's tables at the chunk area's end: 16 constellation points, then the band's
+    // data indices (read per slot and symbol, from global memory they were a cache round
+    // trip each inside the symbol loop)
+    constexpr int kTabBytes = 16 * (int)sizeof(double2) + kMaxBand * (int)sizeof(int16_t);
+    constexpr int kTabOff = ((int)sizeof(sm.chunk) - kTabBytes) & ~15;
+    constexpr int kLdsStreamWords = (kTabOff - kTwBytes) / 4;
     static_assert(kLdsStreamWords > 0, "room for a stream past the twiddles");
     const bool lds_stream = nwords + 8 <= kLdsStreamWords;
     if (lds_stream) bits = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(sm.chunk) + kTwBytes);
@@ -962,6 +967,10 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
       double2 *const twl = reinterpret_cast<double2 *>(sm.chunk);
       static_assert(sizeof(sm.chunk) >= (kFft - 1) * sizeof(double2), "twiddles in the chunk area");
       for (int i = tid; i < kFft - 1; i += XT) twl[i] = cfg.t.tw_exact[i];
+      double2 *const ptl = reinterpret_cast<double2 *>(reinterpret_cast<char *>(sm.chunk) + kTabOff);
+      int16_t *const dil = reinterpret_cast<int16_t *>(ptl + 16);
+      if (tid < 16) ptl[tid] = tid < npts ? cfg.t.points[tid] : make_double2(0.0, 0.0);
+      for (int b = tid; b < cfg.nband; b += XT) dil[b] = cfg.t.band_di[b];
       __syncthreads();
       float xv[8]; // the next symbol's samples, requested a symbol ahead
       if (wave < M) wave_fft_load(sig + data0 + wave * SYM + CP, xv, lane);
@@ -1023,7 +1032,7 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
         }
         if (Ds && lane == 0 && s < AMOD_DBG_SYMS) Ds->phase[s] = ph;
         for (int b = lane; b < cfg.nband; b += 64) {
-          const int di = cfg.t.band_di[b];
+          const int di = dil[b];
           if (di < 0) continue;
           const double2 e = eqb[b];
           const double cr = e.x + e.y * ph;
@@ -1031,7 +1040,8 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
           double md = __builtin_inf();
           int mi = 0;
           for (int i = 0; i < npts; ++i) {
-            const double dr = cr - cfg.t.points[i].x, dd = ci - cfg.t.points[i].y;
+            const double2 pt = ptl[i];
+            const double dr = cr - pt.x, dd = ci - pt.y;
             const double dist = dr * dr + dd * dd;
             if (dist < md) { md = dist; mi = i; }
           }
