@@ -1060,7 +1060,10 @@ __device__ __forceinline__ void exact_body(const DevCfg &cfg, const DevWork &w) 
             }
           }
           const uint32_t val = (uint32_t)mi << (32 - cfg.bps - (pos & 31));
-          if (val) atomicOr(&bits[pos >> 5], val);
+          if (val) { // (an LDS-typed pointer: ds_or, not the flat atomic a generic one takes)
+            if (lds_stream) atomicOr(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(sm.chunk) + kTwBytes) + (pos >> 5), val);
+            else atomicOr(&bits[pos >> 5], val);
+          }
         }
         __builtin_amdgcn_wave_barrier(); // (the slot is rewritten by the next symbol)
       }
