@@ -25,7 +25,7 @@ constexpr int CH = 3072;    // sample chunk staged in LDS (XSmem <= 40 KB: four 
 
 constexpr int SCH = kFft * 2; // Schmidl-Cox positions per chunk (3 x SCH doubles overlay the FFT arrays)
 #ifndef AMOD_SC_CQ
-#define AMOD_SC_CQ 4
+#define AMOD_SC_CQ 8
 #endif
 
 struct alignas(16) XSmem { // (static_assert below: four per CU fit the 160 KB of LDS)
