@@ -192,14 +192,17 @@ __device__ void wave_fft_exact(const float (&xv)[8], double (&re)[8], double (&i
 }
 
 // Make this workgroup's global stores (plain or atomic) visible to its own later
-// plain loads. Workgroup scope is enough: every wave of the workgroup runs on one CU and
-// shares its L1 (the LLVM AMDGPU memory model for gfx942/gfx950 without threadgroup
-// split). Agent scope compiled to buffer_wbl2 sc1 + buffer_inv sc1 at each call: a write-
-// back and invalidate of the XCD's L2 under every k_demod and exact workgroup sharing it.
+// plain loads. Every wave of the workgroup runs on one CU and shares its L1, so the
+// stores need only workgroup scope (the LLVM AMDGPU memory model for gfx942/gfx950
+// without threadgroup split); the atomics (the global bit stream's ORs) are performed in
+// L2, so the CU's L1 is dropped after the barrier (buffer_inv sc0: this CU's vector L1
+// only), in case a line of the slot is still there from an earlier frame's reads. Agent
+// scope compiled to buffer_wbl2 sc1 + buffer_inv sc1 at each call: a write-back and
+// invalidate of the XCD's L2 under every k_demod and exact workgroup sharing it.
 __device__ __forceinline__ void wg_global_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  asm volatile("buffer_inv sc0" ::: "memory");
 }
 
 // fn(i, p[i]) for this thread's strided indices i = tid + k XT < N, in ascending order,
